@@ -1,0 +1,158 @@
+#!/usr/bin/env python
+"""
+Flagship benchmark: one k-means Lloyd iteration (assign + update + all-reduce) on split=0 float32
+data, the BASELINE.json config "k-means k=1024 on 1e8 x 64 float32 split=0, 8 x MI355X".
+
+Weak scaling: every GPU holds ``--n-per-gpu`` points (default 1.25e7, so 8 GPUs = 1e8 points).
+Data are synthetic (Threefry normal samples generated on the device, random-init centroids).
+``value`` is the whole-job GFLOP/s of the distance computation (2*n*k*f per iteration, the
+quantity the reference's benchmark scales with); ``ms_per_step`` the wall time of one iteration.
+
+Run: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Secondary workloads: ``--workload cdist`` (distance_matrix, streamed) and ``--workload moments``
+(statistical_moments mean/var of 1e9 float32).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="kmeans", choices=["kmeans", "cdist", "moments"])
+    p.add_argument("--n-per-gpu", type=int, default=12_500_000)
+    p.add_argument("--k", type=int, default=1024)
+    p.add_argument("--f", type=int, default=64)
+    p.add_argument("--with-reference", action="store_true",
+                   help="also time a reference-style (heat 1.1 algorithm) iteration on torch-ROCm")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import heat_amd as ht
+    from heat_amd.core.communication import MPI_WORLD
+
+    comm = MPI_WORLD
+    if torch.cuda.is_available():
+        ht.use_device("gpu")
+    dev = ht.get_device()
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        comm.Barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    n_gpus = comm.size
+    extra = {}
+    if args.workload == "kmeans":
+        n, k, f = args.n_per_gpu * n_gpus, args.k, args.f
+        ht.random.seed(1234)
+        x = ht.random.randn(n, f, split=0, device=dev)
+        km = ht.cluster.KMeans(n_clusters=k, init="random", max_iter=1, tol=None, random_state=42)
+        for _ in range(args.warmup):
+            km.step(x)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            km.step(x)
+        sync()
+        dt = time.perf_counter() - t0
+        # slowest rank defines the step
+        dt = comm.allreduce(dt, ht.MPI.MAX) if comm.size > 1 else dt
+        ms = dt / args.steps * 1e3
+        flops = 2.0 * n * k * f
+        value = flops / (ms * 1e-3) / 1e9
+        metric = "kmeans_iter_gflops"
+        unit = "GFLOP/s"
+        cfg = {"model": "kmeans k={} f={} float32 split=0 (assign+update+allreduce)".format(k, f),
+               "global_batch": n, "seq_len": f, "parallelism": "dp{}".format(n_gpus), "k": k,
+               "n_per_gpu": args.n_per_gpu}
+        extra["iter_ms"] = ms
+        extra["tflops_per_gpu"] = value / n_gpus / 1e3
+        if args.with_reference:
+            extra["reference_impl_ms"] = reference_iteration(x, km, k)
+            extra["speedup_vs_reference_impl"] = extra["reference_impl_ms"] / ms
+    elif args.workload == "cdist":
+        n, f = args.n_per_gpu * n_gpus, args.f
+        x = ht.random.rand(n, f, split=0, device=dev)
+        for _ in range(args.warmup):
+            d = ht.spatial.cdist(x, x)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            d = ht.spatial.cdist(x, x)
+        sync()
+        dt = time.perf_counter() - t0
+        dt = comm.allreduce(dt, ht.MPI.MAX) if comm.size > 1 else dt
+        ms = dt / args.steps * 1e3
+        value = 2.0 * n * n * f / (ms * 1e-3) / 1e9
+        metric, unit = "cdist_gflops", "GFLOP/s"
+        cfg = {"model": "cdist n={} f={} float32 split=0".format(n, f), "global_batch": n, "seq_len": f,
+               "parallelism": "dp{}".format(n_gpus)}
+        extra["output_GB_per_s"] = n * n * 4 / (ms * 1e-3) / 1e9
+    else:
+        n = args.n_per_gpu * n_gpus
+        x = ht.random.rand(n, split=0, device=dev)
+        for _ in range(args.warmup):
+            ht.mean(x), ht.var(x)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            m = ht.mean(x)
+            v = ht.var(x)
+        sync()
+        dt = time.perf_counter() - t0
+        dt = comm.allreduce(dt, ht.MPI.MAX) if comm.size > 1 else dt
+        ms = dt / args.steps * 1e3
+        value = 2 * n * 4 / (ms * 1e-3) / 1e9
+        metric, unit = "moments_GB_per_s", "GB/s"
+        cfg = {"model": "mean+var float32 split=0", "global_batch": n, "seq_len": 1,
+               "parallelism": "dp{}".format(n_gpus)}
+    if comm.rank == 0:
+        out = {"metric": metric, "value": value, "unit": unit, "n_gpus": n_gpus, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "fp32", "data": "synthetic (device Threefry normal samples)",
+               "config": cfg, "extra": extra}
+        print(json.dumps(out), flush=True)
+
+
+def reference_iteration(x, km, k):
+    """Time ONE iteration of the reference's algorithm (heat 1.1 kmeans.py:73-100 + _kcluster
+    assign) expressed with torch on the same data: cdist by quadratic expansion (n x k matrix),
+    argmin, then k masked passes for the update + one all-reduce per cluster."""
+    import heat_amd as ht
+
+    X = x.larray
+    C = km.cluster_centers_.larray
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d2 = torch.clamp((X * X).sum(1, keepdim=True) + (C * C).sum(1) - 2 * X @ C.T, min=0).sqrt()
+    lab = d2.argmin(1, keepdim=True)
+    del d2
+    newc = torch.empty_like(C)
+    for i in range(k):
+        sel = (lab == i).to(X.dtype)
+        s = (X * sel).sum(0)
+        cnt = sel.sum().clamp(min=1)
+        if x.comm.size > 1:
+            x.comm.Allreduce(ht.MPI.IN_PLACE, s, ht.MPI.SUM)
+            x.comm.Allreduce(ht.MPI.IN_PLACE, cnt, ht.MPI.SUM)
+        newc[i] = s / cnt
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3
+
+
+if __name__ == "__main__":
+    main()

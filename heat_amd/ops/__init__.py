@@ -1,0 +1,115 @@
+"""
+Native CDNA4 (gfx950) kernels and their Python entry points.
+
+``heat_amd.ops`` is the only place where device compute leaves PyTorch: the hot paths of the
+framework (k-means assign/update, pairwise distances, statistical moments, Threefry RNG, ...)
+are hand-written HIP kernels in ``csrc/`` compiled into ``_lib/libheat_amd_kernels.so``.
+
+Dispatch rule: a CUDA (= HIP) tensor ALWAYS goes to the native kernel; if the library cannot be
+loaded on a GPU process this raises (set ``HEAT_AMD_ALLOW_FALLBACK=1`` to permit the PyTorch
+reference path instead). Host tensors use the PyTorch reference implementation, which is also
+the numerics oracle in the tests.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from . import _build
+
+_lib = None
+_lock = threading.Lock()
+_load_error = None
+
+c_void_p, c_int, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+
+_SIGNATURES = {
+    "ha_km_workspace_floats": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "ha_km_assign": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_int64, c_void_p, c_void_p,
+                             c_void_p, c_void_p]),
+    "ha_km_update_fc": (c_int, [c_int, c_int]),
+    "ha_km_update": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                             c_void_p]),
+    "ha_moments_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
+    "ha_moments_cols": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
+}
+
+
+def _optional_signatures():
+    """Signatures of kernels added in later files (registered if the symbol exists)."""
+    from . import signatures
+
+    return signatures.SIGNATURES
+
+
+def lib():
+    """Load (building first if the sources are newer) the native kernel library."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        try:
+            path = _build.LIBPATH
+            if _build.needs_build():
+                try:
+                    path = _build.build()
+                except Exception as e:  # no hipcc on this machine: use a prebuilt library if present
+                    if not os.path.exists(_build.LIBPATH):
+                        raise
+            handle = ctypes.CDLL(path)
+            sigs = dict(_SIGNATURES)
+            try:
+                sigs.update(_optional_signatures())
+            except ImportError:
+                pass
+            for name, (res, args) in sigs.items():
+                if hasattr(handle, name):
+                    fn = getattr(handle, name)
+                    fn.restype = res
+                    fn.argtypes = args
+            _lib = handle
+        except Exception as e:
+            _load_error = e
+            raise
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def allow_fallback() -> bool:
+    return os.environ.get("HEAT_AMD_ALLOW_FALLBACK", "0") == "1"
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True if ``t`` must be processed by the native kernels (device tensor). Raises if the
+    library is unavailable on a device tensor and fallback is not explicitly allowed."""
+    if not t.is_cuda:
+        return False
+    if available():
+        return True
+    if allow_fallback():
+        return False
+    raise RuntimeError("heat_amd native kernel library is not available for a device tensor: {}".format(_load_error))
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError("native kernel {} failed with status {}".format(name, rc))
+
+
+from .kernels import *  # noqa: E402,F401,F403

@@ -1,0 +1,71 @@
+"""
+Build the native CDNA4 kernel library in-tree:
+``hipcc --offload-arch=gfx950 -O3 -shared -fPIC heat_amd/ops/csrc/*.hip -> heat_amd/ops/_lib/libheat_amd_kernels.so``.
+
+The library exports a plain C ABI (``ha_*`` functions taking device pointers and a ``hipStream_t``)
+and is loaded with ctypes after torch, so it shares torch's HIP runtime (same SONAME
+``libamdhip64.so.7``) and runs on torch's current stream. No torch headers are compiled, so a
+full rebuild takes seconds and cross-compiles without a GPU.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+LIBNAME = "libheat_amd_kernels.so"
+LIBPATH = os.path.join(LIBDIR, LIBNAME)
+ARCH = os.environ.get("HEAT_AMD_ARCH", "gfx950")
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def headers():
+    return sorted(glob.glob(os.path.join(CSRC, "*.h")))
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found; the native kernels need ROCm's hipcc")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIBPATH):
+        return True
+    t = os.path.getmtime(LIBPATH)
+    return any(os.path.getmtime(s) > t for s in sources() + headers() + [__file__])
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile all kernels into one shared library (atomic replace). Returns the library path."""
+    if not force and not needs_build():
+        return LIBPATH
+    os.makedirs(LIBDIR, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(suffix=".so", dir=LIBDIR)
+    os.close(fd)
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-value",
+           "-Wno-unused-result", "-I" + CSRC] + sources() + ["-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    try:
+        subprocess.run(cmd, check=True, capture_output=not verbose)
+    except subprocess.CalledProcessError as e:
+        os.unlink(tmp)
+        msg = e.stderr.decode() if e.stderr else ""
+        raise RuntimeError("building the native kernels failed:\n" + msg) from e
+    os.replace(tmp, LIBPATH)
+    return LIBPATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,198 @@
+// Pairwise distances on CDNA4 (gfx950): the hot path of heat.spatial (reference
+// heat/spatial/distance.py: _euclidian 16 / _euclidian_fast 31 / _gaussian 66 / _manhattan 105).
+//
+// L2 family: one fp32-MFMA (v_mfma_f32_32x32x2_f32) GEMM tile of X.Y^T per 128x128 output block
+// with a fused epilogue  d2 = |x|^2 + |y|^2 - 2 x.y, clamp >= 0, then sqrt (euclidean), nothing
+// (squared) or exp(-d2 / (2 sigma^2)) (gaussian / rbf).  Row norms are computed while staging.
+// As in the k-means kernel the K dimension is permuted (half h of the wave owns features
+// h*16 + s of each 32-feature chunk), so operand fragments are contiguous 16-byte LDS reads.
+//
+// L1: VALU tile kernel (|x - y| has no matrix-core form), 64x64 outputs per workgroup, no
+// m x n x f intermediate (the reference's _manhattan_fast materialises one).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, KB = 32;   // output tile, features per LDS chunk
+constexpr int S4 = KB / 2 / 4;               // float4 groups per half per chunk (=4)
+
+enum { MODE_EUCLID = 0, MODE_SQEUCLID = 1, MODE_GAUSS = 2 };
+
+// LDS image of one 128-row operand chunk: [rb (4)][s4 (4)][lane (64)][4]
+__device__ __forceinline__ int frag_off(int rb, int s4, int lane) { return ((rb * S4 + s4) * 64 + lane) * 4; }
+
+__device__ __forceinline__ void stage(const float* __restrict__ src, int64_t nrows, int f, int64_t ld, int64_t row0,
+                                      int k0, float* __restrict__ dst, float* __restrict__ nrm, int tid) {
+  // 128 rows x 32 features = 1024 float4, 4 per thread
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int q = tid + 256 * it;        // float4 index in fragment order
+    const int lane = q & 63;
+    const int s4 = (q >> 6) & (S4 - 1);
+    const int rb = q >> 8;
+    const int j = lane & 31, h = lane >> 5;
+    const int64_t row = row0 + rb * 32 + j;
+    const int col = k0 + h * (KB / 2) + 4 * s4;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < nrows && col < f) v = *reinterpret_cast<const floatx4*>(src + row * ld + col);
+    *reinterpret_cast<floatx4*>(dst + frag_off(rb, s4, lane)) = v;
+    float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    // 8 float4 per row per chunk (2 halves x 4 groups): reduce into the row's norm
+    atomicAdd(&nrm[rb * 32 + j], ss);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void cdist_l2(const float* __restrict__ X, int64_t m, const float* __restrict__ Y,
+                                                  int64_t n, int f, int64_t ldx, int64_t ldy, float* __restrict__ C,
+                                                  int64_t ldc, int mode, float scale) {
+  __shared__ __attribute__((aligned(16))) float sx[BM * KB];
+  __shared__ __attribute__((aligned(16))) float sy[BN * KB];
+  __shared__ float xn[BM];
+  __shared__ float yn[BN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5;
+  // XCD-friendly order: consecutive workgroups walk along a row of tiles (they share X rows)
+  const int64_t tiles_n = (n + BN - 1) / BN;
+  const int64_t tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int64_t row0 = tm * BM, col0 = tn * BN;
+  const int wr = wave >> 1, wc = wave & 1;  // wave owns a 64x64 quadrant: row blocks 2wr..2wr+1
+  if (tid < BM) xn[tid] = 0.f;
+  if (tid >= 128 && tid < 128 + BN) yn[tid - 128] = 0.f;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (floatx16)(0.f);
+  __syncthreads();
+  for (int k0 = 0; k0 < f; k0 += KB) {
+    stage(X, m, f, ldx, row0, k0, sx, xn, tid);
+    stage(Y, n, f, ldy, col0, k0, sy, yn, tid);
+    __syncthreads();
+#pragma unroll
+    for (int s4 = 0; s4 < S4; ++s4) {
+      floatx4 a[2], b[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        a[u] = *reinterpret_cast<const floatx4*>(sx + frag_off(2 * wr + u, s4, lane));
+        b[u] = *reinterpret_cast<const floatx4*>(sy + frag_off(2 * wc + u, s4, lane));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][t], b[v][t], acc[u][v], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // epilogue: lane owns column j of each 32x32 block, rows (reg&3) + 8*(reg>>2) + 4*h
+  const int j = lane & 31;
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int cl = (2 * wc + v) * 32 + j;
+    const int64_t col = col0 + cl;
+    const float ynv = yn[cl];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (2 * wr + u) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t row = row0 + rl;
+        float d2 = fmaxf(fmaf(-2.f, acc[u][v][r], xn[rl] + ynv), 0.f);
+        float out;
+        if (mode == MODE_EUCLID) out = sqrtf(d2);
+        else if (mode == MODE_SQEUCLID) out = d2;
+        else out = __expf(-d2 * scale);
+        if (row < m && col < n) C[row * ldc + col] = out;
+      }
+    }
+  }
+}
+
+// L1 distance: VALU, 64x64 outputs per workgroup, 4x4 per thread, features staged through LDS
+constexpr int LB = 64, LK = 32;
+// OP 0: sum |x-y| ; OP 1: sqrt(sum (x-y)^2) ; OP 2: sum (x-y)^2 ; OP 3: exp(-scale * sum (x-y)^2)
+// (the exact, cancellation-free L2 family used when quadratic_expansion=False)
+template <int OP>
+__global__ __launch_bounds__(256) void cdist_vk(const float* __restrict__ X, int64_t m, const float* __restrict__ Y,
+                                                int64_t n, int f, int64_t ldx, int64_t ldy, float* __restrict__ C,
+                                                int64_t ldc, float scale) {
+  __shared__ float sx[LK][LB + 1];
+  __shared__ float sy[LK][LB + 1];
+  const int tid = threadIdx.x;
+  const int64_t tiles_n = (n + LB - 1) / LB;
+  const int64_t row0 = (blockIdx.x / tiles_n) * LB, col0 = (blockIdx.x % tiles_n) * LB;
+  const int tr = tid / 16, tc = tid % 16;  // 16x16 threads, 4x4 outputs each
+  float acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+  for (int k0 = 0; k0 < f; k0 += LK) {
+    for (int e = tid; e < LB * LK; e += 256) {
+      const int r = e / LK, c = e % LK;
+      const int64_t gr = row0 + r, gc = col0 + r;
+      sx[c][r] = (gr < m && k0 + c < f) ? X[gr * ldx + k0 + c] : 0.f;
+      sy[c][r] = (gc < n && k0 + c < f) ? Y[gc * ldy + k0 + c] : 0.f;
+    }
+    __syncthreads();
+    const int kk = (f - k0) < LK ? (f - k0) : LK;
+    for (int k = 0; k < kk; ++k) {
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = sx[k][tr + 16 * u];
+        b[u] = sy[k][tc + 16 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float d = a[u] - b[v];
+          if (OP == 0) acc[u][v] += fabsf(d);
+          else acc[u][v] = fmaf(d, d, acc[u][v]);
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t row = row0 + tr + 16 * u;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int64_t col = col0 + tc + 16 * v;
+      float r = acc[u][v];
+      if (OP == 1) r = sqrtf(r);
+      else if (OP == 3) r = __expf(-r * scale);
+      if (row < m && col < n) C[row * ldc + col] = r;
+    }
+  }
+}
+
+}  // namespace
+
+// mode: 0 euclidean, 1 squared euclidean, 2 gaussian (exp(-d2*scale)) - MFMA quadratic expansion;
+//       3 manhattan; 4 / 5 / 6 = exact (difference-based) euclidean / squared / gaussian on the VALU
+HA_EXPORT int ha_cdist(const float* X, int64_t m, const float* Y, int64_t n, int f, int64_t ldx, int64_t ldy, float* C,
+                       int64_t ldc, int mode, float scale, void* stream) {
+  if (m <= 0 || n <= 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (mode >= 3) {
+    const int64_t tiles = ((m + LB - 1) / LB) * ((n + LB - 1) / LB);
+    if (tiles > 0x7fffffffLL) return HA_UNSUPPORTED;
+    const dim3 g((unsigned)tiles), b(256);
+    switch (mode) {
+      case 3: hipLaunchKernelGGL(cdist_vk<0>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
+      case 4: hipLaunchKernelGGL(cdist_vk<1>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
+      case 5: hipLaunchKernelGGL(cdist_vk<2>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
+      case 6: hipLaunchKernelGGL(cdist_vk<3>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
+      default: return HA_BAD_ARG;
+    }
+    return ha_launch_status();
+  }
+  if (f % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0) return HA_BAD_ARG;
+  const int64_t tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
+  if (tiles > 0x7fffffffLL) return HA_UNSUPPORTED;
+  hipLaunchKernelGGL(cdist_l2, dim3((unsigned)tiles), dim3(256), 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, mode, scale);
+  return ha_launch_status();
+}

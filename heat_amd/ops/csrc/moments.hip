@@ -1,0 +1,242 @@
+// Single-pass statistical moments (count, mean, M2) on CDNA4: the HBM-bound core of
+// mean/var/std (reference heat/core/statistics.py:726-835 mean, 1634-1769 var).
+//
+// Each thread accumulates SHIFTED sums (x-K, (x-K)^2) in fp32 over its elements (K = a value of
+// the same data, so the sums do not cancel), converts them to (n, mean, M2) in fp64 and the
+// partial triples are merged with Chan's formula (fp64) across the wave, the workgroup and,
+// outside this file, across workgroup partials and ranks.  Loads are 16-byte vectorised.
+#include "common.h"
+
+namespace {
+
+struct Trip {
+  double n, mean, m2;
+};
+
+__device__ __forceinline__ Trip trip_from_shifted(double n, float K, float s1, float s2) {
+  Trip t;
+  t.n = n;
+  if (n > 0) {
+    const double d1 = s1, d2 = s2;
+    t.mean = (double)K + d1 / n;
+    double m2 = d2 - d1 * d1 / n;
+    t.m2 = m2 > 0 ? m2 : 0.0;
+  } else {
+    t.mean = 0.0;
+    t.m2 = 0.0;
+  }
+  return t;
+}
+
+__device__ __forceinline__ Trip chan(const Trip& a, const Trip& b) {
+  if (a.n == 0) return b;
+  if (b.n == 0) return a;
+  Trip r;
+  r.n = a.n + b.n;
+  const double d = b.mean - a.mean;
+  r.mean = a.mean + d * (b.n / r.n);
+  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / r.n);
+  return r;
+}
+
+__device__ __forceinline__ Trip wave_merge(Trip t) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Trip u;
+    u.n = __shfl_xor(t.n, o, 64);
+    u.mean = __shfl_xor(t.mean, o, 64);
+    u.m2 = __shfl_xor(t.m2, o, 64);
+    t = chan(t, u);
+  }
+  return t;
+}
+
+// rows: x[r * ld + i], i in [0, len).  Grid.x = nrows * nchunks; part[(r*nchunks + c)*3 + {0,1,2}]
+__global__ __launch_bounds__(256) void mom_rows(const float* __restrict__ x, int64_t nrows, int64_t len,
+                                                int64_t ld, int nchunks, double* __restrict__ part) {
+  const int64_t g = blockIdx.x;
+  const int64_t r = g / nchunks;
+  const int c = (int)(g % nchunks);
+  const int64_t per = (len + nchunks - 1) / nchunks;
+  int64_t c0 = (int64_t)c * per;
+  int64_t c1 = c0 + per < len ? c0 + per : len;
+  const float* row = x + r * ld;
+  const int tid = threadIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  double cnt = 0;
+  float K = c0 < c1 ? row[c0] : 0.f;
+  const bool vec = ((reinterpret_cast<uintptr_t>(row) & 15) == 0);
+  if (c0 < c1) {
+    int64_t i0 = c0;
+    if (vec) {
+      // scalar head up to 16-byte alignment, then float4 body
+      const int64_t a0 = (c0 + 3) & ~(int64_t)3;
+      const int64_t head_end = a0 < c1 ? a0 : c1;
+      for (int64_t i = c0 + tid; i < head_end; i += 256) {
+        const float d = row[i] - K;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+        cnt += 1;
+      }
+      i0 = head_end;
+      const int64_t nv = (c1 - i0) / 4;
+      const floatx4* v4 = reinterpret_cast<const floatx4*>(row + i0);
+      int64_t q = tid;
+      for (; q + 3 * 256 < nv; q += 4 * 256) {
+        floatx4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = v4[q + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = a[u][e] - K;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+          }
+        }
+        cnt += 16;
+      }
+      for (; q < nv; q += 256) {
+        const floatx4 a = v4[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = a[e] - K;
+          s1 += d;
+          s2 = fmaf(d, d, s2);
+        }
+        cnt += 4;
+      }
+      i0 += nv * 4;
+    }
+    for (int64_t i = i0 + tid; i < c1; i += 256) {
+      const float d = row[i] - K;
+      s1 += d;
+      s2 = fmaf(d, d, s2);
+      cnt += 1;
+    }
+  }
+  Trip t = trip_from_shifted(cnt, K, s1, s2);
+  t = wave_merge(t);
+  __shared__ double sh[4][3];
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    sh[w][0] = t.n;
+    sh[w][1] = t.mean;
+    sh[w][2] = t.m2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    Trip acc = {sh[0][0], sh[0][1], sh[0][2]};
+    for (int k = 1; k < 4; ++k) acc = chan(acc, Trip{sh[k][0], sh[k][1], sh[k][2]});
+    double* o = part + g * 3;
+    o[0] = acc.n;
+    o[1] = acc.mean;
+    o[2] = acc.m2;
+  }
+}
+
+// columns: x[i * ld + col], reduce over i in [0, len).  Each thread owns VEC consecutive
+// columns; grid = (ceil(ncols / (256*VEC)), nchunks).  part[(c*ncols + col)*3 + {0,1,2}]
+template <int VEC>
+__global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int64_t len, int64_t ncols,
+                                                int64_t ld, int nchunks, double* __restrict__ part) {
+  const int64_t col0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
+  const int c = blockIdx.y;
+  const int64_t per = (len + nchunks - 1) / nchunks;
+  const int64_t r0 = (int64_t)c * per;
+  const int64_t r1 = r0 + per < len ? r0 + per : len;
+  if (col0 >= ncols) return;
+  float K[VEC], s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+    K[e] = 0.f;
+  }
+  if (r0 < r1) {
+    if (VEC == 4) {
+      const floatx4 k4 = *reinterpret_cast<const floatx4*>(x + r0 * ld + col0);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) K[e] = k4[e];
+    } else {
+      K[0] = x[r0 * ld + col0];
+    }
+  }
+  int64_t i = r0;
+  for (; i + 3 < r1; i += 4) {
+    if (VEC == 4) {
+      floatx4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const floatx4*>(x + (i + u) * ld + col0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = a[u][e] - K[e];
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
+    } else {
+      float a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = x[(i + u) * ld + col0];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float d = a[u] - K[0];
+        s1[0] += d;
+        s2[0] = fmaf(d, d, s2[0]);
+      }
+    }
+  }
+  for (; i < r1; ++i) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float d = x[i * ld + col0 + e] - K[e];
+      s1[e] += d;
+      s2[e] = fmaf(d, d, s2[e]);
+    }
+  }
+  const double n = (double)(r1 > r0 ? r1 - r0 : 0);
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int64_t col = col0 + e;
+    if (col < ncols) {
+      const Trip t = trip_from_shifted(n, K[e], s1[e], s2[e]);
+      double* o = part + ((int64_t)c * ncols + col) * 3;
+      o[0] = t.n;
+      o[1] = t.mean;
+      o[2] = t.m2;
+    }
+  }
+}
+
+}  // namespace
+
+HA_EXPORT int ha_moments_rows(const float* x, int64_t nrows, int64_t len, int64_t ld, int nchunks, double* part,
+                              void* stream) {
+  if (nrows <= 0) return HA_OK;
+  if (nchunks < 1) return HA_BAD_ARG;
+  const int64_t grid = nrows * nchunks;
+  if (grid > 0x7fffffffLL) return HA_UNSUPPORTED;
+  hipLaunchKernelGGL(mom_rows, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, x, nrows, len, ld, nchunks,
+                     part);
+  return ha_launch_status();
+}
+
+HA_EXPORT int ha_moments_cols(const float* x, int64_t len, int64_t ncols, int64_t ld, int nchunks, double* part,
+                              void* stream) {
+  if (ncols <= 0) return HA_OK;
+  if (nchunks < 1 || nchunks > 65535) return HA_BAD_ARG;
+  const bool vec = (ncols % 4 == 0) && (ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  if (vec) {
+    const int64_t gx = (ncols / 4 + 255) / 256;
+    hipLaunchKernelGGL(mom_cols<4>, dim3((unsigned)gx, nchunks), dim3(256), 0, (hipStream_t)stream, x, len, ncols,
+                       ld, nchunks, part);
+  } else {
+    const int64_t gx = (ncols + 255) / 256;
+    hipLaunchKernelGGL(mom_cols<1>, dim3((unsigned)gx, nchunks), dim3(256), 0, (hipStream_t)stream, x, len, ncols,
+                       ld, nchunks, part);
+  }
+  return ha_launch_status();
+}

@@ -1,0 +1,150 @@
+// Counter-based Threefry RNG, bit-exact with the reference's 8-round variant
+// (heat/core/random.py:864-1062; counter layout 55-200; float conversion 220-245; Kundu normal
+// transform 248-265; biased randint 556-560) - fused into ONE kernel: counter -> 8 rounds ->
+// uint->float / normal / integer, instead of ~40 elementwise torch launches per call.
+//
+// Global element e of the flat random stream uses counter pair g = e >> 1 (component e & 1).
+// 32-bit variant: V = counter + g (mod 2^64), x0 = hi32(V), x1 = lo32(V), key = seed & 0x7FFFFFFF.
+// 64-bit variant: V = counter + g (mod 2^128), x0 = hi64(V), x1 = lo64(V), key = seed.
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+__device__ __forceinline__ void tf32(uint32_t& x0, uint32_t& x1, uint32_t k) {
+  const uint32_t ks0 = k, ks1 = k, ks2 = 466688986u ^ k ^ k;
+  x0 += ks0;
+  x1 += ks1;
+  x0 += x1; x1 = rotl32(x1, 13); x1 ^= x0;
+  x0 += x1; x1 = rotl32(x1, 15); x1 ^= x0;
+  x0 += x1; x1 = rotl32(x1, 26); x1 ^= x0;
+  x0 += x1; x1 = rotl32(x1, 6); x1 ^= x0;
+  x0 += ks1;
+  x1 += ks2 + 1u;
+  x0 += x1; x1 = rotl32(x1, 17); x1 ^= x0;
+  x0 += x1; x1 = rotl32(x1, 29); x1 ^= x0;
+  x0 += x1; x1 = rotl32(x1, 16); x1 ^= x0;
+  x0 += x1; x1 = rotl32(x1, 24); x1 ^= x0;
+  x0 += ks0;
+  x1 += ks1 + 3u;
+}
+
+__device__ __forceinline__ void tf64(uint64_t& x0, uint64_t& x1, uint64_t k) {
+  const uint64_t ks0 = k, ks1 = k, ks2 = 2004413935125273122ull ^ k ^ k;
+  x0 += ks0;
+  x1 += ks1;
+  x0 += x1; x1 = rotl64(x1, 16); x1 ^= x0;
+  x0 += x1; x1 = rotl64(x1, 42); x1 ^= x0;
+  x0 += x1; x1 = rotl64(x1, 12); x1 ^= x0;
+  x0 += x1; x1 = rotl64(x1, 31); x1 ^= x0;
+  x0 += ks1;
+  x1 += ks2 + 1ull;
+  x0 += x1; x1 = rotl64(x1, 16); x1 ^= x0;
+  x0 += x1; x1 = rotl64(x1, 32); x1 ^= x0;
+  x0 += x1; x1 = rotl64(x1, 24); x1 ^= x0;
+  x0 += x1; x1 = rotl64(x1, 21); x1 ^= x0;
+  x0 += ks0;
+  x1 += ks1 + 3ull;
+}
+
+// distribution codes
+enum { DIST_UNIFORM = 0, DIST_NORMAL = 1, DIST_INT = 2 };
+
+__device__ __forceinline__ float kundu_f(float u) {
+  const float inner = 1.f - powf(u, 0.0775f);
+  const float tiny = 1.17549435e-38f;
+  return (logf(-logf(inner + tiny) + tiny) - 1.0821f) * (1.0f / 0.3807f);
+}
+
+__device__ __forceinline__ double kundu_d(double u) {
+  const double inner = 1.0 - pow(u, 0.0775);
+  const double tiny = 2.2250738585072014e-308;
+  return (log(-log(inner + tiny) + tiny) - 1.0821) * (1.0 / 0.3807);
+}
+
+// out: local block of n elements; global element index of out[0] is e0.
+__global__ __launch_bounds__(256) void tf_fill32(void* __restrict__ out, int64_t e0, int64_t n, uint64_t counter_lo,
+                                                 uint32_t key, int dist, int64_t low, int64_t span) {
+  const int64_t p0 = e0 >> 1;
+  const int64_t p1 = (e0 + n + 1) >> 1;
+  for (int64_t p = p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < p1;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t V = counter_lo + (uint64_t)p;
+    uint32_t x0 = (uint32_t)(V >> 32), x1 = (uint32_t)V;
+    tf32(x0, x1, key);
+    const uint32_t comp[2] = {x0, x1};
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t e = 2 * p + c;
+      const int64_t i = e - e0;
+      if (i < 0 || i >= n) continue;
+      const uint32_t v = comp[c];
+      if (dist == DIST_INT) {
+        int32_t s = (int32_t)v;
+        int32_t a = s < 0 ? (int32_t)(0u - (uint32_t)s) : s;  // torch abs (wraps at INT_MIN)
+        int64_t r = (int64_t)a % span;
+        if (r < 0) r += span;
+        reinterpret_cast<int32_t*>(out)[i] = (int32_t)(r + low);
+      } else {
+        const float u = (float)(v & 0x7FFFFFu) * (1.0f / 8388608.0f);
+        reinterpret_cast<float*>(out)[i] = dist == DIST_NORMAL ? kundu_f(u) : u;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void tf_fill64(void* __restrict__ out, int64_t e0, int64_t n, uint64_t counter_lo,
+                                                 uint64_t counter_hi, uint64_t key, int dist, int64_t low,
+                                                 int64_t span) {
+  const int64_t p0 = e0 >> 1;
+  const int64_t p1 = (e0 + n + 1) >> 1;
+  for (int64_t p = p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < p1;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t lo = counter_lo + (uint64_t)p;
+    const uint64_t hi = counter_hi + (lo < counter_lo ? 1ull : 0ull);
+    uint64_t x0 = hi, x1 = lo;
+    tf64(x0, x1, key);
+    const uint64_t comp[2] = {x0, x1};
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t e = 2 * p + c;
+      const int64_t i = e - e0;
+      if (i < 0 || i >= n) continue;
+      const uint64_t v = comp[c];
+      if (dist == DIST_INT) {
+        int64_t s = (int64_t)v;
+        int64_t a = s < 0 ? (int64_t)(0ull - (uint64_t)s) : s;
+        int64_t r = a % span;
+        if (r < 0) r += span;
+        reinterpret_cast<int64_t*>(out)[i] = r + low;
+      } else {
+        const double u = (double)(v & 0x1FFFFFFFFFFFFFull) * (1.0 / 9007199254740992.0);
+        reinterpret_cast<double*>(out)[i] = dist == DIST_NORMAL ? kundu_d(u) : u;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// bits: 32 or 64. For bits == 32 only counter_lo (the counter mod 2^64) is used.
+HA_EXPORT int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counter_lo, uint64_t counter_hi, uint64_t seed,
+                               int bits, int dist, double low, double span, void* stream) {
+  if (n <= 0) return HA_OK;
+  const int64_t pairs = ((e0 + n + 1) >> 1) - (e0 >> 1);
+  int64_t blocks = (pairs + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipStream_t s = (hipStream_t)stream;
+  if (bits == 32) {
+    hipLaunchKernelGGL(tf_fill32, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo,
+                       (uint32_t)(seed & 0x7FFFFFFFull), dist, (int64_t)low, (int64_t)span);
+  } else if (bits == 64) {
+    hipLaunchKernelGGL(tf_fill64, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo, counter_hi, seed,
+                       dist, (int64_t)low, (int64_t)span);
+  } else {
+    return HA_BAD_ARG;
+  }
+  return ha_launch_status();
+}

@@ -1,0 +1,232 @@
+"""
+Python entry points of the native kernels (device tensors) with PyTorch reference paths (host
+tensors; also the numerics oracle of the tests).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import check, lib, stream_ptr, use_native
+
+__all__ = ["kmeans_assign", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist"]
+
+_NUM_CUS = {}
+
+
+def num_cus(device) -> int:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _NUM_CUS:
+        _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _NUM_CUS[idx]
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+# --------------------------------------------------------------------------------------------- k-means
+def _rows_f32_aligned(X: torch.Tensor) -> torch.Tensor:
+    """fp32, row-contiguous, feature count a multiple of 4 (zero padding changes no dot product)."""
+    if X.dtype != torch.float32:
+        X = X.float()
+    if X.stride(-1) != 1 or X.stride(0) % 4 != 0 or X.data_ptr() % 16 != 0:
+        X = X.contiguous()
+    f = X.shape[1]
+    if f % 4 != 0:
+        X = F.pad(X, (0, 4 - f % 4))
+    if X.stride(0) % 4 != 0 or X.data_ptr() % 16 != 0:
+        X = X.contiguous()
+    return X
+
+
+def kmeans_assign(X: torch.Tensor, C: torch.Tensor, want_mind: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Nearest centroid (squared L2) of every row of X. Returns (int32 labels, min squared distance).
+
+    Device tensors: fused fp32-MFMA distance + running argmin kernel (no n x k intermediate)."""
+    n, f = X.shape
+    k = C.shape[0]
+    if n == 0:
+        return (torch.empty(0, dtype=torch.int32, device=X.device),
+                torch.empty(0, dtype=torch.float32, device=X.device) if want_mind else None)
+    if use_native(X) and f <= 128:
+        Xa = _rows_f32_aligned(X)
+        Ca = _rows_f32_aligned(C.to(X.device))
+        fa = Xa.shape[1]
+        L = lib()
+        fpad, kpad = ctypes.c_int(), ctypes.c_int()
+        wsz = L.ha_km_workspace_floats(k, fa, ctypes.byref(fpad), ctypes.byref(kpad))
+        ws = torch.empty(wsz, dtype=torch.float32, device=X.device)
+        labels = torch.empty(n, dtype=torch.int32, device=X.device)
+        mind = torch.empty(n, dtype=torch.float32, device=X.device) if want_mind else None
+        rc = L.ha_km_assign(_ptr(Xa), n, fa, Xa.stride(0), _ptr(Ca), k, Ca.stride(0), _ptr(ws), _ptr(labels),
+                            _ptr(mind), ctypes.c_void_p(stream_ptr(X.device)))
+        check(rc, "ha_km_assign")
+        return labels, mind
+    Xf = X.float() if X.dtype not in (torch.float32, torch.float64) else X
+    Cf = C.to(Xf.dtype)
+    cn = (Cf * Cf).sum(1)
+    d = torch.addmm(cn.unsqueeze(0), Xf, Cf.t(), beta=1.0, alpha=-2.0)
+    best, labels = torch.min(d, dim=1)
+    mind = None
+    if want_mind:
+        mind = torch.clamp(best + (Xf * Xf).sum(1), min=0).float()
+    return labels.to(torch.int32), mind
+
+
+def kmeans_update(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-cluster feature sums [k, f] and counts [k] (float32) of the rows of X."""
+    n, f = X.shape
+    if use_native(X) and X.dtype == torch.float32:
+        L = lib()
+        if L.ha_km_update_fc(k, f) > 0:
+            Xc = X if X.stride(-1) == 1 else X.contiguous()
+            lab = labels.to(torch.int32).contiguous()
+            sums = torch.zeros((k, f), dtype=torch.float32, device=X.device)
+            counts = torch.zeros(k, dtype=torch.float32, device=X.device)
+            rc = L.ha_km_update(_ptr(Xc), n, f, Xc.stride(0), _ptr(lab), k, _ptr(sums), _ptr(counts),
+                                num_cus(X.device), ctypes.c_void_p(stream_ptr(X.device)))
+            check(rc, "ha_km_update")
+            return sums, counts
+    lab = labels.to(torch.int64)
+    sums = torch.zeros((k, f), dtype=X.dtype if X.is_floating_point() else torch.float32, device=X.device)
+    sums.index_add_(0, lab, X.to(sums.dtype))
+    counts = torch.bincount(lab, minlength=k).to(sums.dtype)
+    return sums, counts
+
+
+# --------------------------------------------------------------------------------------------- moments
+def merge_moments(n: torch.Tensor, mean: torch.Tensor, m2: torch.Tensor, dim: int):
+    """Chan/Golub/LeVeque merge of (count, mean, M2) partials along ``dim`` (fp64)."""
+    N = n.sum(dim)
+    safe = torch.where(N > 0, N, torch.ones_like(N))
+    mu = (n * mean).sum(dim) / safe
+    M2 = (m2 + n * (mean - mu.unsqueeze(dim)) ** 2).sum(dim)
+    return N, mu, M2
+
+
+def _moments_native(x: torch.Tensor, axis):
+    L = lib()
+    s = ctypes.c_void_p(stream_ptr(x.device))
+    ncu = num_cus(x.device)
+    if axis is None:
+        flat = x.reshape(-1)
+        if not flat.is_contiguous():
+            flat = flat.contiguous()
+        numel = flat.numel()
+        nchunks = max(1, min(8 * ncu, (numel + 16383) // 16384))
+        part = torch.empty((1, nchunks, 3), dtype=torch.float64, device=x.device)
+        check(L.ha_moments_rows(_ptr(flat), 1, numel, numel, nchunks, _ptr(part), s), "ha_moments_rows")
+        N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 1)
+        return N.reshape(()), mu.reshape(()), M2.reshape(())
+    nd = x.dim()
+    if not x.is_contiguous():
+        x = x.contiguous()
+    shape = list(x.shape)
+    red = shape[axis]
+    outer = 1
+    for d in shape[:axis]:
+        outer *= d
+    inner = 1
+    for d in shape[axis + 1:]:
+        inner *= d
+    out_shape = shape[:axis] + shape[axis + 1:]
+    if inner == 1:
+        nrows = outer
+        nchunks = max(1, min((2 * 8 * ncu + nrows - 1) // max(nrows, 1), (red + 4095) // 4096))
+        part = torch.empty((nrows, nchunks, 3), dtype=torch.float64, device=x.device)
+        check(L.ha_moments_rows(_ptr(x), nrows, red, red, nchunks, _ptr(part), s), "ha_moments_rows")
+        N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 1)
+    elif outer == 1:
+        ncols = inner
+        col_blocks = max(1, (ncols + 1023) // 1024)
+        nchunks = max(1, min(65535, (8 * ncu + col_blocks - 1) // col_blocks, (red + 63) // 64))
+        part = torch.empty((nchunks, ncols, 3), dtype=torch.float64, device=x.device)
+        check(L.ha_moments_cols(_ptr(x), red, ncols, ncols, nchunks, _ptr(part), s), "ha_moments_cols")
+        N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 0)
+    else:
+        y = x.movedim(axis, -1).contiguous()
+        return _moments_native(y, y.dim() - 1)
+    return N.reshape(out_shape), mu.reshape(out_shape), M2.reshape(out_shape)
+
+
+def moments(x: torch.Tensor, axis: Optional[int] = None):
+    """(count, mean, M2) over ``axis`` (None = all) as float64 tensors.
+
+    Device fp32 tensors: one HBM pass with 16-byte loads (``moments.hip``)."""
+    if use_native(x) and x.dtype == torch.float32 and x.numel() > 0:
+        return _moments_native(x, axis)
+    xd = x.double() if not x.is_complex() else x
+    if axis is None:
+        n = torch.tensor(float(x.numel()), dtype=torch.float64, device=x.device)
+        if x.numel() == 0:
+            z = torch.tensor(0.0, dtype=torch.float64, device=x.device)
+            return n, z, z.clone()
+        var, mean = torch.var_mean(xd, correction=0)
+        return n, mean, var * n
+    n = torch.full([s for i, s in enumerate(x.shape) if i != axis], float(x.shape[axis]), dtype=torch.float64,
+                   device=x.device)
+    if x.shape[axis] == 0:
+        z = torch.zeros_like(n)
+        return n, z, z.clone()
+    var, mean = torch.var_mean(xd, dim=axis, correction=0)
+    return n, mean, var * n
+
+
+# --------------------------------------------------------------------------------------------- cdist
+_CDIST_MODES = {"euclidean": 0, "sqeuclidean": 1, "gaussian": 2, "manhattan": 3}
+_CDIST_EXACT = {"euclidean": 4, "sqeuclidean": 5, "gaussian": 6, "manhattan": 3}
+
+
+def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: float = 1.0,
+          out: Optional[torch.Tensor] = None, exact: bool = False) -> torch.Tensor:
+    """Pairwise distances between the rows of X [m, f] and Y [n, f] as an [m, n] float32 matrix.
+
+    Device tensors: ``exact=False`` -> fp32-MFMA tile kernel of the quadratic expansion with a
+    fused norm/clamp/sqrt|exp epilogue; ``exact=True`` (and manhattan) -> VALU tile kernel on the
+    differences (no cancellation for near-identical points). No m x n x f intermediate."""
+    m, f = X.shape
+    n = Y.shape[0]
+    if metric not in _CDIST_MODES:
+        raise ValueError("unknown metric {}".format(metric))
+    if use_native(X) and X.dtype == torch.float32 and Y.dtype == torch.float32:
+        L = lib()
+        mode = (_CDIST_EXACT if exact else _CDIST_MODES)[metric]
+        if mode < 3:
+            Xa = _rows_f32_aligned(X)
+            Ya = _rows_f32_aligned(Y.to(X.device))
+        else:
+            Xa = X if X.stride(-1) == 1 else X.contiguous()
+            Ya = Y.to(X.device)
+            Ya = Ya if Ya.stride(-1) == 1 else Ya.contiguous()
+        C = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=X.device)
+        if m and n:
+            rc = L.ha_cdist(_ptr(Xa), m, _ptr(Ya), n, Xa.shape[1], Xa.stride(0), Ya.stride(0), _ptr(C), C.stride(0),
+                            mode, ctypes.c_float(1.0 / (2.0 * sigma * sigma)), ctypes.c_void_p(stream_ptr(X.device)))
+            check(rc, "ha_cdist")
+        return C
+    Xf = X if X.is_floating_point() else X.float()
+    Yf = Y.to(Xf.dtype)
+    if metric == "manhattan":
+        res = torch.cdist(Xf, Yf, p=1)
+    elif exact:
+        d2 = torch.cdist(Xf, Yf, p=2, compute_mode="donot_use_mm_for_euclid_dist") ** 2
+        res = {"euclidean": lambda: d2.sqrt(), "sqeuclidean": lambda: d2,
+               "gaussian": lambda: torch.exp(-d2 / (2.0 * sigma * sigma))}[metric]()
+    else:
+        xn = (Xf * Xf).sum(1, keepdim=True)
+        yn = (Yf * Yf).sum(1).unsqueeze(0)
+        d2 = torch.clamp(torch.addmm(xn + yn, Xf, Yf.t(), beta=1.0, alpha=-2.0), min=0)
+        if metric == "euclidean":
+            res = torch.sqrt(d2)
+        elif metric == "sqeuclidean":
+            res = d2
+        else:
+            res = torch.exp(-d2 / (2.0 * sigma * sigma))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res

@@ -1,0 +1,13 @@
+"""ctypes signatures of native kernels beyond the core set (registered when present)."""
+import ctypes
+
+c_void_p, c_int, c_int64, c_uint64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
+                                                         ctypes.c_uint64, ctypes.c_float, ctypes.c_double)
+
+SIGNATURES = {
+    "ha_cdist": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_void_p, c_int64, c_int,
+                         c_float, c_void_p]),
+    "ha_threefry_fill": (c_int, [c_void_p, c_int64, c_int64, c_uint64, c_uint64, c_uint64, c_int, c_int, c_double,
+                                 c_double, c_void_p]),
+    "ha_lasso_cd_epoch": (c_int, [c_void_p]),
+}

@@ -1,0 +1,52 @@
+"""Multi-process test harness: run a check function in N ranks over gloo on 127.0.0.1.
+
+``run_distributed("tests.dist_checks:check_x", 3)`` starts N fresh interpreters with the
+launcher environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT); each imports heat_amd,
+which initialises the process group, then runs the function. Any rank failing fails the test.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None):
+    port = _free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "WORLD_SIZE": str(nprocs), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(nprocs),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HEAT_COMM_BACKEND": "gloo",
+                    "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1",
+                    "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        if env_extra:
+            env.update(env_extra)
+        procs.append(subprocess.Popen([sys.executable, "-m", "tests._dist_runner", target], cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs, failed = [], []
+    for r, p in enumerate(procs):
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("distributed test {} timed out on rank {}".format(target, r))
+        outs.append(out.decode(errors="replace"))
+        if p.returncode != 0:
+            failed.append(r)
+    if failed:
+        msg = "\n".join("----- rank {} -----\n{}".format(r, outs[r][-6000:]) for r in failed)
+        raise AssertionError("distributed test {} failed on ranks {}\n{}".format(target, failed, msg))
+    return outs

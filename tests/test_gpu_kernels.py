@@ -1,0 +1,134 @@
+"""Numerics of the native CDNA4 kernels against plain PyTorch fp32/fp64 references (GPU only)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from heat_amd import ops
+
+    assert ops.available(), "native library must load on a GPU box"
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("n,k,f", [(1000, 7, 3), (4096, 128, 16), (5000, 300, 32), (20000, 1024, 64),
+                                   (3333, 100, 100), (777, 65, 128)])
+def test_kmeans_assign(n, k, f):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + k + f)
+    X = torch.randn(n, f, generator=g).to(dev)
+    C = torch.randn(k, f, generator=g).to(dev)
+    lab, mind = ops.kmeans_assign(X, C)
+    Xd, Cd = X.double(), C.double()
+    d = torch.cdist(Xd, Cd) ** 2
+    ref_min, ref_lab = d.min(1)
+    # labels may only differ on numerical near-ties
+    chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+    assert torch.all(chosen - ref_min <= 1e-4 * (1 + ref_min)), "assigned centroid not (near-)minimal"
+    assert (lab.long() == ref_lab).float().mean() > 0.999
+    assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,k,f", [(1000, 7, 3), (50000, 1024, 64), (12345, 33, 100), (4096, 8, 18)])
+def test_kmeans_update(n, k, f):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n)
+    X = torch.randn(n, f, generator=g).to(dev)
+    lab = torch.randint(0, k, (n,), generator=g).to(dev).to(torch.int32)
+    sums, counts = ops.kmeans_update(X, lab, k)
+    ref = torch.zeros(k, f, dtype=torch.float64, device=dev).index_add_(0, lab.long(), X.double())
+    rc = torch.bincount(lab.long(), minlength=k).double()
+    assert torch.allclose(sums.double(), ref, rtol=1e-4, atol=1e-3)
+    assert torch.equal(counts.double(), rc)
+
+
+@pytest.mark.parametrize("shape,axis", [((10_000_003,), None), ((1000, 999), None), ((1000, 999), 0),
+                                        ((1000, 999), 1), ((3, 1000, 4), 1), ((513, 1024), 0), ((7, 5), 1)])
+def test_moments(shape, axis):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(len(shape))
+    x = (torch.randn(*shape, generator=g) * 3 + 100).to(dev)
+    n, mu, m2 = ops.moments(x, axis)
+    xd = x.double()
+    if axis is None:
+        rv, rm = torch.var_mean(xd, correction=0)
+    else:
+        rv, rm = torch.var_mean(xd, dim=axis, correction=0)
+    assert torch.allclose(mu, rm, rtol=1e-6, atol=1e-5)
+    assert torch.allclose(m2 / n, rv, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian", "manhattan"])
+@pytest.mark.parametrize("m,n,f", [(100, 50, 3), (1000, 777, 18), (257, 300, 128), (64, 64, 200)])
+def test_cdist(metric, m, n, f, exact):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(m * n)
+    X = torch.rand(m, f, generator=g).to(dev)
+    Y = torch.rand(n, f, generator=g).to(dev)
+    out = ops.cdist(X, Y, metric, sigma=2.0, exact=exact)
+    Xd, Yd = X.double(), Y.double()
+    if metric == "manhattan":
+        ref = torch.cdist(Xd, Yd, p=1)
+    else:
+        d2 = torch.cdist(Xd, Yd) ** 2
+        ref = {"euclidean": d2.sqrt(), "sqeuclidean": d2, "gaussian": torch.exp(-d2 / 8.0)}[metric]
+    tol = 2e-3 if (metric == "euclidean" and not exact) else 1e-4
+    assert torch.allclose(out.double(), ref, rtol=tol, atol=tol)
+    if exact and metric == "euclidean":
+        # identical rows: exactly zero distance (no cancellation)
+        self_d = ops.cdist(X, X, metric, exact=True)
+        assert torch.all(torch.diagonal(self_d) == 0)
+
+
+def test_threefry_bit_exact():
+    """Device Threefry kernel == host torch implementation, bit for bit (uniform / int)."""
+    import heat_amd as ht
+
+    _dev()
+    for dtype in (ht.float32, ht.float64):
+        for state in (0, 0xFFFFFFFFFFFFFFF0, (1 << 128) - 16):
+            ht.random.set_state(("Threefry", 12345, state))
+            a = ht.random.rand(1001, 3, dtype=dtype, device="cpu")
+            ht.random.set_state(("Threefry", 12345, state))
+            b = ht.random.rand(1001, 3, dtype=dtype, device="gpu")
+            assert torch.equal(a.larray, b.larray.cpu())
+    for dtype in (ht.int32, ht.int64):
+        ht.random.set_state(("Threefry", 99, 5))
+        a = ht.random.randint(-7, 1000, size=(333, 7), dtype=dtype, device="cpu")
+        ht.random.set_state(("Threefry", 99, 5))
+        b = ht.random.randint(-7, 1000, size=(333, 7), dtype=dtype, device="gpu")
+        assert torch.equal(a.larray, b.larray.cpu())
+    ht.random.set_state(("Threefry", 3, 0))
+    a = ht.random.randn(2000, device="cpu")
+    ht.random.set_state(("Threefry", 3, 0))
+    b = ht.random.randn(2000, device="gpu")
+    # the Kundu transform goes through device transcendentals: equal to a few ulp
+    assert torch.allclose(a.larray, b.larray.cpu(), rtol=1e-4, atol=1e-4)
+
+
+def test_kmeans_fit_gpu(gpu):
+    import heat_amd as ht
+
+    ht.random.seed(1)
+    # well separated blobs
+    centers = torch.tensor([[0.0, 0.0], [10.0, 10.0], [-10.0, 10.0], [10.0, -10.0]])
+    pts = torch.cat([c + torch.randn(500, 2) for c in centers])
+    x = ht.array(pts, split=0, device="gpu")
+    km = ht.cluster.KMeans(n_clusters=4, init="kmeans++", max_iter=50, random_state=2)
+    km.fit(x)
+    got = km.cluster_centers_.larray.cpu()
+    d = torch.cdist(got, centers)
+    assert torch.all(d.min(1).values < 0.5)
+    assert km.labels_.shape == (2000, 1)
