@@ -25,3 +25,5 @@ from . import optim
 from . import utils
 from . import models
 from . import profiling
+
+profiling._auto_enable()

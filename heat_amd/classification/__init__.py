@@ -1,1 +1,4 @@
 """Classification (reference ``heat/classification``)."""
+from .kneighborsclassifier import KNeighborsClassifier
+
+__all__ = ["KNeighborsClassifier"]

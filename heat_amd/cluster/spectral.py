@@ -14,6 +14,7 @@ from .. import core as ht
 from ..core.base import BaseEstimator, ClusteringMixin
 from ..core.dndarray import DNDarray
 from .kmeans import KMeans
+from .. import graph, spatial
 
 
 class Spectral(ClusteringMixin, BaseEstimator):
@@ -32,11 +33,11 @@ class Spectral(ClusteringMixin, BaseEstimator):
         self.assign_labels = assign_labels
         if metric == "rbf":
             sig = math.sqrt(1 / (2 * gamma))
-            self._laplacian = ht.graph.Laplacian(lambda x: ht.spatial.rbf(x, sigma=sig, quadratic_expansion=True),
+            self._laplacian = graph.Laplacian(lambda x: spatial.rbf(x, sigma=sig, quadratic_expansion=True),
                                                  definition="norm_sym", mode=laplacian, threshold_key=boundary,
                                                  threshold_value=threshold)
         elif metric == "euclidean":
-            self._laplacian = ht.graph.Laplacian(lambda x: ht.spatial.cdist(x, quadratic_expansion=True),
+            self._laplacian = graph.Laplacian(lambda x: spatial.cdist(x, quadratic_expansion=True),
                                                  definition="norm_sym", mode=laplacian, threshold_key=boundary,
                                                  threshold_value=threshold)
         else:

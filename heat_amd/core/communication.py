@@ -328,6 +328,13 @@ class MPICommunication(Communication):
         self.Ibcast(buf, root).Wait()
 
     # ---------------------------------------------------------------- reductions
+    def _stack_async(self, src: torch.Tensor):
+        """All-gather ``src`` from every rank into a [p, *src.shape] tensor (async)."""
+        flat = src.reshape(-1)
+        out = torch.empty(self.size * flat.numel(), dtype=src.dtype, device=src.device)
+        work = dist.all_gather_into_tensor(out, flat, group=self.group, async_op=True)
+        return out.view((self.size,) + tuple(src.shape)), work
+
     def _fold_gathered(self, stacked: torch.Tensor, op: Op, upto: Optional[int] = None) -> torch.Tensor:
         n = stacked.shape[0] if upto is None else upto
         acc = stacked[0]
@@ -358,8 +365,7 @@ class MPICommunication(Communication):
             return work, fin
         # generic: all-gather the partials, fold on device (p <= 8 per node)
         src = _wire_dtype(t).contiguous()
-        gathered = torch.empty((self.size,) + tuple(src.shape), dtype=src.dtype, device=src.device)
-        work = dist.all_gather_into_tensor(gathered, src, group=self.group, async_op=True)
+        gathered, work = self._stack_async(src)
 
         def fin():
             g = gathered.to(t.dtype) if gathered.dtype != t.dtype else gathered
@@ -410,8 +416,7 @@ class MPICommunication(Communication):
             if not exclusive and send is not recv:
                 recv.copy_(send)
             return MPIRequest()
-        gathered = torch.empty((self.size,) + tuple(src.shape), dtype=src.dtype, device=src.device)
-        work = dist.all_gather_into_tensor(gathered, src, group=self.group, async_op=True)
+        gathered, work = self._stack_async(src)
 
         def fin():
             g = gathered.to(send.dtype) if gathered.dtype != send.dtype else gathered

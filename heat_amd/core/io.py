@@ -63,7 +63,7 @@ def load_npy(path: str, dtype=None, split: Optional[int] = None, device=None, co
     gshape = tuple(arr.shape)
     split = sanitize_axis(gshape, split)
     _, _, sl = comm.chunk(gshape, split)
-    local = np.ascontiguousarray(arr[sl])
+    local = np.array(arr[sl], copy=True)          # writable private copy of the mmap slice
     t = torch.from_numpy(local)
     htype = types.canonical_heat_type(dtype) if dtype is not None else types.canonical_heat_type(t.dtype)
     t = t.to(device=device.torch_device, dtype=htype.torch_type())
@@ -132,6 +132,7 @@ def load_csv(path: str, header_lines: int = 0, sep: str = ",", dtype=types.float
         hi = body_start + body * (comm.rank + 1) // comm.size
         with open(path, "rb") as f:
             # a line belongs to the rank in whose range it STARTS
+            f.seek(lo)
             if lo > body_start:
                 f.seek(lo - 1)
                 prev = f.read(1)

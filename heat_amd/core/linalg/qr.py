@@ -78,6 +78,8 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
         src.balance_()
     Ql, R2 = _tsqr(src.larray.to(tt), src.comm, n, calc_q)
     k = min(m, n)
+    if mode == "complete" and m > R2.shape[0]:
+        R2 = torch.cat([R2, R2.new_zeros((m - R2.shape[0], n))], dim=0)
     R = factories.array(R2, split=a.split, device=a.device, comm=a.comm, dtype=dtype)
     if not calc_q:
         return QR(None, R)

@@ -1,1 +1,4 @@
 """Naive Bayes (reference ``heat/naive_bayes``)."""
+from .gaussianNB import GaussianNB
+
+__all__ = ["GaussianNB"]

@@ -195,38 +195,41 @@ __global__ __launch_bounds__(256, 2) void km_assign(const float* __restrict__ X,
 
 // One pass over the points: per-(centroid, column) sums in LDS (ds_add_f32), counts in LDS,
 // flushed once per workgroup with coalesced global float atomics (256 contiguous bytes per
-// wave instruction).  Grid = (row ranges, column blocks of FC columns).
+// wave instruction).  Grid = (row ranges, column blocks of FC columns).  1024 threads and 8 rows
+// per thread in flight keep ~64 KB of loads outstanding per CU (the kernel is HBM-bound; at one
+// workgroup per CU the first version was latency-bound at ~0.8 TB/s).
+constexpr int KU_THREADS = 1024;
+constexpr int KU_UNROLL = 8;
 template <int FC>
-__global__ __launch_bounds__(512) void km_update(const float* __restrict__ X, int64_t n, int f, int64_t ldx,
-                                                 const int* __restrict__ labels, int k, int64_t rows_per_wg,
-                                                 float* __restrict__ sums, float* __restrict__ counts) {
+__global__ __launch_bounds__(KU_THREADS) void km_update(const float* __restrict__ X, int64_t n, int f, int64_t ldx,
+                                                        const int* __restrict__ labels, int k, int64_t rows_per_wg,
+                                                        float* __restrict__ sums, float* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* lsum = lds;               // [k][FC]
+  float* lsum = lds;                    // [k][FC]
   float* lcnt = lds + (int64_t)k * FC;  // [k]
   const int tid = threadIdx.x;
-  for (int e = tid; e < k * FC + k; e += 512) lds[e] = 0.f;
+  for (int e = tid; e < k * FC + k; e += KU_THREADS) lds[e] = 0.f;
   __syncthreads();
   const int cblk = blockIdx.y;
   const int c0 = cblk * FC;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t r1 = r0 + rows_per_wg < n ? r0 + rows_per_wg : n;
-  constexpr int RP = 512 / FC;  // rows handled per pass by the block
+  constexpr int RP = KU_THREADS / FC;  // rows handled per pass by the block
   const int c = tid % FC, rs = tid / FC;
   const bool colok = c0 + c < f;
   const bool counter = (cblk == 0) && (c == 0);
   int64_t i = r0 + rs;
-  // unrolled by 4 rows per thread for memory-level parallelism
-  for (; i + 3 * RP < r1; i += 4 * RP) {
-    int lab[4];
-    float v[4];
+  for (; i + (KU_UNROLL - 1) * RP < r1; i += KU_UNROLL * RP) {
+    int lab[KU_UNROLL];
+    float v[KU_UNROLL];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < KU_UNROLL; ++u) {
       const int64_t r = i + u * RP;
       lab[u] = labels[r];
       v[u] = colok ? X[r * ldx + c0 + c] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < KU_UNROLL; ++u) {
       atomicAdd(&lsum[lab[u] * FC + c], v[u]);
       if (counter) atomicAdd(&lcnt[lab[u]], 1.f);
     }
@@ -238,13 +241,13 @@ __global__ __launch_bounds__(512) void km_update(const float* __restrict__ X, in
     if (counter) atomicAdd(&lcnt[lab], 1.f);
   }
   __syncthreads();
-  for (int e = tid; e < k * FC; e += 512) {
+  for (int e = tid; e < k * FC; e += KU_THREADS) {
     const int kk = e / FC, cc = e % FC;
     const float v = lsum[e];
     if (v != 0.f && c0 + cc < f) atomicAdd(&sums[(int64_t)kk * f + c0 + cc], v);
   }
   if (cblk == 0) {
-    for (int e = tid; e < k; e += 512) {
+    for (int e = tid; e < k; e += KU_THREADS) {
       const float v = lcnt[e];
       if (v != 0.f) atomicAdd(&counts[e], v);
     }
@@ -320,7 +323,7 @@ HA_EXPORT int ha_km_update(const float* X, int64_t n, int f, int64_t ldx, const 
   const int ncb = (f + fc - 1) / fc;
   const size_t lds = ((size_t)k * fc + k) * sizeof(float);
   // one resident workgroup per CU (LDS-bound); enough row ranges to cover the chip
-  int64_t wgs_per_cb = (int64_t)num_cus * (lds <= 48 * 1024 ? 3 : 1) / ncb;
+  int64_t wgs_per_cb = (int64_t)num_cus * (lds <= 72 * 1024 ? 2 : 1) / ncb;
   if (wgs_per_cb < 1) wgs_per_cb = 1;
   int64_t rows = (n + wgs_per_cb - 1) / wgs_per_cb;
   if (rows < 512) rows = 512;
@@ -330,11 +333,11 @@ HA_EXPORT int ha_km_update(const float* X, int64_t n, int f, int64_t ldx, const 
   switch (fc) { case 4: HA_KU(4); break; case 8: HA_KU(8); break; case 16: HA_KU(16); break; case 32: HA_KU(32); break; case 64: HA_KU(64); break; }
 #undef HA_KU
   switch (fc) {
-    case 4: hipLaunchKernelGGL(km_update<4>, grid, dim3(512), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 8: hipLaunchKernelGGL(km_update<8>, grid, dim3(512), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 16: hipLaunchKernelGGL(km_update<16>, grid, dim3(512), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 32: hipLaunchKernelGGL(km_update<32>, grid, dim3(512), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 64: hipLaunchKernelGGL(km_update<64>, grid, dim3(512), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
+    case 4: hipLaunchKernelGGL(km_update<4>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
+    case 8: hipLaunchKernelGGL(km_update<8>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
+    case 16: hipLaunchKernelGGL(km_update<16>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
+    case 32: hipLaunchKernelGGL(km_update<32>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
+    case 64: hipLaunchKernelGGL(km_update<64>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
     default: return HA_UNSUPPORTED;
   }
   return ha_launch_status();

@@ -1,0 +1,94 @@
+// Lasso cyclic coordinate descent on CDNA4 (reference heat/regression/lasso.py:121-175).
+//
+// The reference recomputes the full prediction x @ theta for EVERY coordinate (O(m n^2) per
+// sweep) and syncs the host ~3 times per coordinate.  Here the residual r = y - X theta is kept
+// on the device and the features are stored transposed (one contiguous row per feature), so one
+// coordinate step is ONE fused pass:  r -= delta_{j-1} * X_{j-1}  and  partial += X_j . r
+// (coalesced 16-byte loads), then a one-thread update applies the (reference-identical) rule
+//   rho = <X_j, r>/m + theta_j * <X_j, X_j>/m ;  theta_j = rho (intercept) | soft(rho, lambda)
+// without any host round trip.  Distributed rows add ONE scalar all-reduce between the two.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void lasso_pass(const float* __restrict__ xt, int64_t m, int64_t ldxt, int jprev,
+                                                  int jnext, const float* __restrict__ delta, float* __restrict__ r,
+                                                  float* __restrict__ partial) {
+  const float d = (jprev >= 0) ? *delta : 0.f;
+  const float* xp = jprev >= 0 ? xt + (int64_t)jprev * ldxt : nullptr;
+  const float* xn = jnext >= 0 ? xt + (int64_t)jnext * ldxt : nullptr;
+  float acc = 0.f;
+  const int64_t nv = m / 4;
+  const bool vec = ((ldxt & 3) == 0) && ((reinterpret_cast<uintptr_t>(r) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(xt) & 15) == 0);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t tail0 = 0;
+  if (vec) {
+    floatx4* r4 = reinterpret_cast<floatx4*>(r);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nv; q += stride) {
+      floatx4 rv = r4[q];
+      if (xp) {
+        const floatx4 a = reinterpret_cast<const floatx4*>(xp)[q];
+        rv = rv - d * a;
+        r4[q] = rv;
+      }
+      if (xn) {
+        const floatx4 b = reinterpret_cast<const floatx4*>(xn)[q];
+        acc = fmaf(b[0], rv[0], acc);
+        acc = fmaf(b[1], rv[1], acc);
+        acc = fmaf(b[2], rv[2], acc);
+        acc = fmaf(b[3], rv[3], acc);
+      }
+    }
+    tail0 = nv * 4;
+  }
+  for (int64_t i = tail0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    float rv = r[i];
+    if (xp) {
+      rv -= d * xp[i];
+      r[i] = rv;
+    }
+    if (xn) acc = fmaf(xn[i], rv, acc);
+  }
+  if (xn) {
+    acc = ha_wave_sum(acc);
+    __shared__ float sh[4];
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(partial, sh[0] + sh[1] + sh[2] + sh[3]);
+  }
+}
+
+__global__ void lasso_update(float* __restrict__ theta, int j, float* __restrict__ partial,
+                             const float* __restrict__ colsq, float lam, float inv_m, float* __restrict__ delta,
+                             int intercept) {
+  const float old = theta[j];
+  const float rho = partial[0] * inv_m + old * colsq[j];
+  float nw;
+  if (intercept) nw = rho;
+  else nw = rho < -lam ? rho + lam : (rho > lam ? rho - lam : 0.f);
+  theta[j] = nw;
+  *delta = nw - old;
+  partial[0] = 0.f;
+}
+
+}  // namespace
+
+HA_EXPORT int ha_lasso_pass(const float* xt, int64_t m, int64_t ldxt, int jprev, int jnext, const float* delta,
+                            float* r, float* partial, int num_cus, void* stream) {
+  if (m <= 0 && jnext < 0) return HA_OK;
+  int64_t blocks = (m / 4 + 255) / 256;
+  const int64_t cap = (int64_t)num_cus * 4;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(lasso_pass, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, xt, m, ldxt, jprev, jnext,
+                     delta, r, partial);
+  return ha_launch_status();
+}
+
+HA_EXPORT int ha_lasso_update(float* theta, int j, float* partial, const float* colsq, float lam, float inv_m,
+                              float* delta, int intercept, void* stream) {
+  hipLaunchKernelGGL(lasso_update, dim3(1), dim3(1), 0, (hipStream_t)stream, theta, j, partial, colsq, lam, inv_m,
+                     delta, intercept);
+  return ha_launch_status();
+}

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["kmeans_assign", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist"]
+__all__ = ["kmeans_assign", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch"]
 
 _NUM_CUS = {}
 
@@ -230,3 +230,46 @@ def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: fl
         out.copy_(res)
         return out
     return res
+
+
+# --------------------------------------------------------------------------------------------- lasso
+def lasso_epoch(XT: torch.Tensor, r: torch.Tensor, theta: torch.Tensor, colsq: torch.Tensor, lam: float,
+                m_global: int, allreduce=None):
+    """One cyclic coordinate-descent sweep over all features (in place on ``r`` and ``theta``).
+
+    ``XT`` [n_features, m_local] (features contiguous), ``r`` residual [m_local], ``theta`` [n],
+    ``colsq`` = <X_j, X_j>/m [n]. ``allreduce(t)`` sums a 1-element device tensor over the ranks
+    (None for a single process). Feature 0 is the intercept column (not thresholded)."""
+    n = XT.shape[0]
+    m = XT.shape[1]
+    inv_m = 1.0 / float(m_global)
+    if use_native(XT) and XT.dtype == torch.float32:
+        L = lib()
+        s = ctypes.c_void_p(stream_ptr(XT.device))
+        partial = torch.zeros(1, dtype=torch.float32, device=XT.device)
+        delta = torch.zeros(1, dtype=torch.float32, device=XT.device)
+        ncu = num_cus(XT.device)
+        for j in range(n):
+            check(L.ha_lasso_pass(_ptr(XT), m, XT.stride(0), j - 1, j, _ptr(delta), _ptr(r), _ptr(partial), ncu, s),
+                  "ha_lasso_pass")
+            if allreduce is not None:
+                allreduce(partial)
+            check(L.ha_lasso_update(_ptr(theta), j, _ptr(partial), _ptr(colsq), ctypes.c_float(lam),
+                                    ctypes.c_float(inv_m), _ptr(delta), 1 if j == 0 else 0, s), "ha_lasso_update")
+        # apply the last coordinate's change to the residual
+        check(L.ha_lasso_pass(_ptr(XT), m, XT.stride(0), n - 1, -1, _ptr(delta), _ptr(r), _ptr(partial), ncu, s),
+              "ha_lasso_pass")
+        return
+    for j in range(n):
+        xj = XT[j]
+        p = (xj * r).sum().reshape(1)
+        if allreduce is not None:
+            allreduce(p)
+        old = theta[j].clone()
+        rho = p[0] * inv_m + old * colsq[j]
+        if j == 0:
+            new = rho
+        else:
+            new = torch.where(rho < -lam, rho + lam, torch.where(rho > lam, rho - lam, torch.zeros_like(rho)))
+        theta[j] = new
+        r -= (new - old) * xj

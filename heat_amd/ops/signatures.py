@@ -9,5 +9,7 @@ SIGNATURES = {
                          c_float, c_void_p]),
     "ha_threefry_fill": (c_int, [c_void_p, c_int64, c_int64, c_uint64, c_uint64, c_uint64, c_int, c_int, c_double,
                                  c_double, c_void_p]),
-    "ha_lasso_cd_epoch": (c_int, [c_void_p]),
+    "ha_lasso_pass": (c_int, [c_void_p, c_int64, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                              c_void_p]),
+    "ha_lasso_update": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p, c_int, c_void_p]),
 }

@@ -1,2 +1,114 @@
-"""Lasso placeholder (filled in below)."""
-__all__ = []
+"""
+Lasso regression by cyclic coordinate descent (reference ``heat/regression/lasso.py``: ``Lasso`` 10,
+``soft_threshold`` 90, ``rmse`` 108, ``fit`` 121-175, ``predict`` 177).
+
+Same objective, same update rule (feature 0 is the intercept column and is not thresholded), but
+O(m n) per sweep instead of O(m n^2): the residual stays on the device and every coordinate is
+one fused native pass (``ops.lasso_epoch``) plus, for split data, one scalar all-reduce.
+"""
+from __future__ import annotations
+
+from typing import Optional, Union
+
+import torch
+
+from .. import core as ht
+from ..core.base import BaseEstimator, RegressionMixin
+from ..core.communication import MPI
+from ..core.dndarray import DNDarray
+from .. import ops
+
+__all__ = ["Lasso"]
+
+
+class Lasso(RegressionMixin, BaseEstimator):
+    """Least absolute shrinkage and selection operator: min 1/(2m)|y - Xw|^2 + lam |w_1:|_1."""
+
+    def __init__(self, lam: Optional[float] = 0.1, max_iter: Optional[int] = 100, tol: Optional[float] = 1e-6) -> None:
+        self.__lam = lam
+        self.max_iter = max_iter
+        self.tol = tol
+        self.__theta = None
+        self.n_iter = None
+
+    @property
+    def coef_(self) -> Optional[DNDarray]:
+        return None if self.__theta is None else self.__theta[1:]
+
+    @property
+    def intercept_(self) -> Optional[DNDarray]:
+        return None if self.__theta is None else self.__theta[0]
+
+    @property
+    def lam(self) -> float:
+        return self.__lam
+
+    @lam.setter
+    def lam(self, arg: float) -> None:
+        self.__lam = arg
+
+    @property
+    def theta(self) -> Optional[DNDarray]:
+        return self.__theta
+
+    def soft_threshold(self, rho):
+        """Soft-threshold operator ``S(rho, lam)``."""
+        lam = self.__lam
+        if isinstance(rho, DNDarray):
+            rho = rho.item()
+        if rho < -lam:
+            return rho + lam
+        if rho > lam:
+            return rho - lam
+        return 0.0
+
+    def rmse(self, gt: DNDarray, yest: DNDarray) -> float:
+        """Root mean square error between two arrays."""
+        return float(ht.sqrt(ht.mean((gt - yest) ** 2)).item())
+
+    def fit(self, x: DNDarray, y: DNDarray) -> None:
+        """Coordinate descent until the RMS change of theta is below ``tol`` or ``max_iter`` sweeps."""
+        if y.ndim > 2:
+            raise ValueError("y.ndim must <= 2, currently: {}".format(y.ndim))
+        if x.ndim != 2:
+            raise ValueError("X.ndim must == 2, currently: {}".format(x.ndim))
+        if x.split not in (None, 0):
+            raise NotImplementedError("Lasso supports split=None or split=0 inputs")
+        m, n = x.gshape
+        X = x.larray
+        if not X.is_floating_point():
+            X = X.float()
+        tt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
+        X = X.to(tt)
+        yl = y.larray.reshape(-1).to(tt)
+        if y.split is None and x.is_distributed():
+            counts, displs = x.counts_displs()
+            r0 = displs[x.comm.rank]
+            yl = yl[r0: r0 + counts[x.comm.rank]]
+        dist = x.is_distributed()
+        XT = X.t().contiguous()                               # [n, m_local]: features contiguous
+        colsq = (XT * XT).sum(1)
+        if dist:
+            x.comm.Allreduce(MPI.IN_PLACE, colsq, MPI.SUM)
+        colsq = colsq / m
+        theta = torch.zeros(n, dtype=tt, device=X.device)
+        r = yl.clone()                                        # residual y - X theta (theta = 0)
+
+        def allreduce(t):
+            x.comm.Allreduce(MPI.IN_PLACE, t, MPI.SUM)
+
+        i = 0
+        for i in range(self.max_iter):
+            theta_old = theta.clone()
+            ops.lasso_epoch(XT, r, theta, colsq, float(self.__lam), m, allreduce if dist else None)
+            if self.tol is not None:
+                diff = float(torch.sqrt(torch.mean((theta - theta_old) ** 2)))
+                if diff < self.tol:
+                    break
+        self.n_iter = i + 1
+        self.__theta = DNDarray(theta.reshape(n, 1), (n, 1), ht.types.canonical_heat_type(tt), None, x.device, x.comm,
+                                True)
+
+    def predict(self, x: DNDarray) -> DNDarray:
+        """``x @ theta`` (the first column of x multiplies the intercept)."""
+        return ht.matmul(x, self.__theta.astype(x.dtype) if x.dtype != self.__theta.dtype else self.__theta)

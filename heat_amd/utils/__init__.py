@@ -1,1 +1,3 @@
-"""Utilities (reference ``heat/utils``)."""
+"""Utilities (reference ``heat/utils``): data loading helpers and vision transforms."""
+from . import data
+from . import vision_transforms

@@ -326,3 +326,129 @@ def check_io_csv():
     y = ht.load(p2, split=0)
     assert_array_equal(y, data)
     comm.Barrier()
+
+
+# ---------------------------------------------------------------------------------------------
+# estimators / nn / data (reference: heat/regression/lasso/tests, heat/naive_bayes/tests,
+# heat/classification/tests, heat/nn/tests, heat/optim/tests, heat/utils/data/tests)
+# ---------------------------------------------------------------------------------------------
+def _blobs(n_per, centers, seed=0, scale=0.3):
+    rng = _rng(seed)
+    X = np.concatenate([rng.normal(c, scale, size=(n_per, len(c))) for c in centers]).astype(np.float32)
+    y = np.repeat(np.arange(len(centers)), n_per)
+    return X, y
+
+
+def check_lasso():
+    rng = _rng(3)
+    m, n = 240, 6
+    X = rng.normal(size=(m, n)).astype(np.float32)
+    X[:, 0] = 1.0
+    X /= np.sqrt((X ** 2).mean(0))          # the reference's update assumes unit mean-square columns
+    w = np.array([0.5, 2.0, 0.0, -1.5, 0.0, 0.7], np.float32)
+    y = (X @ w + 0.01 * rng.normal(size=m)).astype(np.float32)
+    thetas = []
+    for split in (None, 0):
+        est = ht.regression.Lasso(lam=0.01, max_iter=200, tol=1e-7)
+        est.fit(ht.array(X, split=split), ht.array(y[:, None], split=split))
+        th = est.theta.numpy().ravel()
+        thetas.append(th)
+        pred = est.predict(ht.array(X, split=split)).numpy().ravel()
+        assert np.sqrt(np.mean((pred - y) ** 2)) < 0.05
+    assert np.allclose(thetas[0], thetas[1], atol=1e-4)
+    assert abs(thetas[0][2]) < 0.02 and abs(thetas[0][4]) < 0.02       # sparsity of the zero weights
+    assert np.allclose(thetas[0], w, atol=0.05)
+
+
+def check_gaussian_nb():
+    from sklearn.naive_bayes import GaussianNB as SkNB
+
+    X, y = _blobs(40, [(0, 0, 0), (2, 2, 0), (0, 3, 3)], seed=5, scale=0.8)
+    sk = SkNB().fit(X, y)
+    for split in (None, 0):
+        nb = ht.naive_bayes.GaussianNB()
+        nb.fit(ht.array(X, split=split), ht.array(y, split=split))
+        assert np.allclose(nb.theta_.numpy(), sk.theta_, atol=1e-4)
+        assert np.allclose(nb.var_.numpy() if hasattr(nb, "var_") else nb.sigma_.numpy(), sk.var_, rtol=1e-3,
+                           atol=1e-5)
+        pred = nb.predict(ht.array(X, split=split)).numpy()
+        assert np.array_equal(pred, sk.predict(X))
+        proba = nb.predict_proba(ht.array(X, split=split)).numpy()
+        assert np.allclose(proba, sk.predict_proba(X), atol=1e-4)
+
+
+def check_knn():
+    from sklearn.neighbors import KNeighborsClassifier as SkKNN
+
+    X, y = _blobs(30, [(0, 0), (3, 0), (0, 3)], seed=7, scale=1.0)
+    Q = _rng(8).normal(1.0, 1.5, size=(25, 2)).astype(np.float32)
+    sk = SkKNN(n_neighbors=5).fit(X, y)
+    for split in (None, 0):
+        knn = ht.classification.KNeighborsClassifier(n_neighbors=5)
+        knn.fit(ht.array(X, split=split), ht.array(y, split=split))
+        pred = knn.predict(ht.array(Q, split=split)).numpy().ravel()
+        assert (pred == sk.predict(Q)).mean() > 0.95
+
+
+def check_kmedians_kmedoids_spectral():
+    X, y = _blobs(30, [(0, 0), (6, 6), (-6, 6)], seed=9, scale=0.5)
+    for cls in (ht.cluster.KMedians, ht.cluster.KMedoids):
+        est = cls(n_clusters=3, init="kmeans++", random_state=1)
+        labels = est.fit_predict(ht.array(X, split=0)).numpy().ravel()
+        for c in range(3):
+            assert len(np.unique(labels[y == c])) == 1
+        assert len(np.unique(labels)) == 3
+    sp = ht.cluster.Spectral(n_clusters=3, gamma=0.5, metric="rbf", laplacian="fully_connected", n_lanczos=40)
+    labels = sp.fit_predict(ht.array(X, split=0)).numpy().ravel()
+    assert len(np.unique(labels)) == 3
+    for c in range(3):
+        assert len(np.unique(labels[y == c])) == 1
+
+
+def check_data_parallel():
+    comm = ht.MPI_WORLD
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.ReLU(), torch.nn.Linear(8, 1))
+    opt = ht.optim.DataParallelOptimizer(torch.optim.SGD(net.parameters(), lr=0.1), blocking=True)
+    dp = ht.nn.DataParallel(net, comm, opt, blocking_parameter_updates=True, bucket_cap_mb=0.0001)
+    ref = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.ReLU(), torch.nn.Linear(8, 1))
+    ref.load_state_dict(net.state_dict())
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(1)
+    per = 6
+    for _ in range(3):
+        Xg = torch.randn(per * comm.size, 4, generator=g)
+        yg = torch.randn(per * comm.size, 1, generator=g)
+        Xl, yl = Xg[comm.rank * per:(comm.rank + 1) * per], yg[comm.rank * per:(comm.rank + 1) * per]
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(dp(Xl), yl).backward()
+        opt.step()
+        ref_opt.zero_grad()
+        torch.nn.functional.mse_loss(ref(Xg), yg).backward()
+        ref_opt.step()
+    for p, q in zip(net.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, atol=1e-5), (p, q)
+
+
+def check_dataloader_shuffle():
+    comm = ht.MPI_WORLD
+    n = 8 * comm.size          # Dataset keeps gshape // size rows per rank (reference semantics)
+    data = ht.array(np.arange(n * 2, dtype=np.float32).reshape(n, 2), split=0)
+    ds = ht.utils.data.Dataset(data)
+    loader = ht.utils.data.DataLoader(ds, batch_size=4)
+    for _epoch in range(3):
+        seen = torch.cat([b for b in loader]) if len(loader) else torch.empty(0, 2)
+        assert seen.shape[0] == data.lshape[0]
+        allrows = np.concatenate(comm.allgather(seen.numpy()))
+        assert sorted(allrows[:, 0].tolist()) == list(np.arange(0, 2 * n, 2, dtype=np.float32))
+
+
+def check_tiling():
+    a = ht.zeros((7, 5, 6), split=1)
+    t = ht.tiling.SplitTiles(a)
+    assert tuple(t.tile_dimensions.sum(dim=1).tolist()) == (7, 5, 6)
+    assert t.tile_locations.shape == (a.comm.size,) * 3
+    m = ht.zeros((12, 9), split=0)
+    sq = ht.tiling.SquareDiagTiles(m, tiles_per_proc=2)
+    assert sum(sq.row_indices[i + 1] - sq.row_indices[i] for i in range(len(sq.row_indices) - 1)) <= 12
+    assert sq.tile_rows >= 2
