@@ -35,6 +35,20 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         self._labels = None
         self._inertia = None
         self._n_iter = None
+        # "fast": fp16x3 split assignment (fp32-GEMM accuracy, points packed once per fit);
+        # "exact": bit-exact fp32 (f32-input MFMA) assignment
+        self.precision = "fast"
+        self._pack_cache = None
+
+    def _packed(self, X: torch.Tensor):
+        """fp16x3 planes of the local points, cached while X is unchanged (None: exact path)."""
+        if self.precision != "fast" or not X.is_cuda:
+            return None
+        key = ops.kernels._points_key(X)
+        if self._pack_cache is None or self._pack_cache.key != key:
+            self._pack_cache = None
+            self._pack_cache = ops.kmeans_pack_points(X)
+        return self._pack_cache
 
     @property
     def cluster_centers_(self) -> DNDarray:
@@ -123,7 +137,9 @@ class _KCluster(ClusteringMixin, BaseEstimator):
 
     def _assign_to_cluster(self, x: DNDarray) -> DNDarray:
         """(n, 1) int64 labels of the nearest centroid (split like ``x``)."""
-        labels, _ = ops.kmeans_assign(x.larray, self._cluster_centers.larray.to(x.larray.device), want_mind=False)
+        X = x.larray
+        labels, _ = ops.kmeans_assign(X, self._cluster_centers.larray.to(X.device), want_mind=False,
+                                      packed=self._packed(X) if X.dtype == torch.float32 else None)
         lab = labels.to(torch.int64).reshape(-1, 1)
         return DNDarray(lab, (x.gshape[0], 1), ht.int64, x.split, x.device, x.comm, x.balanced)
 

@@ -30,9 +30,9 @@ _SIGNATURES = {
     "ha_km_workspace_floats": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "ha_km_assign": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_int64, c_void_p, c_void_p,
                              c_void_p, c_void_p]),
-    "ha_km_update_fc": (c_int, [c_int, c_int]),
-    "ha_km_update": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int,
-                             c_void_p]),
+    "ha_km_update_workspace": (c_int64, [c_int64, c_int, c_int, c_int]),
+    "ha_km_update": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                             c_int, c_void_p]),
     "ha_moments_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     "ha_moments_cols": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
 }

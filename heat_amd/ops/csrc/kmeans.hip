@@ -1,5 +1,5 @@
 // K-means on CDNA4 (gfx950): fused assignment (distance GEMM + running argmin, the n x k distance
-// matrix is never materialised) and a one-pass centroid update with LDS-privatised sums.
+// matrix is never materialised) and a counting-sort centroid update (one gather pass over X).
 //
 // Replaces the reference's cdist + argmin (heat/cluster/_kcluster.py:196-209) and its k-pass
 // update loop with 2k all-reduces (heat/cluster/kmeans.py:73-100).
@@ -193,64 +193,145 @@ __global__ __launch_bounds__(256, 2) void km_assign(const float* __restrict__ X,
   }
 }
 
-// One pass over the points: per-(centroid, column) sums in LDS (ds_add_f32), counts in LDS,
-// flushed once per workgroup with coalesced global float atomics (256 contiguous bytes per
-// wave instruction).  Grid = (row ranges, column blocks of FC columns).  1024 threads and 8 rows
-// per thread in flight keep ~64 KB of loads outstanding per CU (the kernel is HBM-bound; at one
-// workgroup per CU the first version was latency-bound at ~0.8 TB/s).
-constexpr int KU_THREADS = 1024;
-constexpr int KU_UNROLL = 8;
-template <int FC>
-__global__ __launch_bounds__(KU_THREADS) void km_update(const float* __restrict__ X, int64_t n, int f, int64_t ldx,
-                                                        const int* __restrict__ labels, int k, int64_t rows_per_wg,
-                                                        float* __restrict__ sums, float* __restrict__ counts) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* lsum = lds;                    // [k][FC]
-  float* lcnt = lds + (int64_t)k * FC;  // [k]
-  const int tid = threadIdx.x;
-  for (int e = tid; e < k * FC + k; e += KU_THREADS) lds[e] = 0.f;
+// ---------------------------------------------------------------------------------- update
+// Centroid sums by COUNTING SORT instead of scattered float atomics.  Measured on MI355X
+// (tools/microbench/ku_bench.hip): LDS float atomics (ds_add_f32) retire at ~1 lane per 3 clocks
+// per CU whatever the address pattern, so an LDS-privatised update of 12.5M x 64 points took
+// 3.9 ms (0.8 TB/s).  Integer LDS atomics on 4-byte labels are cheap, so:
+//   1. ku_hist     per-block label histograms            (labels read once, LDS int atomics)
+//   2. ku_scan_blk per-cluster exclusive prefix over blocks
+//   3. ku_scan_tot exclusive prefix over clusters -> cluster start offsets, counts
+//   4. ku_scatter  row ids into cluster order            (labels read again, 4-byte scatter)
+//   5. ku_gather   each workgroup streams a contiguous chunk of the sorted order, gathering
+//                  whole 256-byte rows of X and summing in registers; a thread flushes its
+//                  running sum with one global atomic when the cluster changes (~2 per thread).
+// X is read exactly once, as full rows.  Out-of-range labels are ignored.
+constexpr int KU_BLOCK = 1024;     // threads of hist/scatter blocks
+constexpr int KU_CHUNK = 2048;     // sorted positions per gather workgroup
+constexpr int KU_RU = 8;           // rows in flight per gather thread
+
+__global__ __launch_bounds__(KU_BLOCK) void ku_hist(const int* __restrict__ lab, int64_t n, int k,
+                                                    int64_t rows_per_blk, int* __restrict__ hist) {
+  extern __shared__ int h[];
+  for (int e = threadIdx.x; e < k; e += KU_BLOCK) h[e] = 0;
   __syncthreads();
-  const int cblk = blockIdx.y;
-  const int c0 = cblk * FC;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
-  const int64_t r1 = r0 + rows_per_wg < n ? r0 + rows_per_wg : n;
-  constexpr int RP = KU_THREADS / FC;  // rows handled per pass by the block
-  const int c = tid % FC, rs = tid / FC;
-  const bool colok = c0 + c < f;
-  const bool counter = (cblk == 0) && (c == 0);
-  int64_t i = r0 + rs;
-  for (; i + (KU_UNROLL - 1) * RP < r1; i += KU_UNROLL * RP) {
-    int lab[KU_UNROLL];
-    float v[KU_UNROLL];
-#pragma unroll
-    for (int u = 0; u < KU_UNROLL; ++u) {
-      const int64_t r = i + u * RP;
-      lab[u] = labels[r];
-      v[u] = colok ? X[r * ldx + c0 + c] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < KU_UNROLL; ++u) {
-      atomicAdd(&lsum[lab[u] * FC + c], v[u]);
-      if (counter) atomicAdd(&lcnt[lab[u]], 1.f);
-    }
-  }
-  for (; i < r1; i += RP) {
-    const int lab = labels[i];
-    const float v = colok ? X[i * ldx + c0 + c] : 0.f;
-    atomicAdd(&lsum[lab * FC + c], v);
-    if (counter) atomicAdd(&lcnt[lab], 1.f);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  const int64_t r1 = r0 + rows_per_blk < n ? r0 + rows_per_blk : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += KU_BLOCK) {
+    const int l = lab[i];
+    if ((unsigned)l < (unsigned)k) atomicAdd(&h[l], 1);
   }
   __syncthreads();
-  for (int e = tid; e < k * FC; e += KU_THREADS) {
-    const int kk = e / FC, cc = e % FC;
-    const float v = lsum[e];
-    if (v != 0.f && c0 + cc < f) atomicAdd(&sums[(int64_t)kk * f + c0 + cc], v);
+  for (int e = threadIdx.x; e < k; e += KU_BLOCK) hist[(int64_t)blockIdx.x * k + e] = h[e];
+}
+
+__global__ __launch_bounds__(256) void ku_scan_blk(int* __restrict__ hist, int nblk, int k, int* __restrict__ total) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= k) return;
+  int run = 0;
+  for (int b = 0; b < nblk; ++b) {
+    const int v = hist[(int64_t)b * k + c];
+    hist[(int64_t)b * k + c] = run;
+    run += v;
   }
-  if (cblk == 0) {
-    for (int e = tid; e < k; e += KU_THREADS) {
-      const float v = lcnt[e];
-      if (v != 0.f) atomicAdd(&counts[e], v);
+  total[c] = run;
+}
+
+__global__ __launch_bounds__(1024) void ku_scan_tot(const int* __restrict__ total, int k, int* __restrict__ cstart,
+                                                    float* __restrict__ counts) {
+  __shared__ int sh[1024];
+  const int per = (k + 1023) / 1024;
+  const int t = threadIdx.x;
+  int loc = 0;
+  for (int j = 0; j < per; ++j) {
+    const int c = t * per + j;
+    if (c < k) loc += total[c];
+  }
+  sh[t] = loc;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? sh[t - off] : 0;
+    __syncthreads();
+    sh[t] += v;
+    __syncthreads();
+  }
+  int run = sh[t] - loc;
+  for (int j = 0; j < per; ++j) {
+    const int c = t * per + j;
+    if (c < k) {
+      cstart[c] = run;
+      counts[c] = (float)total[c];
+      run += total[c];
     }
+  }
+  if (t == 1023) cstart[k] = sh[1023];
+}
+
+__global__ __launch_bounds__(KU_BLOCK) void ku_scatter(const int* __restrict__ lab, int64_t n, int k,
+                                                       int64_t rows_per_blk, const int* __restrict__ hist,
+                                                       const int* __restrict__ cstart, int* __restrict__ order) {
+  extern __shared__ int h[];
+  for (int e = threadIdx.x; e < k; e += KU_BLOCK) h[e] = cstart[e] + hist[(int64_t)blockIdx.x * k + e];
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  const int64_t r1 = r0 + rows_per_blk < n ? r0 + rows_per_blk : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += KU_BLOCK) {
+    const int l = lab[i];
+    if ((unsigned)l < (unsigned)k) order[atomicAdd(&h[l], 1)] = (int)i;
+  }
+}
+
+// 256 threads = 64 columns x 4 row lanes; columns beyond 64 in further passes.
+__global__ __launch_bounds__(256) void ku_gather(const float* __restrict__ X, int f, int64_t ldx,
+                                                 const int* __restrict__ order, const int* __restrict__ cstart, int k,
+                                                 float* __restrict__ sums) {
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int64_t nvalid = cstart[k];
+  const int64_t p0 = (int64_t)blockIdx.x * KU_CHUNK;
+  const int64_t p1 = p0 + KU_CHUNK < nvalid ? p0 + KU_CHUNK : nvalid;
+  const int64_t p = p0 + rl;
+  if (p >= p1) return;
+  int lo = 0, hi = k - 1;  // cluster of position p: last c with cstart[c] <= p
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cstart[mid + 1] > p) hi = mid; else lo = mid + 1;
+  }
+  for (int cb = 0; cb < f; cb += 64) {
+    const int col = cb + c;
+    const bool ok = col < f;
+    int cur = lo;
+    int64_t nb = cstart[cur + 1];
+    float acc = 0.f;
+    int64_t q = p;
+    for (; q + (KU_RU - 1) * 4 < p1; q += KU_RU * 4) {
+      int idx[KU_RU];
+      float v[KU_RU];
+#pragma unroll
+      for (int u = 0; u < KU_RU; ++u) idx[u] = order[q + u * 4];
+#pragma unroll
+      for (int u = 0; u < KU_RU; ++u) v[u] = ok ? X[(int64_t)idx[u] * ldx + col] : 0.f;
+#pragma unroll
+      for (int u = 0; u < KU_RU; ++u) {
+        while (q + u * 4 >= nb) {
+          if (ok) atomicAdd(&sums[(int64_t)cur * f + col], acc);
+          acc = 0.f;
+          ++cur;
+          nb = cstart[cur + 1];
+        }
+        acc += v[u];
+      }
+    }
+    for (; q < p1; q += 4) {
+      const float v = ok ? X[(int64_t)order[q] * ldx + col] : 0.f;
+      while (q >= nb) {
+        if (ok) atomicAdd(&sums[(int64_t)cur * f + col], acc);
+        acc = 0.f;
+        ++cur;
+        nb = cstart[cur + 1];
+      }
+      acc += v;
+    }
+    if (ok) atomicAdd(&sums[(int64_t)cur * f + col], acc);
   }
 }
 
@@ -303,42 +384,56 @@ HA_EXPORT int ha_km_assign(const float* X, int64_t n, int f, int64_t ldx, const 
   return ha_launch_status();
 }
 
-// Largest power-of-two column block whose [k][FC] sums + [k] counts fit in LDS.
-HA_EXPORT int ha_km_update_fc(int k, int f) {
-  const int64_t budget = 160 * 1024 - 1024;
-  int fc = 64;
-  while (fc >= 4 && (int64_t)k * (fc + 1) * 4 > budget) fc >>= 1;
-  if (fc < 4) return -1;
-  while (fc > 4 && fc / 2 >= f) fc >>= 1;
-  return fc;
+static void ku_grid(int64_t n, int64_t* nblk, int64_t* rows_per_blk) {
+  int64_t rows = 16384;  // >= 16 rows per thread amortises the LDS histogram setup
+  int64_t nb = (n + rows - 1) / rows;
+  if (nb > 512) {
+    nb = 512;
+    rows = (n + nb - 1) / nb;
+  }
+  if (nb < 1) nb = 1;
+  *nblk = nb;
+  *rows_per_blk = rows;
 }
 
-// sums [k][f] and counts [k] must be zeroed by the caller (stream-ordered memset).
+// int32 scratch ha_km_update needs (-1: unsupported k).
+HA_EXPORT int64_t ha_km_update_workspace(int64_t n, int k, int f, int num_cus) {
+  (void)f;
+  (void)num_cus;
+  if (k <= 0 || (int64_t)k * 4 > 150 * 1024 || n >= (int64_t)1 << 31) return -1;
+  int64_t nblk, rows;
+  ku_grid(n, &nblk, &rows);
+  return n + nblk * k + k + (k + 1);
+}
+
+// sums [k][f] and counts [k] are written completely.
 HA_EXPORT int ha_km_update(const float* X, int64_t n, int f, int64_t ldx, const int* labels, int k, float* sums,
-                           float* counts, int num_cus, void* stream) {
-  if (n <= 0) return HA_OK;
-  const int fc = ha_km_update_fc(k, f);
-  if (fc < 0) return HA_UNSUPPORTED;
+                           float* counts, int* workspace, int num_cus, void* stream) {
+  (void)num_cus;
   hipStream_t s = (hipStream_t)stream;
-  const int ncb = (f + fc - 1) / fc;
-  const size_t lds = ((size_t)k * fc + k) * sizeof(float);
-  // one resident workgroup per CU (LDS-bound); enough row ranges to cover the chip
-  int64_t wgs_per_cb = (int64_t)num_cus * (lds <= 72 * 1024 ? 2 : 1) / ncb;
-  if (wgs_per_cb < 1) wgs_per_cb = 1;
-  int64_t rows = (n + wgs_per_cb - 1) / wgs_per_cb;
-  if (rows < 512) rows = 512;
-  const int64_t npt = (n + rows - 1) / rows;
-  dim3 grid((unsigned)npt, (unsigned)ncb);
-#define HA_KU(FC_) hipFuncSetAttribute((const void*)km_update<FC_>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
-  switch (fc) { case 4: HA_KU(4); break; case 8: HA_KU(8); break; case 16: HA_KU(16); break; case 32: HA_KU(32); break; case 64: HA_KU(64); break; }
-#undef HA_KU
-  switch (fc) {
-    case 4: hipLaunchKernelGGL(km_update<4>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 8: hipLaunchKernelGGL(km_update<8>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 16: hipLaunchKernelGGL(km_update<16>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 32: hipLaunchKernelGGL(km_update<32>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    case 64: hipLaunchKernelGGL(km_update<64>, grid, dim3(KU_THREADS), lds, s, X, n, f, ldx, labels, k, rows, sums, counts); break;
-    default: return HA_UNSUPPORTED;
+  if (ha_km_update_workspace(n, k, f, num_cus) < 0) return HA_UNSUPPORTED;
+  hipMemsetAsync(sums, 0, sizeof(float) * (size_t)k * f, s);
+  if (n <= 0) {
+    hipMemsetAsync(counts, 0, sizeof(float) * (size_t)k, s);
+    return ha_launch_status();
   }
+  int64_t nblk, rows;
+  ku_grid(n, &nblk, &rows);
+  int* order = workspace;
+  int* hist = order + n;
+  int* total = hist + nblk * k;
+  int* cstart = total + k;
+  const size_t lds = (size_t)k * sizeof(int);
+  if (lds > 64 * 1024) {
+    hipFuncSetAttribute((const void*)ku_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)ku_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  }
+  hipLaunchKernelGGL(ku_hist, dim3((unsigned)nblk), dim3(KU_BLOCK), lds, s, labels, n, k, rows, hist);
+  hipLaunchKernelGGL(ku_scan_blk, dim3((k + 255) / 256), dim3(256), 0, s, hist, (int)nblk, k, total);
+  hipLaunchKernelGGL(ku_scan_tot, dim3(1), dim3(1024), 0, s, total, k, cstart, counts);
+  hipLaunchKernelGGL(ku_scatter, dim3((unsigned)nblk), dim3(KU_BLOCK), lds, s, labels, n, k, rows, hist, cstart,
+                     order);
+  hipLaunchKernelGGL(ku_gather, dim3((unsigned)((n + KU_CHUNK - 1) / KU_CHUNK)), dim3(256), 0, s, X, f, ldx, order,
+                     cstart, k, sums);
   return ha_launch_status();
 }

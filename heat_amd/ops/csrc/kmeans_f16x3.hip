@@ -1,0 +1,332 @@
+// K-means assignment on the FP16 matrix cores with a 3-term split ("f16x3"): ~fp32-GEMM accuracy
+// at 16x the per-instruction MFMA rate of the f32-input MFMA (v_mfma_f32_32x32x16_f16: 16K MACs
+// in 32 cycles/SIMD vs v_mfma_f32_32x32x2_f32: 2K MACs in 64).
+//
+// Points are scaled per row by a power of two s_x (max |x_i| in [0.5, 1)) and split once per fit
+// into fp16 hi = fp16(x s_x), lo = fp16(x s_x - hi) ("planes", cached across Lloyd iterations by
+// the caller).  Centroids use ONE power-of-two scale s_C for all of them and are packed per
+// iteration into the MFMA A-fragment image.  Per (point, centroid):
+//     D = hi_c.hi_x + hi_c.lo_x + lo_c.hi_x           (three MFMAs, fp32 accumulation)
+//       = s_x s_C x.c  up to ~3 * 2^-22 relative per product term
+//   argmin_c |c|^2 - 2 x.c  =  argmin_c  s_x * u_c - D,   u_c = s_C |c|^2 / 2
+// so the epilogue is one FMA per pair, a 16-way min per 32-centroid tile and, only when that min
+// beats the running best (rare after the first tiles), a search for its index.
+//
+// Layout and orientation follow km_assign (kmeans.hip): centroids = A (rows), points = B
+// (columns), the K dimension is permuted so lane half h owns features [h*F2, h*F2 + F2) of its
+// point and reads them as 16-byte loads; the packed centroid image in LDS is read with
+// conflict-free lane-linear ds_read_b128.
+#include "common.h"
+
+namespace {
+
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+template <int FPAD>
+struct H3Cfg {
+  static constexpr int F2 = FPAD / 2;                  // features per lane half
+  static constexpr int KS = F2 / 8;                    // k-steps (16 features each)
+  static constexpr int CB = FPAD >= 128 ? 64 : 128;    // centroids per LDS chunk
+  static constexpr int NPB = 2;                        // 32-point blocks per wave
+  static constexpr int WAVES = 4;
+  static constexpr int PTS_PER_WG = WAVES * NPB * 32;
+  static constexpr int CHUNK_H = CB * FPAD * 2;        // halfs of packed (hi, lo) per chunk
+};
+
+// planes[row][0:FPAD] = hi, planes[row][FPAD:2 FPAD] = lo; sx[row] = s_x.
+template <int FPAD>
+__global__ __launch_bounds__(256) void h3_pack_points(const float* __restrict__ X, int64_t n, int f, int64_t ldx,
+                                                      _Float16* __restrict__ planes, float* __restrict__ sx) {
+  constexpr int LPR = FPAD / 8;  // lanes per row (divides 64)
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = t / LPR;
+  const int grp = (int)(t % LPR);
+  const bool live = row < n;
+  float v[8];
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int col = grp * 8 + i;
+    v[i] = (live && col < f) ? X[row * ldx + col] : 0.f;
+    mx = fmaxf(mx, fabsf(v[i]));
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  int e = 0;
+  if (mx > 0.f && mx < __builtin_huge_valf()) frexpf(mx, &e);
+  const float s = ldexpf(1.f, -e);
+  if (!live) return;
+  halfx8 hi, lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float xs = v[i] * s;
+    const _Float16 h = (_Float16)xs;
+    hi[i] = h;
+    lo[i] = (_Float16)(xs - (float)h);
+  }
+  *reinterpret_cast<halfx8*>(planes + row * (2 * FPAD) + grp * 8) = hi;
+  *reinterpret_cast<halfx8*>(planes + row * (2 * FPAD) + FPAD + grp * 8) = lo;
+  if (grp == 0) sx[row] = s;
+}
+
+// One workgroup: global max |c| -> s_C, then the packed image
+//   image[chunk][cb][ks][hl][lane][8] (lane = h*32 + j, centroid chunk*CB + cb*32 + j,
+//   features h*F2 + 8 ks .. +8), u[c] = s_C |c|^2 / 2 (+inf for padding), meta[0] = s_C.
+template <int FPAD>
+__global__ __launch_bounds__(1024) void h3_pack_centroids(const float* __restrict__ C, int k, int f, int64_t ldc,
+                                                          int kpad, _Float16* __restrict__ image,
+                                                          float* __restrict__ u, float* __restrict__ meta) {
+  using K = H3Cfg<FPAD>;
+  __shared__ float red[1024];
+  const int tid = threadIdx.x;
+  float mx = 0.f;
+  for (int64_t e = tid; e < (int64_t)k * f; e += 1024) mx = fmaxf(mx, fabsf(C[(e / f) * ldc + e % f]));
+  red[tid] = mx;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+    __syncthreads();
+  }
+  int ex = 0;
+  if (red[0] > 0.f && red[0] < __builtin_huge_valf()) frexpf(red[0], &ex);
+  const float s = ldexpf(1.f, -ex);
+  if (tid == 0) meta[0] = s;
+  constexpr int G8 = FPAD / 8;
+  for (int64_t it = tid; it < (int64_t)kpad * G8; it += 1024) {
+    const int c = (int)(it / G8), g8 = (int)(it % G8);
+    const int fe = g8 * 8;
+    halfx8 hi, lo;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float x = (c < k && fe + i < f) ? C[(int64_t)c * ldc + fe + i] * s : 0.f;
+      const _Float16 h = (_Float16)x;
+      hi[i] = h;
+      lo[i] = (_Float16)(x - (float)h);
+    }
+    const int h = fe / K::F2, ks = (fe % K::F2) / 8;
+    const int chunk = c / K::CB, cb = (c % K::CB) / 32, j = c % 32;
+    const int lane = h * 32 + j;
+    const int64_t base = ((((int64_t)chunk * (K::CB / 32) + cb) * K::KS + ks) * 2) * 64 * 8;
+    *reinterpret_cast<halfx8*>(image + base + (int64_t)lane * 8) = hi;
+    *reinterpret_cast<halfx8*>(image + base + 64 * 8 + (int64_t)lane * 8) = lo;
+  }
+  for (int c = tid; c < kpad; c += 1024) {
+    if (c < k) {
+      float acc = 0.f;
+      for (int i = 0; i < f; ++i) {
+        const float x = C[(int64_t)c * ldc + i];
+        acc = fmaf(x, x, acc);
+      }
+      u[c] = 0.5f * s * acc;
+    } else {
+      u[c] = __builtin_huge_valf();
+    }
+  }
+}
+
+template <int FPAD>
+__global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+                                                   int64_t n, const _Float16* __restrict__ image,
+                                                   const float* __restrict__ u, const float* __restrict__ meta,
+                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
+  using K = H3Cfg<FPAD>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  constexpr int BUF_B = CHUNK_H * 2 + CB * 4;      // bytes per buffer: image + u
+  constexpr int STG = CHUNK_H * 2 / 16 / 256;      // 16-byte pieces staged per thread per chunk
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+
+  halfx8 bhi[NPB][KS], blo[NPB][KS];
+  float sx[NPB], xsq[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int64_t row = pbase + pb * 32 + j;
+    row = row < n ? row : n - 1;
+    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+      blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
+        q = fmaf(xv, xv, q);
+      }
+    }
+    sx[pb] = sxv[row];
+    xsq[pb] = q;
+  }
+  float best[NPB];
+  int bidx[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    best[pb] = __builtin_huge_valf();
+    bidx[pb] = 0;
+  }
+
+  {
+    const floatx4* src = reinterpret_cast<const floatx4*>(image);
+    floatx4* dst = reinterpret_cast<floatx4*>(smem);
+#pragma unroll
+    for (int i = 0; i < STG; ++i) dst[tid + 256 * i] = src[tid + 256 * i];
+    if (tid < CB / 4) reinterpret_cast<floatx4*>(smem + CHUNK_H * 2)[tid] = reinterpret_cast<const floatx4*>(u)[tid];
+  }
+  __syncthreads();
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const bool more = ch + 1 < nchunks;
+    floatx4 stg[STG];
+    floatx4 stn = {0.f, 0.f, 0.f, 0.f};
+    if (more) {
+      const floatx4* src = reinterpret_cast<const floatx4*>(image + (int64_t)(ch + 1) * CHUNK_H);
+#pragma unroll
+      for (int i = 0; i < STG; ++i) stg[i] = src[tid + 256 * i];
+      if (tid < CB / 4) stn = reinterpret_cast<const floatx4*>(u + (ch + 1) * CB)[tid];
+    }
+    const unsigned char* buf = smem + (ch & 1) * BUF_B;
+    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
+    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
+#pragma unroll 1
+    for (int cb = 0; cb < CB / 32; ++cb) {
+      floatx16 acc[NPB];
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) acc[pb] = (floatx16)(0.f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
+        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
+        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) {
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[pb], 0, 0, 0);
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[pb], 0, 0, 0);
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[pb], 0, 0, 0);
+        }
+      }
+      // accumulator reg r holds centroid row (r&3) + 8(r>>2) + 4h of this 32-block
+      floatx4 cn[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cn[g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = fmaf(sx[pb], cn[r >> 2][r & 3], -acc[pb][r]);
+        float m = v[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fminf(m, v[r]);
+        if (m < best[pb]) {
+          int bi = 15;
+#pragma unroll
+          for (int r = 14; r >= 0; --r) bi = v[r] == m ? r : bi;
+          best[pb] = m;
+          bidx[pb] = ch * CB + cb * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+        }
+      }
+    }
+    if (more) {
+      unsigned char* nb = smem + ((ch + 1) & 1) * BUF_B;
+      floatx4* dst = reinterpret_cast<floatx4*>(nb);
+#pragma unroll
+      for (int i = 0; i < STG; ++i) dst[tid + 256 * i] = stg[i];
+      if (tid < CB / 4) reinterpret_cast<floatx4*>(nb + CHUNK_H * 2)[tid] = stn;
+    }
+    __syncthreads();
+  }
+
+  const float sC = meta[0];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const float ob = __shfl_xor(best[pb], 32, 64);
+    const int oi = __shfl_xor(bidx[pb], 32, 64);
+    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
+    if (ob < best[pb] || (ob == best[pb] && oi < bidx[pb])) {
+      best[pb] = ob;
+      bidx[pb] = oi;
+    }
+    const int64_t row = pbase + pb * 32 + j;
+    if (h == 0 && row < n) {
+      labels[row] = bidx[pb];
+      if (mind) {
+        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
+        const float isx = 1.f / sx[pb];
+        mind[row] = fmaxf(xs * isx * isx + 2.f * best[pb] * isx / sC, 0.f);
+      }
+    }
+  }
+}
+
+int h3_fpad(int f) { return f <= 16 ? 16 : f <= 32 ? 32 : f <= 64 ? 64 : f <= 128 ? 128 : -1; }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------ C ABI
+// Feature padding used by the planes (row stride = 2 * fpad halfs), -1 if unsupported.
+HA_EXPORT int ha_h3_fpad(int f) { return h3_fpad(f); }
+
+HA_EXPORT int ha_h3_pack_points(const float* X, int64_t n, int f, int64_t ldx, void* planes, float* sx,
+                                void* stream) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0) return HA_UNSUPPORTED;
+  if (n <= 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t threads = n * (fpad / 8);
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+  _Float16* p = (_Float16*)planes;
+  switch (fpad) {
+    case 16: hipLaunchKernelGGL(h3_pack_points<16>, dim3(blocks), dim3(256), 0, s, X, n, f, ldx, p, sx); break;
+    case 32: hipLaunchKernelGGL(h3_pack_points<32>, dim3(blocks), dim3(256), 0, s, X, n, f, ldx, p, sx); break;
+    case 64: hipLaunchKernelGGL(h3_pack_points<64>, dim3(blocks), dim3(256), 0, s, X, n, f, ldx, p, sx); break;
+    default: hipLaunchKernelGGL(h3_pack_points<128>, dim3(blocks), dim3(256), 0, s, X, n, f, ldx, p, sx); break;
+  }
+  return ha_launch_status();
+}
+
+// Workspace bytes for the centroid image + u + meta.
+HA_EXPORT int64_t ha_h3_workspace_bytes(int k, int f) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || k <= 0) return -1;
+  const int cb = fpad >= 128 ? 64 : 128;
+  const int64_t kpad = (int64_t)(k + cb - 1) / cb * cb;
+  return kpad * fpad * 2 * 2 + kpad * 4 + 16;
+}
+
+HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f, const float* C, int k, int64_t ldc,
+                           void* workspace, int* labels, float* mind, void* stream) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || k <= 0) return HA_UNSUPPORTED;
+  if (n <= 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int cb = fpad >= 128 ? 64 : 128;
+  const int kpad = (k + cb - 1) / cb * cb;
+  _Float16* image = (_Float16*)workspace;
+  float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
+  float* meta = u + kpad;
+  const _Float16* p = (const _Float16*)planes;
+#define HA_H3(FP)                                                                                           \
+  case FP: {                                                                                                \
+    using KC = H3Cfg<FP>;                                                                                   \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3(1), dim3(1024), 0, s, C, k, f, ldc, kpad, image, u, meta); \
+    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 4);                                          \
+    hipFuncSetAttribute((const void*)h3_assign<FP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
+    const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                         \
+    hipLaunchKernelGGL(h3_assign<FP>, dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,            \
+                       kpad / KC::CB, labels, mind);                                                       \
+    break;                                                                                                  \
+  }
+  switch (fpad) {
+    HA_H3(16)
+    HA_H3(32)
+    HA_H3(64)
+    HA_H3(128)
+    default:
+      return HA_UNSUPPORTED;
+  }
+#undef HA_H3
+  return ha_launch_status();
+}

@@ -21,7 +21,7 @@ from ..core.communication import MPI
 from .. import ops
 from ..parallel.ring import ring_pass
 
-__all__ = ["cdist", "manhattan", "rbf"]
+__all__ = ["cdist", "cdist_stream", "manhattan", "rbf"]
 
 _ALLGATHER_BYTES = 2 << 30
 
@@ -147,3 +147,41 @@ def _dist_callable(X: DNDarray, Y: Optional[DNDarray], fn: Callable) -> DNDarray
     else:
         split = None
     return DNDarray(fn(x, y).to(tt), (m, n), dtype, split, X.device, X.comm, True)
+
+
+def cdist_stream(X: DNDarray, Y: Optional[DNDarray], consume: Callable[[torch.Tensor, int, int], None],
+                 metric: str = "euclidean", sigma: float = 1.0, tile: int = 65536,
+                 quadratic_expansion: bool = True) -> None:
+    """Distance matrix too large for memory (e.g. 1e6 x 1e6: 4 TB in fp32), produced tile by tile.
+
+    For every (local row tile, global column tile) the native kernel writes the distances into
+    ONE reused ``tile x tile`` device buffer and calls ``consume(d_tile, global_row0, global_col0)``
+    (reduce it to kNN / row minima / a histogram / a threshold graph ...). ``Y`` blocks travel
+    around the ring (``parallel.ring_pass``), overlapped with the tile compute. No extension in the
+    reference, which materialises the whole matrix (``heat/spatial/distance.py:265-362``)."""
+    if Y is None:
+        Y = X
+    if X.split not in (None, 0) or Y.split not in (None, 0):
+        raise NotImplementedError("Splittings other than 0 or None currently not supported.")
+    x = X.larray if X.larray.dtype == torch.float32 else X.larray.float()
+    y = Y.larray if Y.larray.dtype == torch.float32 else Y.larray.float()
+    comm = X.comm
+    r0 = X.counts_displs()[1][comm.rank] if X.is_distributed() else 0
+    buf = torch.empty((min(tile, max(1, x.shape[0])), min(tile, max(1, Y.gshape[0]))), dtype=torch.float32,
+                      device=x.device)
+    exact = not quadratic_expansion
+
+    def visit(block: torch.Tensor, c0: int):
+        for i in range(0, x.shape[0], tile):
+            xi = x[i: i + tile]
+            for j in range(0, block.shape[0], tile):
+                yj = block[j: j + tile]
+                d = buf[: xi.shape[0], : yj.shape[0]]
+                ops.cdist(xi, yj, metric, sigma=sigma, out=d, exact=exact)
+                consume(d, r0 + i, c0 + j)
+
+    if Y.is_distributed():
+        counts, displs = Y.counts_displs()
+        ring_pass(y.contiguous(), lambda blk, src: visit(blk, displs[src]), comm, counts)
+    else:
+        visit(y, 0)

@@ -439,7 +439,7 @@ def check_dataloader_shuffle():
     for _epoch in range(3):
         seen = torch.cat([b for b in loader]) if len(loader) else torch.empty(0, 2)
         assert seen.shape[0] == data.lshape[0]
-        allrows = np.concatenate(comm.allgather(seen.numpy()))
+        allrows = np.concatenate(comm.allgather(seen.cpu().numpy()))
         assert sorted(allrows[:, 0].tolist()) == list(np.arange(0, 2 * n, 2, dtype=np.float32))
 
 

@@ -34,6 +34,44 @@ def test_kmeans_assign(n, k, f):
     assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("n,k,f", [(1000, 7, 3), (4096, 128, 16), (5000, 300, 32), (20000, 1024, 64),
+                                   (3333, 100, 100), (777, 65, 128), (70000, 1000, 64)])
+@pytest.mark.parametrize("scale", [1.0, 1e-3, 1e4])
+def test_kmeans_assign_f16x3(n, k, f, scale):
+    """fp16x3 split assignment: the chosen centroid is minimal up to fp32-GEMM rounding."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + 3 * k + f)
+    X = (torch.randn(n, f, generator=g) * scale).to(dev)
+    C = (torch.randn(k, f, generator=g) * scale).to(dev)
+    packed = ops.kmeans_pack_points(X)
+    assert packed is not None
+    lab, mind = ops.kmeans_assign(X, C, packed=packed)
+    Xd, Cd = X.double(), C.double()
+    d = torch.cdist(Xd, Cd) ** 2
+    ref_min, ref_lab = d.min(1)
+    chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+    tol = 2e-6 * ((Xd * Xd).sum(1) + (Cd * Cd).sum(1).max())
+    assert torch.all(chosen - ref_min <= tol), (chosen - ref_min - tol).max()
+    assert (lab.long() == ref_lab).float().mean() > 0.995
+    assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-4 * scale * scale * f)
+
+
+def test_kmeans_fast_matches_exact_fit(gpu):
+    import heat_amd as ht
+
+    ht.random.seed(3)
+    x = ht.random.randn(60000, 32, split=0)
+    res = []
+    for prec in ("exact", "fast"):
+        km = ht.cluster.KMeans(n_clusters=64, init="random", max_iter=5, tol=None, random_state=9)
+        km.precision = prec
+        km.fit(x)
+        res.append(km.cluster_centers_.larray)
+    assert torch.allclose(res[0], res[1], atol=1e-3)
+
+
 @pytest.mark.parametrize("n,k,f", [(1000, 7, 3), (50000, 1024, 64), (12345, 33, 100), (4096, 8, 18)])
 def test_kmeans_update(n, k, f):
     from heat_amd import ops
