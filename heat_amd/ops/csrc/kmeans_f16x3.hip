@@ -8,9 +8,9 @@
 // iteration into the MFMA A-fragment image.  Per (point, centroid):
 //     D = hi_c.hi_x + hi_c.lo_x + lo_c.hi_x           (three MFMAs, fp32 accumulation)
 //       = s_x s_C x.c  up to ~3 * 2^-22 relative per product term
-//   argmin_c |c|^2 - 2 x.c  =  argmin_c  s_x * u_c - D,   u_c = s_C |c|^2 / 2
-// so the epilogue is one FMA per pair, a 16-way min per 32-centroid tile and, only when that min
-// beats the running best (rare after the first tiles), a search for its index.
+//   argmin_c |c|^2 - 2 x.c  =  argmax_c  D - s_x * u_c,   u_c = s_C |c|^2 / 2
+// so the epilogue is one (packed) FMA per pair, a 16-way max per 32-centroid tile and a select
+// that keeps the best tile's 16 values; the index is searched once per point at the end.
 //
 // Layout and orientation follow km_assign (kmeans.hip): centroids = A (rows), points = B
 // (columns), the K dimension is permuted so lane half h owns features [h*F2, h*F2 + F2) of its
@@ -21,13 +21,14 @@
 namespace {
 
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 
-template <int FPAD>
+template <int FPAD, int NPB_ = 2>
 struct H3Cfg {
   static constexpr int F2 = FPAD / 2;                  // features per lane half
   static constexpr int KS = F2 / 8;                    // k-steps (16 features each)
   static constexpr int CB = FPAD >= 128 ? 64 : 128;    // centroids per LDS chunk
-  static constexpr int NPB = 2;                        // 32-point blocks per wave
+  static constexpr int NPB = NPB_;                     // 32-point blocks per wave
   static constexpr int WAVES = 4;
   static constexpr int PTS_PER_WG = WAVES * NPB * 32;
   static constexpr int CHUNK_H = CB * FPAD * 2;        // halfs of packed (hi, lo) per chunk
@@ -124,12 +125,13 @@ __global__ __launch_bounds__(1024) void h3_pack_centroids(const float* __restric
   }
 }
 
-template <int FPAD>
+// EPI = false is a timing-only ablation (tools/microbench): MFMAs without the argmin epilogue.
+template <int FPAD, int NPB_ = 2, bool EPI = true>
 __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                    int64_t n, const _Float16* __restrict__ image,
                                                    const float* __restrict__ u, const float* __restrict__ meta,
                                                    int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
-  using K = H3Cfg<FPAD>;
+  using K = H3Cfg<FPAD, NPB_>;
   constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
   constexpr int BUF_B = CHUNK_H * 2 + CB * 4;      // bytes per buffer: image + u
   constexpr int STG = CHUNK_H * 2 / 16 / 256;      // 16-byte pieces staged per thread per chunk
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__
   const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
 
   halfx8 bhi[NPB][KS], blo[NPB][KS];
-  float sx[NPB], xsq[NPB];
+  float sx[NPB], nsx[NPB], xsq[NPB];
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
     int64_t row = pbase + pb * 32 + j;
@@ -159,14 +161,18 @@ __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__
       }
     }
     sx[pb] = sxv[row];
+    nsx[pb] = -sx[pb];
     xsq[pb] = q;
   }
   float best[NPB];
-  int bidx[NPB];
+  int btile[NPB];
+  float sv[NPB][16];
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
-    best[pb] = __builtin_huge_valf();
-    bidx[pb] = 0;
+    best[pb] = -__builtin_huge_valf();
+    btile[pb] = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
   }
 
   {
@@ -209,24 +215,38 @@ __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__
         }
       }
       // accumulator reg r holds centroid row (r&3) + 8(r>>2) + 4h of this 32-block
+      if (!EPI) {
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) best[pb] = fmaxf(best[pb], acc[pb][0] + acc[pb][15]);
+        continue;
+      }
       floatx4 cn[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) cn[g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+      const int tile = ch * (CB / 32) + cb;
 #pragma unroll
       for (int pb = 0; pb < NPB; ++pb) {
-        float v[16];
+        // w = D - s_x u_c (= -v) on packed FMAs, maximised; the tile's 16 values are kept when
+        // its max improves, so the index search runs once per point at the end instead of in a
+        // (nearly always taken) per-tile branch.
+        const floatx2 sx2 = {nsx[pb], nsx[pb]};
+        float w[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = fmaf(sx[pb], cn[r >> 2][r & 3], -acc[pb][r]);
-        float m = v[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) m = fminf(m, v[r]);
-        if (m < best[pb]) {
-          int bi = 15;
-#pragma unroll
-          for (int r = 14; r >= 0; --r) bi = v[r] == m ? r : bi;
-          best[pb] = m;
-          bidx[pb] = ch * CB + cb * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+        for (int q = 0; q < 8; ++q) {
+          const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+          const floatx2 a2 = {acc[pb][2 * q], acc[pb][2 * q + 1]};
+          const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+          w[2 * q] = r2[0];
+          w[2 * q + 1] = r2[1];
         }
+        float m = w[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
+        const bool imp = m > best[pb];
+        best[pb] = imp ? m : best[pb];
+        btile[pb] = imp ? tile : btile[pb];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
       }
     }
     if (more) {
@@ -240,12 +260,20 @@ __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__
   }
 
   const float sC = meta[0];
+  int bidx[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int bi = 15;
+#pragma unroll
+    for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
+    bidx[pb] = btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+  }
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
     const float ob = __shfl_xor(best[pb], 32, 64);
     const int oi = __shfl_xor(bidx[pb], 32, 64);
     const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
-    if (ob < best[pb] || (ob == best[pb] && oi < bidx[pb])) {
+    if (ob > best[pb] || (ob == best[pb] && oi < bidx[pb])) {
       best[pb] = ob;
       bidx[pb] = oi;
     }
@@ -255,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__
       if (mind) {
         // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
         const float isx = 1.f / sx[pb];
-        mind[row] = fmaxf(xs * isx * isx + 2.f * best[pb] * isx / sC, 0.f);
+        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
       }
     }
   }
