@@ -25,5 +25,6 @@ from . import optim
 from . import utils
 from . import models
 from . import profiling
+from . import datasets
 
 profiling._auto_enable()

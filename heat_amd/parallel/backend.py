@@ -9,6 +9,7 @@ environment the process is a world of one and no process group is created at all
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
 
@@ -59,6 +60,7 @@ def ensure_initialized() -> bool:
     timeout = datetime.timedelta(seconds=int(os.environ.get("HEAT_COMM_TIMEOUT", "1800")))
     dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout, **kwargs)
     _INITIALISED_BY_US = True
+    atexit.register(shutdown)
     return True
 
 
