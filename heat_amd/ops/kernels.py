@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch"]
+__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch"]
 
 _NUM_CUS = {}
 
@@ -231,12 +231,47 @@ _CDIST_MODES = {"euclidean": 0, "sqeuclidean": 1, "gaussian": 2, "manhattan": 3}
 _CDIST_EXACT = {"euclidean": 4, "sqeuclidean": 5, "gaussian": 6, "manhattan": 3}
 
 
+class PackedRows(NamedTuple):
+    """Rows split into fp16 hi/lo planes (power-of-two row scale) + {|x|^2, 1/scale} for the
+    fp16x3 cdist kernel (``csrc/cdist_f16x3.hip``). Row slices of both tensors stay valid."""
+    planes: torch.Tensor  # [n, 2 * fpad] float16
+    aux: torch.Tensor     # [n, 2] float32
+    f: int
+
+    def rows(self, lo: int, hi: int) -> "PackedRows":
+        return PackedRows(self.planes[lo:hi], self.aux[lo:hi], self.f)
+
+
+def cdist_pack(X: torch.Tensor) -> PackedRows:
+    """Pack the rows of a float32 device matrix for :func:`cdist` (quadratic-expansion path)."""
+    L = lib()
+    n, f = X.shape
+    fpad = L.ha_cdist_h3_fpad(f)
+    Xc = X if X.stride(-1) == 1 else X.contiguous()
+    planes = torch.empty((n, 2 * fpad), dtype=torch.float16, device=X.device)
+    aux = torch.empty((n, 2), dtype=torch.float32, device=X.device)
+    check(L.ha_cdist_h3_pack(_ptr(Xc), n, f, Xc.stride(0), _ptr(planes), _ptr(aux),
+                             ctypes.c_void_p(stream_ptr(X.device))), "ha_cdist_h3_pack")
+    return PackedRows(planes, aux, f)
+
+
+def _cdist_h3(px: PackedRows, py: PackedRows, mode: int, scale: float, C: torch.Tensor) -> None:
+    m, n = px.planes.shape[0], py.planes.shape[0]
+    if m and n:
+        check(lib().ha_cdist_h3(_ptr(px.planes), _ptr(px.aux), m, _ptr(py.planes), _ptr(py.aux), n, px.f, _ptr(C),
+                                C.stride(0), mode, ctypes.c_float(scale), ctypes.c_void_p(stream_ptr(C.device))),
+              "ha_cdist_h3")
+
+
 def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: float = 1.0,
-          out: Optional[torch.Tensor] = None, exact: bool = False) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, exact: bool = False, precision: str = "f16x3",
+          packed_x: Optional[PackedRows] = None, packed_y: Optional[PackedRows] = None) -> torch.Tensor:
     """Pairwise distances between the rows of X [m, f] and Y [n, f] as an [m, n] float32 matrix.
 
-    Device tensors: ``exact=False`` -> fp32-MFMA tile kernel of the quadratic expansion with a
-    fused norm/clamp/sqrt|exp epilogue; ``exact=True`` (and manhattan) -> VALU tile kernel on the
+    Device tensors, L2 family with ``exact=False`` (quadratic expansion, fused norm/clamp/
+    sqrt|exp epilogue): ``precision="f16x3"`` -> 3-term fp16 split on the FP16 matrix cores
+    (fp32-GEMM accuracy; ``packed_x/packed_y`` from :func:`cdist_pack` skip the packing),
+    ``"fp32"`` -> f32-input MFMA kernel. ``exact=True`` (and manhattan) -> VALU tile kernel on the
     differences (no cancellation for near-identical points). No m x n x f intermediate."""
     m, f = X.shape
     n = Y.shape[0]
@@ -244,6 +279,12 @@ def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: fl
         raise ValueError("unknown metric {}".format(metric))
     if use_native(X) and X.dtype == torch.float32 and Y.dtype == torch.float32:
         L = lib()
+        if not exact and metric != "manhattan" and precision == "f16x3":
+            C = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=X.device)
+            px = packed_x if packed_x is not None else cdist_pack(X)
+            py = packed_y if packed_y is not None else (px if Y is X else cdist_pack(Y.to(X.device)))
+            _cdist_h3(px, py, _CDIST_MODES[metric], 1.0 / (2.0 * sigma * sigma), C)
+            return C
         mode = (_CDIST_EXACT if exact else _CDIST_MODES)[metric]
         if mode < 3:
             Xa = _rows_f32_aligned(X)

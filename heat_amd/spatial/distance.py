@@ -170,14 +170,22 @@ def cdist_stream(X: DNDarray, Y: Optional[DNDarray], consume: Callable[[torch.Te
     buf = torch.empty((min(tile, max(1, x.shape[0])), min(tile, max(1, Y.gshape[0]))), dtype=torch.float32,
                       device=x.device)
     exact = not quadratic_expansion
+    # quadratic expansion on the device: pack X once (fp16x3 planes), each Y block once per visit
+    packable = (not exact and metric != "manhattan" and x.is_cuda and ops.use_native(x))
+    px = ops.cdist_pack(x) if packable and x.shape[0] else None
 
     def visit(block: torch.Tensor, c0: int):
+        pb = ops.cdist_pack(block) if px is not None and block.shape[0] else None
         for i in range(0, x.shape[0], tile):
             xi = x[i: i + tile]
             for j in range(0, block.shape[0], tile):
                 yj = block[j: j + tile]
                 d = buf[: xi.shape[0], : yj.shape[0]]
-                ops.cdist(xi, yj, metric, sigma=sigma, out=d, exact=exact)
+                if pb is not None:
+                    ops.cdist(xi, yj, metric, sigma=sigma, out=d, packed_x=px.rows(i, i + tile),
+                              packed_y=pb.rows(j, j + tile))
+                else:
+                    ops.cdist(xi, yj, metric, sigma=sigma, out=d, exact=exact)
                 consume(d, r0 + i, c0 + j)
 
     if Y.is_distributed():

@@ -130,6 +130,47 @@ def test_cdist(metric, m, n, f, exact):
         assert torch.all(torch.diagonal(self_d) == 0)
 
 
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+@pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian"])
+@pytest.mark.parametrize("m,n,f", [(100, 50, 3), (1000, 777, 18), (257, 300, 128), (300, 129, 200), (40, 2000, 1000)])
+@pytest.mark.parametrize("scale", [1.0, 1e-3, 1e3])
+def test_cdist_expansion(metric, m, n, f, precision, scale):
+    """Quadratic-expansion kernels: squared distances within fp32-GEMM rounding of the exact ones."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(m + n + f)
+    X = (torch.randn(m, f, generator=g) * scale).to(dev)
+    Y = (torch.randn(n, f, generator=g) * scale + 0.5 * scale).to(dev)
+    sigma = 2.0 * scale * (f ** 0.5)
+    out = ops.cdist(X, Y, metric, sigma=sigma, precision=precision).double()
+    Xd, Yd = X.double(), Y.double()
+    d2 = torch.cdist(Xd, Yd) ** 2
+    bound = 1e-5 * ((Xd * Xd).sum(1, keepdim=True) + (Yd * Yd).sum(1))   # cancellation scale
+    if metric == "sqeuclidean":
+        assert torch.all((out - d2).abs() <= bound + 1e-30)
+    elif metric == "euclidean":
+        assert torch.all((out ** 2 - d2).abs() <= 2 * bound + 1e-30)
+    else:
+        ref = torch.exp(-d2 / (2 * sigma * sigma))
+        assert torch.allclose(out, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_cdist_stream_matches_full(gpu):
+    import heat_amd as ht
+
+    ht.random.seed(11)
+    x = ht.random.rand(3000, 40, split=0)
+    full = ht.spatial.cdist(x, x, quadratic_expansion=True).larray
+    got = torch.empty_like(full)
+
+    def consume(d, i, j):
+        got[i: i + d.shape[0], j: j + d.shape[1]] = d
+
+    ht.spatial.cdist_stream(x, x, consume, tile=1024)
+    assert torch.allclose(got, full, atol=1e-5)
+
+
 def test_threefry_bit_exact():
     """Device Threefry kernel == host torch implementation, bit for bit (uniform / int)."""
     import heat_amd as ht
