@@ -19,6 +19,8 @@ import math
 from typing import List, Optional, Tuple, Union
 
 import numpy as np
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -88,8 +90,40 @@ def _reduce_scatter(partial: torch.Tensor, comm, axis: int) -> torch.Tensor:
     return res.movedim(0, axis).contiguous()
 
 
+# Largest operand handed to one BLAS call on the device. rocBLAS/hipBLASLt kernels address their
+# operands through 32-bit buffer descriptors, so a single GEMM on a >4 GB operand (a 1.25e6 x 4096
+# fp32 shard is 20 GB on a 288 GB MI355X) faults; larger products are split into blocks.
+_BLAS_MAX_BYTES = int(os.environ.get("HEAT_BLAS_MAX_BYTES", str(1 << 31)))
+_CHUNK_ON_HOST = False  # tests: exercise the blocking on CPU tensors too
+
+
 def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    return torch.matmul(a, b)
+    """``a @ b`` with every BLAS operand below ``_BLAS_MAX_BYTES`` (blocks along the largest of
+    m, k, n; contraction blocks accumulate with addmm)."""
+    if a.dim() != 2 or b.dim() != 2 or not (a.is_cuda or _CHUNK_ON_HOST):
+        return torch.matmul(a, b)
+    m, k = a.shape
+    n = b.shape[1]
+    es = a.element_size()
+    lim = _BLAS_MAX_BYTES
+    if max(m * k, k * n, m * n) * es <= lim:
+        return torch.matmul(a, b)
+    if k >= m and k >= n and k > 1:
+        step = max(1, lim // (max(m, n, 1) * es))
+        out = _mm(a[:, :step], b[:step])
+        for k0 in range(step, k, step):
+            out += _mm(a[:, k0: k0 + step], b[k0: k0 + step])
+        return out
+    out = torch.empty((m, n), dtype=torch.result_type(a, b), device=a.device)
+    if m >= n:
+        step = max(1, lim // (max(k, n) * es))
+        for r0 in range(0, m, step):
+            out[r0: r0 + step] = _mm(a[r0: r0 + step], b)
+    else:
+        step = max(1, lim // (max(k, m) * es))
+        for c0 in range(0, n, step):
+            out[:, c0: c0 + step] = _mm(a, b[:, c0: c0 + step])
+    return out
 
 
 def matmul(a: DNDarray, b: DNDarray, allow_resplit: bool = False) -> DNDarray:

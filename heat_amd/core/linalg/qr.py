@@ -58,7 +58,10 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
 
     if not a.is_distributed():
         t = a.larray.to(tt)
-        q, r = torch.linalg.qr(t, mode=mode)
+        if mode == "reduced":
+            q, r = _local_qr(t, calc_q)
+        else:
+            q, r = torch.linalg.qr(t, mode=mode)
         R = DNDarray(r, tuple(r.shape), dtype, None if a.split is None else a.split, a.device, a.comm, True)
         Q = DNDarray(q, tuple(q.shape), dtype, None if a.split is None else 0, a.device, a.comm, True) if calc_q else None
         return QR(Q, R)
@@ -106,11 +109,48 @@ def _resplit(x: DNDarray, axis):
     return resplit(x, axis)
 
 
+def _local_qr(t: torch.Tensor, calc_q: bool = True):
+    """Reduced QR of one rank's block. Device blocks above the BLAS operand limit (see
+    ``basics._BLAS_MAX_BYTES``) are factorised as a local TSQR over row chunks: QR per chunk,
+    QR of the stacked R factors, Q chunk = Q_i @ Q2_i."""
+    from . import basics
+    from .basics import _mm
+
+    _BLAS_MAX_BYTES = basics._BLAS_MAX_BYTES
+    m, n = t.shape
+    if not (t.is_cuda or basics._CHUNK_ON_HOST) or t.numel() * t.element_size() <= _BLAS_MAX_BYTES or m <= 2 * n:
+        if calc_q:
+            return torch.linalg.qr(t, mode="reduced")
+        return None, torch.linalg.qr(t, mode="r")[1]
+    step = max(n, _BLAS_MAX_BYTES // (n * t.element_size()))
+    qs, rs = [], []
+    for r0 in range(0, m, step):
+        blk = t[r0: r0 + step]
+        if calc_q:
+            q, r = torch.linalg.qr(blk, mode="reduced")
+            qs.append(q)
+        else:
+            r = torch.linalg.qr(blk, mode="r")[1]
+        rs.append(r)
+    stacked = torch.cat(rs, 0)
+    q2, r = torch.linalg.qr(stacked, mode="reduced")
+    if not calc_q:
+        return None, r
+    out = torch.empty((m, r.shape[0]), dtype=t.dtype, device=t.device)
+    off, row = 0, 0
+    for q in qs:
+        kq = q.shape[1]
+        out[row: row + q.shape[0]] = _mm(q, q2[off: off + kq])
+        off += kq
+        row += q.shape[0]
+    return out, r
+
+
 def _tsqr(local: torch.Tensor, comm, n: int, calc_q: bool):
     """One-level TSQR. Returns (this rank's rows of Q, replicated R)."""
     m_r = local.shape[0]
     if m_r > 0:
-        q1, r1 = torch.linalg.qr(local, mode="reduced")  # q1: m_r x min(m_r,n), r1: min(m_r,n) x n
+        q1, r1 = _local_qr(local, calc_q)  # q1: m_r x min(m_r,n), r1: min(m_r,n) x n
     else:
         q1 = local.new_zeros((0, 0))
         r1 = local.new_zeros((0, n))
@@ -126,7 +166,9 @@ def _tsqr(local: torch.Tensor, comm, n: int, calc_q: bool):
         return None, r
     off = sum(rows[: comm.rank])
     q2_r = q2[off: off + rows[comm.rank]]
-    ql = q1 @ q2_r if m_r > 0 else local.new_zeros((0, q2.shape[1]))
+    from .basics import _mm
+
+    ql = _mm(q1, q2_r) if m_r > 0 else local.new_zeros((0, q2.shape[1]))
     return ql, r
 
 

@@ -9,8 +9,8 @@
 //
 // Output tile 128 x 128 per 256-thread workgroup (4 waves x 64 x 64 = 2 x 2 blocks of
 // v_mfma_f32_32x32x16_f16).  Features advance in chunks of 32 (2 k-steps); both operand chunks are
-// staged through LDS in fragment order (lane-linear conflict-free ds_read_b128), double-buffered
-// with the next chunk's global loads in flight during the MFMAs.  Workgroups are mapped so that
+// staged through LDS in fragment order (lane-linear conflict-free ds_read_b128); the next chunk's
+// global loads are in flight (in registers) during the MFMAs, 3 workgroups per CU.  Workgroups are mapped so that
 // the ones resident on one XCD sweep a contiguous band of tile rows (shared X panels in that
 // XCD's L2).  The distance matrix is written with non-temporal stores (it is streamed, never
 // re-read by this kernel).
@@ -73,13 +73,21 @@ __device__ __forceinline__ void piece_addr(int q, int& r, int& src_off, int& dst
   dst_off = ((((rb * 2 + s) * 2 + hl) * 64) + h * 32 + j) * 8;
 }
 
-__global__ __launch_bounds__(256, 2) void cdist_h3(const _Float16* __restrict__ PX, const float2* __restrict__ AX,
+template <int MODE>
+__device__ __forceinline__ float epi(float d2, float scale) {
+  if (MODE == 0) return __builtin_amdgcn_sqrtf(d2);  // v_sqrt_f32 (1 ulp), no denormal rescaling
+  if (MODE == 1) return d2;
+  return __expf(-d2 * scale);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 3) void cdist_h3(const _Float16* __restrict__ PX, const float2* __restrict__ AX,
                                                   int64_t m, const _Float16* __restrict__ PY,
                                                   const float2* __restrict__ AY, int64_t n, int fpad,
-                                                  float* __restrict__ C, int64_t ldc, int mode, float scale) {
+                                                  float* __restrict__ C, int64_t ldc, float scale) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  _Float16* img = reinterpret_cast<_Float16*>(smem);          // [buf][op][IMG_H]
-  float* rowv = reinterpret_cast<float*>(smem + 2 * 2 * IMG_H * 2);  // xn[128], isx[128], yn[128], isy[128]
+  _Float16* img = reinterpret_cast<_Float16*>(smem);          // [op][IMG_H]
+  float* rowv = reinterpret_cast<float*>(smem + 2 * IMG_H * 2);  // xn[128], isx[128], yn[128], isy[128]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, j = lane & 31;
 
@@ -124,9 +132,9 @@ __global__ __launch_bounds__(256, 2) void cdist_h3(const _Float16* __restrict__ 
       stg[i] = v;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&]() {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<halfx8*>(img + buf * 2 * IMG_H + dsto[i]) = stg[i];
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<halfx8*>(img + dsto[i]) = stg[i];
   };
 
   floatx16 acc[2][2];
@@ -136,13 +144,13 @@ __global__ __launch_bounds__(256, 2) void cdist_h3(const _Float16* __restrict__ 
     for (int v = 0; v < 2; ++v) acc[u][v] = (floatx16)(0.f);
   const int wr = wave >> 1, wc = wave & 1;
 
+  // one LDS buffer (3 workgroups per CU fit): the next chunk waits in registers during the MFMAs
   load(0);
-  store(0);
+  store();
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
-    const int buf = ch & 1;
     if (ch + 1 < nch) load(ch + 1);
-    const _Float16* ix = img + buf * 2 * IMG_H;
+    const _Float16* ix = img;
     const _Float16* iy = ix + IMG_H;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -165,29 +173,39 @@ __global__ __launch_bounds__(256, 2) void cdist_h3(const _Float16* __restrict__ 
           acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[u], bh[v], acc[u][v], 0, 0, 0);
         }
     }
-    if (ch + 1 < nch) store(buf ^ 1);
-    __syncthreads();
+    if (ch + 1 < nch) {
+      __syncthreads();
+      store();
+      __syncthreads();
+    }
   }
 
   // epilogue: lane holds column j of each 32x32 block, rows (r&3) + 8(r>>2) + 4h
+  const bool interior = row0 + TM <= m && col0 + TN <= n;
 #pragma unroll
   for (int v = 0; v < 2; ++v) {
     const int cl = (2 * wc + v) * 32 + j;
     const int64_t col = col0 + cl;
-    const float ynv = rowv[256 + cl], isy = rowv[384 + cl];
+    const float ynv = rowv[256 + cl], m2isy = -2.f * rowv[384 + cl];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      const int rbase = (2 * wr + u) * 32 + 4 * h;
+      float* cp = C + (row0 + rbase) * ldc + col;
+      float o[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int rl = (2 * wr + u) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t row = row0 + rl;
-        const float w = -2.f * rowv[128 + rl] * isy;
-        const float d2 = fmaxf(fmaf(w, acc[u][v][r], rowv[rl] + ynv), 0.f);
-        float out;
-        if (mode == 0) out = sqrtf(d2);
-        else if (mode == 1) out = d2;
-        else out = __expf(-d2 * scale);
-        if (row < m && col < n) __builtin_nontemporal_store(out, C + row * ldc + col);
+        const int rl = rbase + (r & 3) + 8 * (r >> 2);
+        const float d2 = fmaxf(fmaf(m2isy * rowv[128 + rl], acc[u][v][r], rowv[rl] + ynv), 0.f);
+        o[r] = epi<MODE>(d2, scale);
+      }
+      if (interior) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) __builtin_nontemporal_store(o[r], cp + ((r & 3) + 8 * (r >> 2)) * ldc);
+      } else if (col < n) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (row0 + rbase + (r & 3) + 8 * (r >> 2) < m)
+            __builtin_nontemporal_store(o[r], cp + ((r & 3) + 8 * (r >> 2)) * ldc);
       }
     }
   }
@@ -217,10 +235,19 @@ HA_EXPORT int ha_cdist_h3(const void* PX, const void* AX, int64_t m, const void*
   if (fpad < 0 || mode < 0 || mode > 2) return HA_BAD_ARG;
   const int64_t tiles = ((m + TM - 1) / TM) * ((n + TN - 1) / TN);
   const int64_t per_xcd = (tiles + 7) / 8;
-  const size_t lds = 2 * 2 * IMG_H * 2 + 512 * 4;
-  hipFuncSetAttribute((const void*)cdist_h3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(cdist_h3, dim3((unsigned)(per_xcd * 8)), dim3(256), lds, (hipStream_t)stream,
-                     (const _Float16*)PX, (const float2*)AX, m, (const _Float16*)PY, (const float2*)AY, n, fpad, C,
-                     ldc, mode, scale);
+  const size_t lds = 2 * IMG_H * 2 + 512 * 4;
+#define HA_CD(MODE_)                                                                                          \
+  case MODE_:                                                                                                 \
+    hipFuncSetAttribute((const void*)cdist_h3<MODE_>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
+    hipLaunchKernelGGL(cdist_h3<MODE_>, dim3((unsigned)(per_xcd * 8)), dim3(256), lds, (hipStream_t)stream,   \
+                       (const _Float16*)PX, (const float2*)AX, m, (const _Float16*)PY, (const float2*)AY, n, fpad, \
+                       C, ldc, scale);                                                                        \
+    break;
+  switch (mode) {
+    HA_CD(0)
+    HA_CD(1)
+    HA_CD(2)
+  }
+#undef HA_CD
   return ha_launch_status();
 }

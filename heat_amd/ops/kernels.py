@@ -189,7 +189,10 @@ def _moments_native(x: torch.Tensor, axis):
         nchunks = max(1, min((2 * 8 * ncu + nrows - 1) // max(nrows, 1), (red + 4095) // 4096))
         part = torch.empty((nrows, nchunks, 3), dtype=torch.float64, device=x.device)
         check(L.ha_moments_rows(_ptr(x), nrows, red, red, nchunks, _ptr(part), s), "ha_moments_rows")
-        N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 1)
+        if nchunks == 1:
+            N, mu, M2 = part[:, 0, 0], part[:, 0, 1], part[:, 0, 2]
+        else:
+            N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 1)
     elif outer == 1:
         ncols = inner
         col_blocks = max(1, (ncols + 1023) // 1024)
