@@ -229,7 +229,19 @@ __global__ __launch_bounds__(256) void ku_scan_blk(int* __restrict__ hist, int n
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= k) return;
   int run = 0;
-  for (int b = 0; b < nblk; ++b) {
+  int b = 0;
+  // 8 independent loads in flight per step (the dependent chain is the running sum only)
+  for (; b + 8 <= nblk; b += 8) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = hist[(int64_t)(b + u) * k + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      hist[(int64_t)(b + u) * k + c] = run;
+      run += v[u];
+    }
+  }
+  for (; b < nblk; ++b) {
     const int v = hist[(int64_t)b * k + c];
     hist[(int64_t)b * k + c] = run;
     run += v;
