@@ -289,6 +289,314 @@ __global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__
   }
 }
 
+// Variant: the centroid chunk is staged by LDS-DMA (global_load_lds_dwordx4; the packed image is
+// lane-linear, 1 KB per wave instruction) into ONE buffer, which frees the 32 staging VGPRs and half
+// the LDS so 3 workgroups share a CU and hide each other's staging.
+template <int FPAD, int NPB_ = 2, bool EPI = true, int MINB = 3>
+__global__ __launch_bounds__(256, MINB) void h3_assign_g(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+                                                   int64_t n, const _Float16* __restrict__ image,
+                                                   const float* __restrict__ u, const float* __restrict__ meta,
+                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
+  using K = H3Cfg<FPAD, NPB_>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+
+  halfx8 bhi[NPB][KS], blo[NPB][KS];
+  float sx[NPB], nsx[NPB], xsq[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int64_t row = pbase + pb * 32 + j;
+    row = row < n ? row : n - 1;
+    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+      blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
+        q = fmaf(xv, xv, q);
+      }
+    }
+    sx[pb] = sxv[row];
+    nsx[pb] = -sx[pb];
+    xsq[pb] = q;
+  }
+  float best[NPB];
+  int btile[NPB];
+  float sv[NPB][16];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    best[pb] = -__builtin_huge_valf();
+    btile[pb] = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
+  }
+
+  constexpr int PIECES = CHUNK_H * 2 / 1024;  // 1 KB (64 lanes x 16 B) per DMA instruction
+  for (int ch = 0; ch < nchunks; ++ch) {
+    {
+      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+#pragma unroll
+      for (int pc = wave; pc < PIECES; pc += 4)
+        __builtin_amdgcn_global_load_lds(src + pc * 1024,
+                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H * 2), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+    const unsigned char* buf = smem;
+    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
+    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
+#pragma unroll 1
+    for (int cb = 0; cb < CB / 32; ++cb) {
+      floatx16 acc[NPB];
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) acc[pb] = (floatx16)(0.f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
+        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
+        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) {
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[pb], 0, 0, 0);
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[pb], 0, 0, 0);
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[pb], 0, 0, 0);
+        }
+      }
+      // accumulator reg r holds centroid row (r&3) + 8(r>>2) + 4h of this 32-block
+      if (!EPI) {
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) best[pb] = fmaxf(best[pb], acc[pb][0] + acc[pb][15]);
+        continue;
+      }
+      floatx4 cn[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cn[g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+      const int tile = ch * (CB / 32) + cb;
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) {
+        // w = D - s_x u_c (= -v) on packed FMAs, maximised; the tile's 16 values are kept when
+        // its max improves, so the index search runs once per point at the end instead of in a
+        // (nearly always taken) per-tile branch.
+        const floatx2 sx2 = {nsx[pb], nsx[pb]};
+        float w[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+          const floatx2 a2 = {acc[pb][2 * q], acc[pb][2 * q + 1]};
+          const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+          w[2 * q] = r2[0];
+          w[2 * q + 1] = r2[1];
+        }
+        float m = w[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
+        const bool imp = m > best[pb];
+        best[pb] = imp ? m : best[pb];
+        btile[pb] = imp ? tile : btile[pb];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
+      }
+    }
+    __syncthreads();  // every wave is done with the buffer before the next chunk's DMA
+  }
+
+  const float sC = meta[0];
+  int bidx[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int bi = 15;
+#pragma unroll
+    for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
+    bidx[pb] = btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+  }
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const float ob = __shfl_xor(best[pb], 32, 64);
+    const int oi = __shfl_xor(bidx[pb], 32, 64);
+    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
+    if (ob > best[pb] || (ob == best[pb] && oi < bidx[pb])) {
+      best[pb] = ob;
+      bidx[pb] = oi;
+    }
+    const int64_t row = pbase + pb * 32 + j;
+    if (h == 0 && row < n) {
+      labels[row] = bidx[pb];
+      if (mind) {
+        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
+        const float isx = 1.f / sx[pb];
+        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
+      }
+    }
+  }
+}
+
+// Software-pipelined variant of h3_assign_g: the argmax epilogue of tile t-1 (VALU) is issued in the
+// same basic block as the MFMAs of tile t (ping-pong accumulators), and sched_group_barrier pins
+// an MFMA / VALU interleave, so the epilogue fills the MFMA issue gaps instead of stalling the
+// matrix pipe once per tile.
+template <int FPAD, int NPB_ = 2, bool EPI = true, int MINB = 3>
+__global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+                                                   int64_t n, const _Float16* __restrict__ image,
+                                                   const float* __restrict__ u, const float* __restrict__ meta,
+                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
+  using K = H3Cfg<FPAD, NPB_>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+
+  halfx8 bhi[NPB][KS], blo[NPB][KS];
+  float sx[NPB], nsx[NPB], xsq[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int64_t row = pbase + pb * 32 + j;
+    row = row < n ? row : n - 1;
+    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+      blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
+        q = fmaf(xv, xv, q);
+      }
+    }
+    sx[pb] = sxv[row];
+    nsx[pb] = -sx[pb];
+    xsq[pb] = q;
+  }
+  float best[NPB];
+  int btile[NPB];
+  float sv[NPB][16];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    best[pb] = -__builtin_huge_valf();
+    btile[pb] = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
+  }
+
+  constexpr int PIECES = CHUNK_H * 2 / 1024;  // 1 KB (64 lanes x 16 B) per DMA instruction
+  floatx16 acc[2][NPB];
+  floatx4 cnr[2][4];
+  int ptile = -1;
+  auto epilogue = [&](const floatx16 (&ac)[NPB], const floatx4 (&cn)[4], int tile) {
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      const floatx2 sx2 = {nsx[pb], nsx[pb]};
+      float w[16];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+        const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
+        const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+        w[2 * q] = r2[0];
+        w[2 * q + 1] = r2[1];
+      }
+      float m = w[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
+      const bool imp = m > best[pb];
+      best[pb] = imp ? m : best[pb];
+      btile[pb] = imp ? tile : btile[pb];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
+    }
+  };
+  for (int ch = 0; ch < nchunks; ++ch) {
+    {
+      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+#pragma unroll
+      for (int pc = wave; pc < PIECES; pc += 4)
+        __builtin_amdgcn_global_load_lds(src + pc * 1024,
+                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H * 2), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+    const unsigned char* buf = smem;
+    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
+    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
+#pragma unroll
+    for (int cb = 0; cb < CB / 32; ++cb) {
+      const int cur = cb & 1;  // CB/32 is even: ping-pong slot is compile-time
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) acc[cur][pb] = (floatx16)(0.f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
+        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
+        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) {
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[cur][pb], 0, 0, 0);
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cnr[cur][g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+      // epilogue of the previous tile (independent of the MFMAs above)
+      if (ptile >= 0) epilogue(acc[cur ^ 1], cnr[cur ^ 1], ptile);
+      ptile = ch * (CB / 32) + cb;
+#pragma unroll
+      for (int i = 0; i < 3 * KS * NPB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to 4 VALU
+      }
+    }
+    __syncthreads();  // every wave is done with the buffer before the next chunk's DMA
+  }
+  if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], cnr[((CB / 32) - 1) & 1], ptile);
+
+  const float sC = meta[0];
+  int bidx[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int bi = 15;
+#pragma unroll
+    for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
+    bidx[pb] = btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+  }
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const float ob = __shfl_xor(best[pb], 32, 64);
+    const int oi = __shfl_xor(bidx[pb], 32, 64);
+    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
+    if (ob > best[pb] || (ob == best[pb] && oi < bidx[pb])) {
+      best[pb] = ob;
+      bidx[pb] = oi;
+    }
+    const int64_t row = pbase + pb * 32 + j;
+    if (h == 0 && row < n) {
+      labels[row] = bidx[pb];
+      if (mind) {
+        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
+        const float isx = 1.f / sx[pb];
+        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
+      }
+    }
+  }
+}
+
 int h3_fpad(int f) { return f <= 16 ? 16 : f <= 32 ? 32 : f <= 64 ? 64 : f <= 128 ? 128 : -1; }
 
 }  // namespace
@@ -340,11 +648,10 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
   case FP: {                                                                                                \
     using KC = H3Cfg<FP>;                                                                                   \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3(1), dim3(1024), 0, s, C, k, f, ldc, kpad, image, u, meta); \
-    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 4);                                          \
-    hipFuncSetAttribute((const void*)h3_assign<FP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
+    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                         \
-    hipLaunchKernelGGL(h3_assign<FP>, dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,            \
-                       kpad / KC::CB, labels, mind);                                                       \
+    hipLaunchKernelGGL((h3_assign_p<FP, 2, true, 2>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u,  \
+                       meta, kpad / KC::CB, labels, mind);                                                 \
     break;                                                                                                  \
   }
   switch (fpad) {

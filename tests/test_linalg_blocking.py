@@ -44,3 +44,29 @@ def test_distributed_matmul_qr_blocked(tiny_limit):
     assert ht.allclose(ht.matmul(x, y), ht.array(x.numpy() @ y.numpy()))
     q, r = ht.linalg.qr(x)
     assert ht.allclose(ht.matmul(q, r), x, atol=1e-10)
+
+
+@pytest.mark.parametrize("cond", [1.0, 1e3, 1e6])
+@pytest.mark.parametrize("calc_q", [True, False])
+def test_cholqr_accuracy(cond, calc_q):
+    """CholeskyQR2 (well conditioned) and the shifted CholeskyQR3 fallback (ill conditioned):
+    Q orthogonal to fp32 accuracy, Q R = A, R upper triangular with a positive diagonal."""
+    import heat_amd as ht
+
+    g = torch.Generator().manual_seed(3)
+    u, _ = torch.linalg.qr(torch.randn(4000, 50, generator=g, dtype=torch.float64))
+    v, _ = torch.linalg.qr(torch.randn(50, 50, generator=g, dtype=torch.float64))
+    s = torch.logspace(0, -torch.log10(torch.tensor(cond)).item(), 50, dtype=torch.float64)
+    a = ((u * s) @ v.T).float()
+    x = ht.array(a, split=0)
+    q, r = ht.linalg.qr(x, calc_q=calc_q, mode="reduced")
+    R = r.larray
+    assert torch.allclose(R, torch.triu(R))
+    assert torch.all(torch.diagonal(R) > 0)
+    ref = torch.linalg.qr(a.double(), mode="r")[1]
+    ref = ref * torch.sign(torch.diagonal(ref)).unsqueeze(1)
+    assert torch.allclose(R.double(), ref, atol=1e-5 * float(s.max()), rtol=1e-3)
+    if calc_q:
+        Q = q.numpy()
+        assert abs(Q.T @ Q - torch.eye(50).numpy()).max() < 1e-5
+        assert abs(Q @ R.numpy() - a.numpy()).max() < 1e-5

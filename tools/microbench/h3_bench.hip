@@ -27,6 +27,46 @@ float time_variant(const _Float16* planes, const float* sx, int64_t n, const _Fl
   return ms / 10;
 }
 
+template <int NPB, bool EPI, int MINB = 3>
+float time_glds(const _Float16* planes, const float* sx, int64_t n, const _Float16* image, const float* u,
+                const float* meta, int nch, int* labels) {
+  using KC = H3Cfg<64, NPB>;
+  const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;
+  const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
+  for (int w = 0; w < 2; ++w)
+    hipLaunchKernelGGL((h3_assign_g<64, NPB, EPI, MINB>), dim3(blocks), dim3(256), lds, 0, planes, sx, n, image, u, meta, nch, labels, (float*)nullptr);
+  CHECK(hipEventRecord(a));
+  for (int w = 0; w < 10; ++w)
+    hipLaunchKernelGGL((h3_assign_g<64, NPB, EPI, MINB>), dim3(blocks), dim3(256), lds, 0, planes, sx, n, image, u, meta, nch, labels, (float*)nullptr);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  CHECK(hipGetLastError());
+  float ms; CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms / 10;
+}
+
+template <int NPB, int MINB = 2>
+float time_pipe(const _Float16* planes, const float* sx, int64_t n, const _Float16* image, const float* u,
+                const float* meta, int nch, int* labels) {
+  using KC = H3Cfg<64, NPB>;
+  const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;
+  const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
+  for (int w = 0; w < 2; ++w)
+    hipLaunchKernelGGL((h3_assign_p<64, NPB, true, MINB>), dim3(blocks), dim3(256), lds, 0, planes, sx, n, image, u, meta, nch, labels, (float*)nullptr);
+  CHECK(hipEventRecord(a));
+  for (int w = 0; w < 10; ++w)
+    hipLaunchKernelGGL((h3_assign_p<64, NPB, true, MINB>), dim3(blocks), dim3(256), lds, 0, planes, sx, n, image, u, meta, nch, labels, (float*)nullptr);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  CHECK(hipGetLastError());
+  float ms; CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms / 10;
+}
+
 int main() {
   const int64_t n = 12500000; const int f = 64, k = 1024;
   float *X, *C, *sx; _Float16* planes; int* labels; void* ws;
@@ -53,5 +93,23 @@ int main() {
   t = time_variant<1, true>(planes, sx, n, image, u, meta, nch, labels);  printf("NPB1 full     %.3f ms  %.0f TF\n", t, flop / t / 1e9);
   t = time_variant<4, true>(planes, sx, n, image, u, meta, nch, labels);  printf("NPB4 full     %.3f ms  %.0f TF\n", t, flop / t / 1e9);
   t = time_variant<4, false>(planes, sx, n, image, u, meta, nch, labels); printf("NPB4 mfma-only %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  // correctness of the glds variant against the double-buffered one
+  int* lab2; CHECK(hipMalloc(&lab2, n * 4));
+  time_variant<2, true>(planes, sx, n, image, u, meta, nch, labels);
+  time_pipe<2>(planes, sx, n, image, u, meta, nch, lab2);
+  {
+    int* h1 = (int*)malloc(n * 4); int* h2 = (int*)malloc(n * 4);
+    CHECK(hipMemcpy(h1, labels, n * 4, hipMemcpyDeviceToHost)); CHECK(hipMemcpy(h2, lab2, n * 4, hipMemcpyDeviceToHost));
+    int64_t diff = 0; for (int64_t i = 0; i < n; ++i) diff += h1[i] != h2[i];
+    printf("pipelined labels differing: %lld\n", (long long)diff);
+  }
+  t = time_glds<2, true>(planes, sx, n, image, u, meta, nch, labels);  printf("GLDS NPB2 full     %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_glds<2, false>(planes, sx, n, image, u, meta, nch, labels); printf("GLDS NPB2 mfma-only %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_glds<1, true>(planes, sx, n, image, u, meta, nch, labels);  printf("GLDS NPB1 full     %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_glds<1, true, 4>(planes, sx, n, image, u, meta, nch, labels);  printf("GLDS NPB1 4wg full %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_glds<2, true, 2>(planes, sx, n, image, u, meta, nch, labels);  printf("GLDS NPB2 2wg full %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_pipe<2, 2>(planes, sx, n, image, u, meta, nch, labels);  printf("PIPE NPB2 2wg full %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_pipe<1, 3>(planes, sx, n, image, u, meta, nch, labels);  printf("PIPE NPB1 3wg full %.3f ms  %.0f TF\n", t, flop / t / 1e9);
+  t = time_pipe<1, 4>(planes, sx, n, image, u, meta, nch, labels);  printf("PIPE NPB1 4wg full %.3f ms  %.0f TF\n", t, flop / t / 1e9);
   return 0;
 }
