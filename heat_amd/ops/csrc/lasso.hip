@@ -72,7 +72,63 @@ __global__ void lasso_update(float* __restrict__ theta, int j, float* __restrict
   partial[0] = 0.f;
 }
 
+// Fit preparation in one pass over X (row-major [m][n]): XT = X^T (feature-major, the layout of
+// lasso_pass) and colsq[j] += sum_i X[i][j]^2.  64 x 64 tiles through LDS (+1 padding), 256 rows
+// per workgroup along m; the column sums go out with one float atomic per (workgroup, column).
+// Replaces torch's transpose copy + (XT*XT).sum(1), which took 4 ms of a 5 ms sweep at 1e7 x 16.
+__global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
+                                                     float* __restrict__ xt, int64_t ldxt,
+                                                     float* __restrict__ colsq) {
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  float sq = 0.f;                                          // column c0 + tx (thread rows ty = 0 only)
+  for (int sub = 0; sub < 4; ++sub) {
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + sub) * 64;
+    if (r0 >= m) break;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rr = ty * 16 + i;
+      const int64_t r = r0 + rr;
+      const int c = c0 + tx;
+      const float v = (r < m && c < n) ? x[r * ldx + c] : 0.f;
+      tile[rr][tx] = v;
+    }
+    __syncthreads();
+    // write transposed: thread (tx, ty) writes rows c0 + ty*16 + i, columns r0 + tx
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int cc = ty * 16 + i;
+      const int c = c0 + cc;
+      const int64_t r = r0 + tx;
+      const float v = tile[tx][cc];
+      if (c < n && r < m) xt[(int64_t)c * ldxt + r] = v;
+    }
+    // column sums of squares: thread tx of wave 0 sums column tx over the 64 rows
+    if (ty == 0) {
+#pragma unroll 8
+      for (int rr = 0; rr < 64; ++rr) {
+        const float v = tile[rr][tx];
+        sq = fmaf(v, v, sq);
+      }
+    }
+    __syncthreads();
+  }
+  if (ty == 0 && c0 + tx < n) atomicAdd(&colsq[c0 + tx], sq);
+}
+
 }  // namespace
+
+HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, float* xt, int64_t ldxt, float* colsq,
+                               void* stream) {
+  if (m <= 0 || n <= 0) return HA_OK;
+  hipMemsetAsync(colsq, 0, sizeof(float) * (size_t)n, (hipStream_t)stream);
+  const int64_t gx = (m + 255) / 256;
+  if (gx > 0x7fffffffLL || (n + 63) / 64 > 65535) return HA_UNSUPPORTED;
+  hipLaunchKernelGGL(lasso_prepare, dim3((unsigned)gx, (unsigned)((n + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+                     x, m, n, ldx, xt, ldxt, colsq);
+  return ha_launch_status();
+}
 
 HA_EXPORT int ha_lasso_pass(const float* xt, int64_t m, int64_t ldxt, int jprev, int jnext, const float* delta,
                             float* r, float* partial, int num_cus, void* stream) {

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch"]
+__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare"]
 
 _NUM_CUS = {}
 
@@ -327,6 +327,19 @@ def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: fl
 
 
 # --------------------------------------------------------------------------------------------- lasso
+def lasso_prepare(X: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(X^T contiguous [n, m], sum of squares per column [n]) in one pass over X."""
+    m, n = X.shape
+    if use_native(X) and X.dtype == torch.float32 and X.stride(-1) == 1:
+        XT = torch.empty((n, m), dtype=torch.float32, device=X.device)
+        colsq = torch.empty(n, dtype=torch.float32, device=X.device)
+        check(lib().ha_lasso_prepare(_ptr(X), m, n, X.stride(0), _ptr(XT), XT.stride(0), _ptr(colsq),
+                                     ctypes.c_void_p(stream_ptr(X.device))), "ha_lasso_prepare")
+        return XT, colsq
+    XT = X.t().contiguous()
+    return XT, (XT * XT).sum(1)
+
+
 def lasso_epoch(XT: torch.Tensor, r: torch.Tensor, theta: torch.Tensor, colsq: torch.Tensor, lam: float,
                 m_global: int, allreduce=None):
     """One cyclic coordinate-descent sweep over all features (in place on ``r`` and ``theta``).

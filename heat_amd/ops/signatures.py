@@ -20,5 +20,6 @@ SIGNATURES = {
     "ha_cdist_h3_pack": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p]),
     "ha_cdist_h3": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_int,
                             c_float, c_void_p]),
+    "ha_lasso_prepare": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "ha_lasso_update": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p, c_int, c_void_p]),
 }

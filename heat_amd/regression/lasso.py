@@ -86,8 +86,7 @@ class Lasso(RegressionMixin, BaseEstimator):
             r0 = displs[x.comm.rank]
             yl = yl[r0: r0 + counts[x.comm.rank]]
         dist = x.is_distributed()
-        XT = X.t().contiguous()                               # [n, m_local]: features contiguous
-        colsq = (XT * XT).sum(1)
+        XT, colsq = ops.lasso_prepare(X)                       # [n, m_local]: features contiguous
         if dist:
             x.comm.Allreduce(MPI.IN_PLACE, colsq, MPI.SUM)
         colsq = colsq / m

@@ -211,3 +211,14 @@ def test_kmeans_fit_gpu(gpu):
     d = torch.cdist(got, centers)
     assert torch.all(d.min(1).values < 0.5)
     assert km.labels_.shape == (2000, 1)
+
+
+@pytest.mark.parametrize("m,n", [(1000, 3), (70001, 16), (513, 130)])
+def test_lasso_prepare(m, n):
+    from heat_amd import ops
+
+    dev = _dev()
+    X = torch.randn(m, n, generator=torch.Generator().manual_seed(m)).to(dev)
+    XT, colsq = ops.lasso_prepare(X)
+    assert torch.equal(XT, X.t().contiguous())
+    assert torch.allclose(colsq.double(), (X.double() ** 2).sum(0), rtol=1e-5)
