@@ -80,7 +80,8 @@ __device__ __forceinline__ float epi(float d2, float scale) {
   return __expf(-d2 * scale);
 }
 
-template <int MODE>
+// ABL (timing ablations in tools/microbench only): 1 = no stores, 2 = no MFMAs
+template <int MODE, int ABL = 0>
 __global__ __launch_bounds__(256, 3) void cdist_h3(const _Float16* __restrict__ PX, const float2* __restrict__ AX,
                                                   int64_t m, const _Float16* __restrict__ PY,
                                                   const float2* __restrict__ AY, int64_t n, int fpad,
@@ -98,7 +99,16 @@ __global__ __launch_bounds__(256, 3) void cdist_h3(const _Float16* __restrict__ 
   const int64_t b = blockIdx.x;
   const int64_t t = (b % 8) * per_xcd + b / 8;  // a bijection of [0, 8 per_xcd)
   if (t >= tiles) return;                          // padding of the last band
-  const int64_t row0 = (t / tiles_n) * TM, col0 = (t % tiles_n) * TN;
+  // grouped order inside the band: GROUP tile-rows advance together, so the ~64 workgroups
+  // resident on one XCD cover an 8 x 8 block of tiles and share 8 X and 8 Y panels in its L2
+  // (row-major order would need 1 X and 64 distinct Y panels)
+  constexpr int64_t GROUP = 8;
+  const int64_t tiles_m = (m + TM - 1) / TM;
+  const int64_t grp = t / (GROUP * tiles_n);
+  const int64_t first = grp * GROUP;
+  const int64_t gsz = tiles_m - first < GROUP ? tiles_m - first : GROUP;
+  const int64_t in = t - grp * GROUP * tiles_n;
+  const int64_t row0 = (first + in % gsz) * TM, col0 = (in / gsz) * TN;
 
   if (tid < 128) {
     const int64_t r = row0 + tid;
@@ -168,6 +178,10 @@ __global__ __launch_bounds__(256, 3) void cdist_h3(const _Float16* __restrict__ 
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
+          if (ABL == 2) {
+            acc[u][v][0] += (float)ah[u][0] * (float)bh[v][0];
+            continue;
+          }
           acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[u], bh[v], acc[u][v], 0, 0, 0);
           acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[u], bl[v], acc[u][v], 0, 0, 0);
           acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[u], bh[v], acc[u][v], 0, 0, 0);
@@ -198,7 +212,12 @@ __global__ __launch_bounds__(256, 3) void cdist_h3(const _Float16* __restrict__ 
         const float d2 = fmaxf(fmaf(m2isy * rowv[128 + rl], acc[u][v][r], rowv[rl] + ynv), 0.f);
         o[r] = epi<MODE>(d2, scale);
       }
-      if (interior) {
+      if (ABL == 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += o[r];
+        if (t == 1234.5f) cp[0] = t;  // keep the epilogue alive
+      } else if (interior) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) __builtin_nontemporal_store(o[r], cp + ((r & 3) + 8 * (r >> 2)) * ldc);
       } else if (col < n) {
