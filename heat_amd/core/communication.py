@@ -555,23 +555,32 @@ class MPICommunication(Communication):
 
     # ---------------------------------------------------------------- gather / scatter
     def Igatherv(self, sendbuf, recvbuf, root: int = 0, axis: int = 0, recv_axis: int = None) -> MPIRequest:
+        """Concatenation of every rank's block along ``axis`` on ``root`` only: one size exchange
+        and one personalised exchange in which only ``root`` receives (no all-gather)."""
         axis = axis if recv_axis is None else recv_axis
         send, _, _ = self._unpack_v(sendbuf)
-        recv, counts, _ = self._unpack_v(recvbuf) if recvbuf is not None else (None, None, None)
+        recv = self._unpack_v(recvbuf)[0] if recvbuf is not None else None
         if self.size == 1:
             if recv is not None:
                 recv.copy_(send.reshape(recv.shape))
             return MPIRequest()
-        if counts is not None:
-            counts = [int(c) for c in (counts.tolist() if isinstance(counts, torch.Tensor) else counts)]
-        work, fin = self._allgatherv_async(send, axis, counts)
-
-        def fin2():
-            res = fin()
-            if self.rank == root and recv is not None:
-                recv.copy_(res.to(recv.dtype).reshape(recv.shape))
-
-        return MPIRequest(work, fin2)
+        if send.dim() == 0:
+            send = send.reshape(1)
+        self._trace("Gatherv", send)
+        counts = self.allgather_sizes(send.shape[axis])
+        blocks = [send if r == root else send.narrow(axis, 0, 0) for r in range(self.size)]
+        if self.rank == root:
+            shapes = []
+            for r in range(self.size):
+                s_ = list(send.shape)
+                s_[axis] = counts[r]
+                shapes.append(tuple(s_))
+        else:
+            shapes = [tuple(send.narrow(axis, 0, 0).shape)] * self.size
+        out = self.exchange(blocks, shapes)
+        if self.rank == root and recv is not None:
+            recv.copy_(torch.cat(out, dim=axis).to(recv.dtype).reshape(recv.shape))
+        return MPIRequest()
 
     def Gatherv(self, sendbuf, recvbuf, root: int = 0, axis: int = 0, recv_axis: int = None):
         self.Igatherv(sendbuf, recvbuf, root, axis, recv_axis).Wait()

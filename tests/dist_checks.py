@@ -452,3 +452,133 @@ def check_tiling():
     sq = ht.tiling.SquareDiagTiles(m, tiles_per_proc=2)
     assert sum(sq.row_indices[i + 1] - sq.row_indices[i] for i in range(len(sq.row_indices) - 1)) <= 12
     assert sq.tile_rows >= 2
+
+
+# ---------------------------------------------------------------------------------------------
+# communication layer, one check per primitive family (reference heat/core/tests/
+# test_communication.py: blocking + non-blocking, IN_PLACE, axis permutations, v-variants)
+# ---------------------------------------------------------------------------------------------
+def check_comm_collectives():
+    comm = ht.MPI_WORLD
+    p, me = comm.size, comm.rank
+    MPI = ht.MPI
+    # Bcast / Ibcast
+    t = torch.full((3, 2), float(me))
+    comm.Bcast(t, root=p - 1)
+    assert torch.all(t == p - 1)
+    t = torch.arange(4.0) * (me + 1)
+    comm.Ibcast(t, root=0).Wait()
+    assert torch.equal(t, torch.arange(4.0))
+    # Allreduce with every op, IN_PLACE and separate buffers, blocking and not
+    vals = [torch.tensor([r + 1.0, -(r + 2.0), 2.0 ** r]) for r in range(p)]
+    mine = vals[me]
+    expect = {MPI.SUM: sum(vals), MPI.PROD: torch.stack(vals).prod(0), MPI.MAX: torch.stack(vals).max(0).values,
+              MPI.MIN: torch.stack(vals).min(0).values}
+    for op, ref in expect.items():
+        out = torch.empty(3)
+        comm.Allreduce(mine, out, op)
+        assert torch.allclose(out, ref), (op, out, ref)
+        buf = mine.clone()
+        comm.Iallreduce(MPI.IN_PLACE, buf, op).Wait()
+        assert torch.allclose(buf, ref)
+    bits = torch.tensor([1 << me, 7], dtype=torch.int64)
+    comm.Allreduce(MPI.IN_PLACE, bits, MPI.BOR)
+    assert int(bits[0]) == (1 << p) - 1 and int(bits[1]) == 7
+    flags = torch.tensor([True, me == 0])
+    comm.Allreduce(MPI.IN_PLACE, flags, MPI.LAND)
+    assert bool(flags[0]) and bool(flags[1]) == (p == 1)
+    flags = torch.tensor([False, me == 0])
+    comm.Allreduce(MPI.IN_PLACE, flags, MPI.LOR)
+    assert not bool(flags[0]) and bool(flags[1])
+    custom = MPI.Op.Create(lambda a, b, *args: torch.maximum(a, b) + 0 * b)
+    buf = torch.tensor([float(me)])
+    comm.Allreduce(MPI.IN_PLACE, buf, custom)
+    assert float(buf) == p - 1
+    # Exscan / Scan
+    s = torch.tensor([float(me + 1)])
+    ex = torch.zeros(1)
+    comm.Exscan(s, ex, MPI.SUM)
+    if me > 0:
+        assert float(ex) == sum(range(1, me + 1))
+    sc = torch.zeros(1)
+    comm.Scan(s, sc, MPI.SUM)
+    assert float(sc) == sum(range(1, me + 2))
+    # Allgather along axis 0 and 1 (equal counts)
+    blk = torch.full((2, 3), float(me))
+    out = torch.empty((2 * p, 3))
+    comm.Allgather(blk, out, recv_axis=0)
+    assert torch.equal(out, torch.cat([torch.full((2, 3), float(r)) for r in range(p)], 0))
+    out = torch.empty((2, 3 * p))
+    comm.Iallgather(blk, out, recv_axis=1).Wait()
+    assert torch.equal(out, torch.cat([torch.full((2, 3), float(r)) for r in range(p)], 1))
+    # Allgatherv with uneven counts + IN_PLACE
+    counts = [r + 1 for r in range(p)]
+    displs = [sum(counts[:r]) for r in range(p)]
+    send = torch.full((counts[me], 2), float(me))
+    recv = torch.empty((sum(counts), 2))
+    comm.Allgatherv(send, (recv, counts, displs))
+    assert torch.equal(recv, torch.cat([torch.full((c, 2), float(r)) for r, c in enumerate(counts)]))
+    recv2 = torch.zeros((sum(counts), 2))
+    recv2[displs[me]: displs[me] + counts[me]] = float(me)
+    comm.Allgatherv(MPI.IN_PLACE, (recv2, counts, displs))
+    assert torch.equal(recv2, recv)
+    # Gatherv / Scatterv
+    g = torch.empty((sum(counts), 2)) if me == 0 else None
+    comm.Gatherv(send, (g, counts, displs) if me == 0 else None, root=0)
+    if me == 0:
+        assert torch.equal(g, recv)
+    sc_out = torch.empty((counts[me], 2))
+    comm.Scatterv((recv, counts, displs) if me == 0 else None, sc_out, root=0)
+    assert torch.all(sc_out == float(me))
+    # Alltoall (equal) and Alltoallv (uneven) along axis 0 and 1
+    a2 = torch.arange(p * 2, dtype=torch.float32).reshape(p * 2, 1) + 100 * me
+    r2 = torch.empty_like(a2)
+    comm.Alltoall(a2, r2)
+    expect = torch.cat([torch.arange(2 * me, 2 * me + 2, dtype=torch.float32).reshape(2, 1) + 100 * r
+                        for r in range(p)])
+    assert torch.equal(r2, expect)
+    a3 = a2.t().contiguous()
+    r3 = torch.empty_like(a3)
+    comm.Alltoall(a3, r3, send_axis=1)
+    assert torch.equal(r3, expect.t())
+    scounts = [(me + r) % 2 + 1 for r in range(p)]
+    rcounts = [(r + me) % 2 + 1 for r in range(p)]
+    sv = torch.cat([torch.full((scounts[r],), float(100 * me + r)) for r in range(p)])
+    rv = torch.empty(sum(rcounts))
+    comm.Alltoallv((sv, scounts), (rv, rcounts))
+    assert torch.equal(rv, torch.cat([torch.full((rcounts[r],), float(100 * r + me)) for r in range(p)]))
+    # point to point ring: Send/Recv and Isend/Irecv
+    if p > 1:
+        nxt, prv = (me + 1) % p, (me - 1) % p
+        got = torch.empty(3)
+        if me % 2 == 0:
+            comm.Send(torch.full((3,), float(me)), nxt)
+            comm.Recv(got, prv)
+        else:
+            comm.Recv(got, prv)
+            comm.Send(torch.full((3,), float(me)), nxt)
+        assert torch.all(got == prv)
+        rq = comm.Irecv(got, prv)
+        sq = comm.Isend(torch.full((3,), float(me + 10)), nxt)
+        sq.Wait()
+        rq.Wait()
+        assert torch.all(got == prv + 10)
+    # pickled object collectives
+    assert comm.bcast({"a": me}, root=0) == {"a": 0}
+    assert comm.allgather(me) == list(range(p))
+    assert comm.allreduce(me + 1) == p * (p + 1) // 2
+    assert comm.alltoall([me * 10 + r for r in range(p)]) == [r * 10 + me for r in range(p)]
+    gathered = comm.gather(me, root=0)
+    assert (gathered == list(range(p))) if me == 0 else gathered is None
+    assert comm.scatter([r * r for r in range(p)] if me == 0 else None, root=0) == me * me
+    # sub-communicators
+    sub = comm.Split(color=me % 2, key=-me)
+    members = [r for r in range(p) if r % 2 == me % 2]
+    assert sub.size == len(members)
+    assert sub.rank == sorted(members, reverse=True).index(me)
+    tot = torch.tensor([float(me)])
+    sub.Allreduce(MPI.IN_PLACE, tot, MPI.SUM)
+    assert float(tot) == sum(members)
+    x = ht.arange(10, split=0, comm=sub)
+    assert int(ht.sum(x).item()) == 45
+    comm.Barrier()
