@@ -296,11 +296,14 @@ class DASO:
     def _global_sync(self, batches_to_wait: int) -> None:
         current_comm = self.reduced_comms[self._send_mod]
         current_ranks = self.reduced_ranks[self._send_mod]
-        if self.comm.rank in current_ranks:
-            self._gs_send_params(current_comm, batches_to_wait)
+        # merge the previous (stale) global average BEFORE posting the new one: with one rank per
+        # node the sending group repeats, and receiving after sending would consume the buffer
+        # just posted (the reference orders it the other way, which is only safe for loc_gpus > 1)
         if self.batches_to_wait != 0:
             self._gs_rcv_update_params()
             self._local_update(self._send_mod_m1)
+        if self.comm.rank in current_ranks:
+            self._gs_send_params(current_comm, batches_to_wait)
         if self.current_batch == self.last_batch or self.batches_to_wait == 0:
             if self.comm.rank in current_ranks:
                 self._gs_rcv_update_params_last_batch(current_ranks)

@@ -582,3 +582,49 @@ def check_comm_collectives():
     x = ht.arange(10, split=0, comm=sub)
     assert int(ht.sum(x).item()) == 45
     comm.Barrier()
+
+
+def check_daso():
+    """DASO end to end (reference optim/tests/test_dp_optimizer.py, which needs 8 GPUs): warm-up,
+    skipping phase with stale global averages, cool-down; afterwards every rank holds the same
+    parameters and the loss went down. Even world sizes run as nodes of 2 ranks."""
+    import os
+
+    comm = ht.MPI_WORLD
+    old = os.environ.get("LOCAL_WORLD_SIZE")
+    os.environ["LOCAL_WORLD_SIZE"] = "2" if comm.size % 2 == 0 else "1"
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.Tanh(), torch.nn.Linear(16, 1))
+        opt = torch.optim.SGD(net.parameters(), lr=0.05)
+        daso = ht.optim.DASO(local_optimizer=opt, total_epochs=6, comm=comm, warmup_epochs=1, cooldown_epochs=1,
+                             max_global_skips=4, stability_level=0.5)
+        dp = ht.nn.DataParallelMultiGPU(net, daso, comm)
+        g = torch.Generator().manual_seed(10 + comm.rank)
+        w_true = torch.linspace(-1, 1, 6)
+        X = torch.randn(96, 6, generator=g)
+        y = (X @ w_true).unsqueeze(1)
+        nb = 12
+        daso.last_batch = nb - 1
+        losses = []
+        for epoch in range(6):
+            tot = 0.0
+            for b in range(nb):
+                xb, yb = X[b * 8:(b + 1) * 8], y[b * 8:(b + 1) * 8]
+                daso.zero_grad()
+                loss = torch.nn.functional.mse_loss(dp(xb), yb)
+                loss.backward()
+                daso.step()
+                tot += float(loss)
+            losses.append(tot / nb)
+            daso.epoch_loss_logic(torch.tensor(tot / nb))
+        flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+        allp = comm.allgather(flat.numpy())
+        for other in allp[1:]:
+            assert np.allclose(other, allp[0], atol=1e-6)
+        assert losses[-1] < losses[0]
+    finally:
+        if old is None:
+            os.environ.pop("LOCAL_WORLD_SIZE", None)
+        else:
+            os.environ["LOCAL_WORLD_SIZE"] = old
