@@ -981,3 +981,26 @@ DNDarray.rot90 = lambda self, k=1, axes=(0, 1): rot90(self, k, axes)
 DNDarray.squeeze = lambda self, axis=None: squeeze(self, axis)
 DNDarray.swapaxes = lambda self, axis1, axis2: swapaxes(self, axis1, axis2)
 DNDarray.unique = lambda self, sorted=False, return_inverse=False, axis=None: unique(self, sorted, return_inverse, axis)
+
+
+
+def mpi_topk(a, b, mpi_type=None) -> None:
+    """Reduction callback of distributed :func:`topk` (reference manipulations.py:3997-4040):
+    buffers are float64 ``[k, dim, largest, sorted, ndim, *shape, values..., indices...]``; the
+    top-k of the concatenation of both candidate sets is written into ``b``."""
+    ap = torch.as_tensor(a) if isinstance(a, torch.Tensor) else torch.from_numpy(np.frombuffer(a, dtype=np.float64))
+    bp = torch.as_tensor(b) if isinstance(b, torch.Tensor) else torch.from_numpy(np.frombuffer(b, dtype=np.float64))
+    k, dim, largest, srt = int(ap[0]), int(ap[1]), bool(ap[2]), bool(ap[3])
+    la, lb = int(ap[4]), int(bp[4])
+    sa = [int(v) for v in ap[5: 5 + la].tolist()]
+    sb = [int(v) for v in bp[5: 5 + lb].tolist()]
+    av, ai = ap[5 + la:].chunk(2)
+    bv, bi = bp[5 + lb:].chunk(2)
+    vals = torch.cat((av.reshape(sa), bv.reshape(sb)), dim=dim)
+    idx = torch.cat((ai.reshape(sa), bi.reshape(sb)), dim=dim)
+    res, kk = torch.topk(vals, k, dim=dim, largest=largest, sorted=srt)
+    out = torch.cat((ap[: 5 + la], res.double().flatten(), torch.gather(idx, dim, kk).double().flatten()))
+    bp.copy_(out)
+
+
+MPI_TOPK = MPI.Op.Create(mpi_topk, commute=True)

@@ -584,3 +584,38 @@ DNDarray.min = lambda self, axis=None, out=None, keepdim=None: min(self, axis, o
 DNDarray.skew = lambda self, axis=None, unbiased=True: skew(self, axis, unbiased)
 DNDarray.std = lambda self, axis=None, ddof=0, **kwargs: std(self, axis, ddof, **kwargs)
 DNDarray.var = lambda self, axis=None, ddof=0, **kwargs: var(self, axis, ddof, **kwargs)
+
+
+# --------------------------------------------------------------------------------------------
+# packed (value, index) reduction operators (reference statistics.py:1139-1207). The buffers hold
+# [values..., indices...] (float64); ties keep the smaller global index. They are Op callbacks
+# ``f(in, inout, datatype)`` usable with ``comm.Allreduce(..., MPI_ARGMAX)``; argmax/argmin use the
+# same rule on all-gathered candidates.
+# --------------------------------------------------------------------------------------------
+def _as_f64(buf) -> torch.Tensor:
+    if isinstance(buf, torch.Tensor):
+        return buf
+    return torch.from_numpy(np.frombuffer(buf, dtype=np.float64))
+
+
+def _arg_combine(a, b, larger: bool) -> None:
+    lhs, rhs = _as_f64(a), _as_f64(b)
+    vl, il = lhs.chunk(2)
+    vr, ir = rhs.chunk(2)
+    take_l = (vl > vr) if larger else (vl < vr)
+    take_l = take_l | ((vl == vr) & (il < ir))
+    rhs.copy_(torch.cat([torch.where(take_l, vl, vr), torch.where(take_l, il, ir)]))
+
+
+def mpi_argmax(a, b, _=None) -> None:
+    """Combine two packed (values, indices) buffers into ``b`` keeping the larger value."""
+    _arg_combine(a, b, True)
+
+
+def mpi_argmin(a, b, _=None) -> None:
+    """Combine two packed (values, indices) buffers into ``b`` keeping the smaller value."""
+    _arg_combine(a, b, False)
+
+
+MPI_ARGMAX = MPI.Op.Create(mpi_argmax, commute=True)
+MPI_ARGMIN = MPI.Op.Create(mpi_argmin, commute=True)

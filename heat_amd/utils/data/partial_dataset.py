@@ -19,7 +19,20 @@ try:
 except ImportError:  # optional dependency
     h5py = None
 
-__all__ = ["PartialH5Dataset", "PartialH5DataLoaderIter"]
+__all__ = ["PartialH5Dataset", "PartialH5DataLoaderIter", "queue_thread"]
+
+
+def queue_thread(q: queue.Queue) -> None:
+    """Worker loop of the loader threads: run ``func(*args)`` (or a bare callable) per queue item."""
+    while True:
+        item = q.get()
+        try:
+            if isinstance(item, tuple):
+                item[0](*item[1:])
+            else:
+                item()
+        finally:
+            q.task_done()
 
 
 class PartialH5Dataset(torch_data.Dataset):
