@@ -2,8 +2,9 @@
 Parallel IO (reference ``heat/core/io.py``: ``load_hdf5`` 55, ``save_hdf5`` 147, ``load_netcdf`` 265,
 ``save_netcdf`` 348, ``load`` 659, ``load_csv`` 710, ``save`` 923).
 
-* HDF5 / NetCDF: available when ``h5py`` / ``netCDF4`` are importable (same file layout as the
-  reference; every rank reads only its hyperslab; writes are serialised rank by rank).
+* HDF5 / NetCDF: through ``h5py`` / ``netCDF4`` when importable, otherwise through the built-in
+  dependency-free HDF5 reader/writer (``_h5lite``) and classic netCDF files (same layout as the
+  reference; every rank reads only its hyperslab and writes its slab in place, in parallel).
 * CSV: every rank parses only its byte range; a line that straddles a boundary belongs to the
   rank where it starts, so no boundary repair messages are needed (the reference exchanges them,
   ``io.py:806-898``). Parsing uses pandas' C parser.
@@ -22,9 +23,11 @@ import torch
 from . import devices, factories, types
 from .communication import MPI, sanitize_comm
 from .dndarray import DNDarray
+from . import _h5lite
 from .stride_tricks import sanitize_axis
 
-__all__ = ["load", "load_csv", "save", "save_csv", "load_npy", "save_npy", "supports_hdf5", "supports_netcdf"]
+__all__ = ["load", "load_csv", "save", "save_csv", "load_npy", "save_npy", "supports_hdf5", "supports_netcdf",
+           "load_hdf5", "save_hdf5", "load_netcdf", "save_netcdf"]
 
 try:
     import h5py  # noqa: F401
@@ -37,11 +40,14 @@ except ImportError:
 
 
 def supports_hdf5() -> bool:
-    return h5py is not None
+    """HDF5 is always available (h5py, or the built-in reader/writer ``_h5lite``)."""
+    return True
 
 
 def supports_netcdf() -> bool:
-    return nc is not None
+    """netCDF is always available (netCDF4, or netCDF-4/HDF5 reading via ``_h5lite`` and classic
+    netCDF reading (scipy) / writing (built in))."""
+    return True
 
 
 def _exception_barrier(comm, exc: Optional[BaseException]):
@@ -191,94 +197,237 @@ def save_csv(data: DNDarray, path: str, header_lines: Optional[List[str]] = None
 
 
 # --------------------------------------------------------------------------------------------- hdf5
-if h5py is not None:
-    __all__ += ["load_hdf5", "save_hdf5"]
+def _hyperslab(gshape, split, comm):
+    _, _, sl = comm.chunk(tuple(gshape), split)
+    return sl
 
-    def load_hdf5(path: str, dataset: str, dtype=types.float32, load_fraction: float = 1.0,
-                  split: Optional[int] = None, device=None, comm=None) -> DNDarray:
-        """Load an HDF5 dataset; every rank reads only its hyperslab."""
-        comm = sanitize_comm(comm)
-        device = devices.sanitize_device(device)
-        htype = types.canonical_heat_type(dtype)
-        with h5py.File(path, "r") as handle:
-            data = handle[dataset]
-            gshape = list(data.shape)
-            if split is not None:
-                gshape[split] = int(gshape[split] * load_fraction)
-            gshape = tuple(gshape)
-            split = sanitize_axis(gshape, split)
-            _, _, sl = comm.chunk(gshape, split)
-            local = torch.tensor(np.asarray(data[sl]), dtype=htype.torch_type(), device=device.torch_device)
-        return DNDarray(local, gshape, htype, split, device, comm, True)
 
-    def save_hdf5(data: DNDarray, path: str, dataset: str, mode: str = "w", **kwargs) -> None:
-        """Write a DNDarray into an HDF5 dataset (rank by rank)."""
-        comm = data.comm
+def load_hdf5(path: str, dataset: str, dtype=types.float32, load_fraction: float = 1.0,
+              split: Optional[int] = None, device=None, comm=None) -> DNDarray:
+    """Load an HDF5 dataset; every rank reads only its hyperslab (h5py when installed, otherwise
+    the built-in reader ``_h5lite``, which memory-maps contiguous storage)."""
+    if not isinstance(path, str):
+        raise TypeError("path must be str, not {}".format(type(path)))
+    if not isinstance(dataset, str):
+        raise TypeError("dataset must be str, not {}".format(type(dataset)))
+    if not isinstance(load_fraction, float):
+        raise TypeError("load_fraction must be float, but is {}".format(type(load_fraction)))
+    if load_fraction <= 0.0 or load_fraction > 1.0:
+        raise ValueError("load_fraction must be between 0 (exclusive) and 1 (inclusive), not {}".format(load_fraction))
+    comm = sanitize_comm(comm)
+    device = devices.sanitize_device(device)
+    htype = types.canonical_heat_type(dtype)
+    handle = h5py.File(path, "r") if h5py is not None else _h5lite.open_file(path)
+    try:
+        data = handle[dataset]
+        gshape = list(data.shape)
+        if split is not None:
+            split = sanitize_axis(tuple(gshape), split)
+            gshape[split] = int(gshape[split] * load_fraction)
+        gshape = tuple(gshape)
+        split = sanitize_axis(gshape, split)
+        local = np.asarray(data[_hyperslab(gshape, split, comm)])
+    finally:
+        handle.close()
+    t = torch.from_numpy(np.ascontiguousarray(local).astype(local.dtype.newbyteorder("=")))
+    t = t.to(device=device.torch_device, dtype=htype.torch_type())
+    return DNDarray(t, gshape, htype, split, device, comm, True)
+
+
+def save_hdf5(data: DNDarray, path: str, dataset: str, mode: str = "w", **kwargs) -> None:
+    """Write a DNDarray into an HDF5 dataset. Without h5py (built-in writer) rank 0 declares the
+    dataset and every rank then writes its slab into the pre-allocated storage in parallel."""
+    if not isinstance(data, DNDarray):
+        raise TypeError("data must be heat tensor, not {}".format(type(data)))
+    if not isinstance(path, str):
+        raise TypeError("path must be str, not {}".format(type(path)))
+    if not isinstance(dataset, str):
+        raise TypeError("dataset must be str, not {}".format(type(path)))
+    if mode not in ("w", "a", "r+"):
+        raise ValueError("mode was {}, not in possible modes ['w', 'a', 'r+']".format(mode))
+    comm = data.comm
+    np_dtype = np.dtype(torch.empty(0, dtype=data.larray.dtype).numpy().dtype)
+    counts, displs = data.counts_displs() if data.is_distributed() else ((None,), (None,))
+    exc = None
+    if comm.rank == 0:
+        try:
+            if h5py is not None:
+                with h5py.File(path, mode) as handle:
+                    handle.create_dataset(dataset, data.gshape, dtype=np_dtype, **kwargs)
+            else:
+                if mode == "w" or not os.path.exists(path):
+                    _h5lite.create_file(path)
+                _h5lite.create_dataset(path, dataset, data.gshape, np_dtype)
+        except Exception as e:  # propagated to every rank
+            exc = e
+    _exception_barrier(comm, exc)
+    local = data.larray.cpu().numpy()
+    if not data.is_distributed():
         if comm.rank == 0:
-            with h5py.File(path, mode) as handle:
-                handle.create_dataset(dataset, data.gshape, dtype=data.larray.cpu().numpy().dtype, **kwargs)
+            _write_slab(path, dataset, (slice(None),) * data.ndim, local)
         comm.Barrier()
-        if data.split is None or not data.is_distributed():
-            if comm.rank == 0:
-                with h5py.File(path, "r+") as handle:
-                    handle[dataset][...] = data.larray.cpu().numpy()
-            comm.Barrier()
-            return
-        counts, displs = data.counts_displs()
+        return
+    me = comm.rank
+    sl = [slice(None)] * data.ndim
+    sl[data.split] = slice(displs[me], displs[me] + counts[me])
+    if h5py is not None:  # h5py without MPI-IO: one writer at a time
         for r in range(comm.size):
-            if r == comm.rank and counts[r]:
-                with h5py.File(path, "r+") as handle:
-                    sl = [slice(None)] * data.ndim
-                    sl[data.split] = slice(displs[r], displs[r] + counts[r])
-                    handle[dataset][tuple(sl)] = data.larray.cpu().numpy()
+            if r == me and counts[me]:
+                _write_slab(path, dataset, tuple(sl), local)
             comm.Barrier()
+    else:
+        if counts[me]:
+            _write_slab(path, dataset, tuple(sl), local)
+        comm.Barrier()
 
-    DNDarray.save_hdf5 = lambda self, path, dataset, mode="w", **kwargs: save_hdf5(self, path, dataset, mode, **kwargs)
+
+def _write_slab(path: str, dataset: str, sl, local: np.ndarray) -> None:
+    if h5py is not None:
+        with h5py.File(path, "r+") as handle:
+            handle[dataset][sl] = local
+        return
+    mm = _h5lite.open_for_write(path, dataset)
+    mm[sl] = local.astype(mm.dtype, copy=False)
+    mm.flush()
+    del mm
+
+
+DNDarray.save_hdf5 = lambda self, path, dataset, mode="w", **kwargs: save_hdf5(self, path, dataset, mode, **kwargs)
+
 
 # --------------------------------------------------------------------------------------------- netcdf
-if nc is not None:
-    __all__ += ["load_netcdf", "save_netcdf"]
+def _netcdf3_header(variable: str, dims: List[str], shape, np_dtype: np.dtype) -> Tuple[bytes, int]:
+    """Classic netCDF (CDF-2, 64-bit offsets) header for ONE fixed-size variable; returns
+    (header bytes, data offset). Layout: magic, numrecs, dim_list, gatt_list, var_list."""
+    import struct
 
-    def load_netcdf(path: str, variable: str, dtype=types.float32, split: Optional[int] = None, device=None,
-                    comm=None) -> DNDarray:
-        comm = sanitize_comm(comm)
-        device = devices.sanitize_device(device)
-        htype = types.canonical_heat_type(dtype)
+    codes = {np.dtype("i1"): 1, np.dtype("S1"): 2, np.dtype("i2"): 3, np.dtype("i4"): 4, np.dtype("f4"): 5,
+             np.dtype("f8"): 6}
+    if np_dtype not in codes:
+        raise TypeError("netCDF classic has no {}".format(np_dtype))
+
+    def name(n: str) -> bytes:
+        raw = n.encode("utf-8")
+        return struct.pack(">i", len(raw)) + raw + b"\0" * ((-len(raw)) % 4)
+
+    h = b"CDF\x02" + struct.pack(">i", 0)
+    h += struct.pack(">ii", 0x0A, len(dims)) + b"".join(name(d) + struct.pack(">i", int(s)) for d, s in zip(dims, shape))
+    h += struct.pack(">ii", 0, 0)
+    vsize = int(np.prod(shape)) * np_dtype.itemsize
+    var = name(variable) + struct.pack(">i", len(dims)) + b"".join(struct.pack(">i", i) for i in range(len(dims)))
+    var += struct.pack(">ii", 0, 0) + struct.pack(">ii", codes[np_dtype], min(vsize + ((-vsize) % 4), 2 ** 31 - 1))
+    begin = len(h) + 8 + len(var) + 8
+    h += struct.pack(">ii", 0x0B, 1) + var + struct.pack(">q", begin)
+    assert len(h) == begin
+    return h, begin
+
+
+def load_netcdf(path: str, variable: str, dtype=types.float32, split: Optional[int] = None, device=None,
+                comm=None) -> DNDarray:
+    """Load a netCDF variable (netCDF4 when installed; otherwise netCDF-4/HDF5 files through the
+    built-in HDF5 reader and classic files through ``scipy.io.netcdf_file``)."""
+    if not isinstance(path, str):
+        raise TypeError("path must be str, not {}".format(type(path)))
+    if not isinstance(variable, str):
+        raise TypeError("dataset must be str, not {}".format(type(variable)))
+    comm = sanitize_comm(comm)
+    device = devices.sanitize_device(device)
+    htype = types.canonical_heat_type(dtype)
+    if nc is not None:
         with nc.Dataset(path, "r") as handle:
             data = handle[variable]
             gshape = tuple(data.shape)
             split = sanitize_axis(gshape, split)
-            _, _, sl = comm.chunk(gshape, split)
-            local = torch.tensor(np.asarray(data[sl]), dtype=htype.torch_type(), device=device.torch_device)
-        return DNDarray(local, gshape, htype, split, device, comm, True)
+            local = np.asarray(data[_hyperslab(gshape, split, comm)])
+    elif _h5lite.is_hdf5(path):
+        with _h5lite.open_file(path) as handle:
+            data = handle[variable]
+            gshape = tuple(data.shape)
+            split = sanitize_axis(gshape, split)
+            local = np.asarray(data[_hyperslab(gshape, split, comm)])
+    else:
+        from scipy.io import netcdf_file
 
-    def save_netcdf(data: DNDarray, path: str, variable: str, mode: str = "w", dimension_names=None,
-                    **kwargs) -> None:
-        comm = data.comm
-        if dimension_names is None:
-            dimension_names = ["dim_{}".format(i) for i in range(data.ndim)]
-        exc = None
+        with netcdf_file(path, "r", mmap=True) as handle:
+            data = handle.variables[variable].data
+            gshape = tuple(data.shape)
+            split = sanitize_axis(gshape, split)
+            local = np.array(data[_hyperslab(gshape, split, comm)])
+            del data  # the mmap must not be referenced when the file closes
+    t = torch.from_numpy(np.ascontiguousarray(local).astype(local.dtype.newbyteorder("=")))
+    t = t.to(device=device.torch_device, dtype=htype.torch_type())
+    return DNDarray(t, gshape, htype, split, device, comm, True)
+
+
+def save_netcdf(data: DNDarray, path: str, variable: str, mode: str = "w", dimension_names=None,
+                **kwargs) -> None:
+    """Write a DNDarray as a netCDF variable. Without netCDF4 a classic (CDF-2) file is written:
+    rank 0 writes the header, every rank writes its slab of the big-endian data block in place."""
+    if not isinstance(data, DNDarray):
+        raise TypeError("data must be heat tensor, not {}".format(type(data)))
+    if not isinstance(path, str):
+        raise TypeError("path must be str, not {}".format(type(path)))
+    if not isinstance(variable, str):
+        raise TypeError("variable must be str, not {}".format(type(variable)))
+    comm = data.comm
+    if dimension_names is None:
+        dimension_names = ["dim_{}".format(i) for i in range(data.ndim)]
+    elif isinstance(dimension_names, str):
+        dimension_names = [dimension_names]
+    if len(dimension_names) != data.ndim:
+        raise ValueError("{0} names given for {1} dimensions".format(len(dimension_names), data.ndim))
+    counts, displs = data.counts_displs() if data.is_distributed() else ((data.gshape[0] if data.ndim else 1,), (0,))
+    local = data.larray.cpu().numpy()
+    sl = [slice(None)] * data.ndim
+    if data.is_distributed():
+        sl[data.split] = slice(displs[comm.rank], displs[comm.rank] + counts[comm.rank])
+    exc = None
+    if nc is not None:
         if comm.rank == 0:
             try:
                 with nc.Dataset(path, mode) as handle:
                     for name, size in zip(dimension_names, data.gshape):
                         if name not in handle.dimensions:
                             handle.createDimension(name, size)
-                    handle.createVariable(variable, data.larray.cpu().numpy().dtype, tuple(dimension_names), **kwargs)
+                    handle.createVariable(variable, local.dtype, tuple(dimension_names), **kwargs)
             except Exception as e:
                 exc = e
         _exception_barrier(comm, exc)
-        counts, displs = data.counts_displs() if data.is_distributed() else ((data.gshape[0],), (0,))
         for r in range(comm.size):
             if r == comm.rank and (data.is_distributed() or r == 0):
                 with nc.Dataset(path, "r+") as handle:
-                    sl = [slice(None)] * data.ndim
-                    if data.is_distributed():
-                        sl[data.split] = slice(displs[r], displs[r] + counts[r])
-                    handle[variable][tuple(sl)] = data.larray.cpu().numpy()
+                    handle[variable][tuple(sl)] = local
             comm.Barrier()
+        return
+    if mode != "w":
+        raise NotImplementedError("without netCDF4 only mode='w' (a new classic file) is supported")
+    np_dtype = np.dtype(local.dtype)
+    if np_dtype == np.dtype("i8"):
+        np_dtype = np.dtype("i4")
+    elif np_dtype == np.dtype("bool") or np_dtype == np.dtype("u1"):
+        np_dtype = np.dtype("i1")
+    begin = 0
+    if comm.rank == 0:
+        try:
+            header, begin = _netcdf3_header(variable, dimension_names, data.gshape, np_dtype)
+            nbytes = int(np.prod(data.gshape)) * np_dtype.itemsize
+            with open(path, "wb") as f:
+                f.write(header)
+                f.truncate(begin + nbytes + ((-nbytes) % 4))
+        except Exception as e:
+            exc = e
+    _exception_barrier(comm, exc)
+    begin = comm.bcast(begin, root=0)
+    if data.is_distributed() or comm.rank == 0:
+        if local.size:
+            mm = np.memmap(path, dtype=np_dtype.newbyteorder(">"), mode="r+", offset=begin, shape=data.gshape)
+            mm[tuple(sl)] = local.astype(np_dtype)
+            mm.flush()
+            del mm
+    comm.Barrier()
 
-    DNDarray.save_netcdf = lambda self, path, variable, mode="w", **kwargs: save_netcdf(self, path, variable, mode, **kwargs)
+
+DNDarray.save_netcdf = lambda self, path, variable, mode="w", **kwargs: save_netcdf(self, path, variable, mode, **kwargs)
 
 
 # --------------------------------------------------------------------------------------------- dispatch

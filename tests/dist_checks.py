@@ -661,3 +661,36 @@ def check_custom_reduction_ops():
     ref = torch.topk(allc, k, dim=0).values
     # a one-rank reduction never calls the operator (MPI semantics): compare the sets
     assert torch.equal(res.sort(0, descending=True).values, ref)
+
+
+def check_io_hdf5_netcdf():
+    """HDF5 / netCDF round trips on every split (parallel slab writes), and reads of the
+    reference's own h5py / netCDF-4 fixtures when the reference tree is present."""
+    import os
+    import tempfile
+
+    comm = ht.MPI_WORLD
+    d = comm.bcast(tempfile.mkdtemp() if comm.rank == 0 else None, root=0)
+    data = np.arange(7 * 5, dtype=np.float32).reshape(7, 5) / 3.0
+    for split in (None, 0, 1):
+        x = ht.array(data, split=split)
+        ht.save_hdf5(x, os.path.join(d, "a.h5"), "data")
+        ht.save_hdf5(x.astype(ht.int64), os.path.join(d, "a.h5"), "ints", mode="a")
+        for rsplit in (None, 0, 1):
+            y = ht.load(os.path.join(d, "a.h5"), "data", split=rsplit)
+            assert_array_equal(y, data)
+            z = ht.load_hdf5(os.path.join(d, "a.h5"), "ints", dtype=ht.int64, split=rsplit)
+            assert_array_equal(z, data.astype(np.int64))
+        ht.save(x, os.path.join(d, "a.nc"), "var")
+        for rsplit in (None, 0, 1):
+            assert_array_equal(ht.load(os.path.join(d, "a.nc"), "var", split=rsplit), data)
+    part = ht.load_hdf5(os.path.join(d, "a.h5"), "data", split=0, load_fraction=0.5)
+    assert part.shape == (3, 5)
+    ref = "/root/reference/heat/datasets"
+    if os.path.isdir(ref):
+        iris_csv = ht.load_csv(os.path.join(ref, "iris.csv"), sep=";", split=0)
+        assert ht.allclose(ht.load(os.path.join(ref, "iris.h5"), "data", split=0), iris_csv)
+        assert ht.allclose(ht.load(os.path.join(ref, "iris.nc"), "data", split=1), iris_csv)
+        xd = ht.load_hdf5(os.path.join(ref, "diabetes.h5"), "x", split=0)
+        assert xd.shape == (442, 11)
+    comm.Barrier()
