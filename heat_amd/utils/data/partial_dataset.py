@@ -1,7 +1,8 @@
 """
 Streaming HDF5 datasets (reference ``heat/utils/data/partial_dataset.py``: ``PartialH5Dataset`` 32,
 ``PartialH5DataLoaderIter`` 224): only a window of the file is resident; a background thread
-loads the next window while the current one is consumed. Needs ``h5py``.
+loads the next window while the current one is consumed. Uses ``h5py`` when installed, the
+built-in HDF5 reader (``heat_amd.core._h5lite``) otherwise.
 """
 from __future__ import annotations
 
@@ -14,10 +15,16 @@ from torch.utils import data as torch_data
 
 from ...core.communication import MPI_WORLD
 
+from ...core import _h5lite
+
 try:
     import h5py
-except ImportError:  # optional dependency
+except ImportError:  # optional dependency: fall back to the built-in reader
     h5py = None
+
+
+def _open(path: str):
+    return h5py.File(path, "r") if h5py is not None else _h5lite.open_file(path)
 
 __all__ = ["PartialH5Dataset", "PartialH5DataLoaderIter", "queue_thread"]
 
@@ -42,8 +49,6 @@ class PartialH5Dataset(torch_data.Dataset):
     def __init__(self, file: str, comm=MPI_WORLD, dataset_names: Union[str, List[str]] = "data",
                  transforms: List[Callable] = None, use_gpu: bool = True, validate_set: bool = False,
                  initial_load: int = 7000, load_length: int = 1000):
-        if h5py is None:
-            raise ImportError("PartialH5Dataset requires h5py")
         self.ishuffle = False
         self.file = file
         self.comm = comm
@@ -51,7 +56,7 @@ class PartialH5Dataset(torch_data.Dataset):
         self.gpu = use_gpu and torch.cuda.is_available()
         self.validate_set = validate_set
         self.dataset_names = [dataset_names] if isinstance(dataset_names, str) else list(dataset_names)
-        with h5py.File(file, "r") as f:
+        with _open(file) as f:
             self.total_size = f[self.dataset_names[0]].shape[0]
         self.lcl_full_sz = self.total_size // comm.size
         self.local_data_start = self.lcl_full_sz * comm.rank
@@ -59,7 +64,7 @@ class PartialH5Dataset(torch_data.Dataset):
         self.load_initial = min(initial_load, self.lcl_full_sz)
         self.load_len = load_length
         self.loads_remaining = max(0, (self.lcl_full_sz - self.load_initial) // max(1, load_length))
-        self._f = h5py.File(file, "r")
+        self._f = _open(file)
         self.next_start = self.local_data_start + self.load_initial
         for name in self.dataset_names:
             arr = torch.tensor(self._f[name][self.local_data_start: self.next_start])

@@ -694,3 +694,29 @@ def check_io_hdf5_netcdf():
         xd = ht.load_hdf5(os.path.join(ref, "diabetes.h5"), "x", split=0)
         assert xd.shape == (442, 11)
     comm.Barrier()
+
+
+def check_partial_h5_dataset():
+    """PartialH5Dataset streams this rank's share of an HDF5 file window by window
+    (reference utils/data/tests/test_partial_dataset.py)."""
+    import os
+    import tempfile
+
+    comm = ht.MPI_WORLD
+    d = comm.bcast(tempfile.mkdtemp() if comm.rank == 0 else None, root=0)
+    n = 40 * comm.size
+    data = np.arange(n * 3, dtype=np.float32).reshape(n, 3)
+    labels = np.arange(n, dtype=np.float32)
+    path = os.path.join(d, "p.h5")
+    ht.save_hdf5(ht.array(data, split=0), path, "data")
+    ht.save_hdf5(ht.array(labels, split=0), path, "labels", mode="a")
+    ds = ht.utils.data.PartialH5Dataset(path, comm=comm, dataset_names=["data", "labels"], use_gpu=False,
+                                        initial_load=16, load_length=8)
+    loader = ht.utils.data.DataLoader(ds, batch_size=4)
+    seen = []
+    for x, y in loader:
+        assert torch.equal(x[:, 0] / 3, y)
+        seen.append(y)
+    got = torch.cat(seen).sort().values
+    lo = comm.rank * (n // comm.size)
+    assert got.numel() >= 16 and float(got.min()) >= lo and float(got.max()) < lo + n // comm.size
