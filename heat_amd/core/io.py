@@ -52,12 +52,9 @@ def supports_netcdf() -> bool:
 
 def _exception_barrier(comm, exc: Optional[BaseException]):
     """Propagate a failure on any rank to every rank (reference io.py:593-650, made generic)."""
-    flags = comm.allgather(None if exc is None else repr(exc))
-    bad = [(r, f) for r, f in enumerate(flags) if f is not None]
-    if bad:
-        if exc is not None:
-            raise exc
-        raise RuntimeError("rank {} failed: {}".format(bad[0][0], bad[0][1]))
+    from ..parallel.guard import exception_barrier
+
+    exception_barrier(comm, exc)
 
 
 # --------------------------------------------------------------------------------------------- npy

@@ -70,30 +70,36 @@ __global__ __launch_bounds__(256) void h3_pack_points(const float* __restrict__ 
   if (grp == 0) sx[row] = s;
 }
 
-// One workgroup: global max |c| -> s_C, then the packed image
+// Centroid packing in two short launches (a single-workgroup version took 90 us at k=1024):
+// h3_cmax: max |c| over all centroids -> meta[1] (float bits, atomicMax on a zeroed word; valid
+// for non-negative floats); h3_pack_centroids: s_C = 2^-e from it, the packed image
 //   image[chunk][cb][ks][hl][lane][8] (lane = h*32 + j, centroid chunk*CB + cb*32 + j,
-//   features h*F2 + 8 ks .. +8), u[c] = s_C |c|^2 / 2 (+inf for padding), meta[0] = s_C.
-template <int FPAD>
-__global__ __launch_bounds__(1024) void h3_pack_centroids(const float* __restrict__ C, int k, int f, int64_t ldc,
-                                                          int kpad, _Float16* __restrict__ image,
-                                                          float* __restrict__ u, float* __restrict__ meta) {
-  using K = H3Cfg<FPAD>;
-  __shared__ float red[1024];
-  const int tid = threadIdx.x;
+//   features h*F2 + 8 ks .. +8), u[c] = s_C |c|^2 / 2 (+inf for padding) and meta[0] = s_C.
+__global__ __launch_bounds__(256) void h3_cmax(const float* __restrict__ C, int k, int f, int64_t ldc,
+                                               float* __restrict__ meta) {
   float mx = 0.f;
-  for (int64_t e = tid; e < (int64_t)k * f; e += 1024) mx = fmaxf(mx, fabsf(C[(e / f) * ldc + e % f]));
-  red[tid] = mx;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
-    __syncthreads();
-  }
-  int ex = 0;
-  if (red[0] > 0.f && red[0] < __builtin_huge_valf()) frexpf(red[0], &ex);
-  const float s = ldexpf(1.f, -ex);
-  if (tid == 0) meta[0] = s;
+  const int64_t total = (int64_t)k * f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256)
+    mx = fmaxf(mx, fabsf(C[(e / f) * ldc + e % f]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0 && mx > 0.f && mx < __builtin_huge_valf())
+    atomicMax(reinterpret_cast<unsigned int*>(meta + 1), __float_as_uint(mx));
+}
+
+template <int FPAD>
+__global__ __launch_bounds__(256) void h3_pack_centroids(const float* __restrict__ C, int k, int f, int64_t ldc,
+                                                         int kpad, _Float16* __restrict__ image,
+                                                         float* __restrict__ u, float* __restrict__ meta) {
+  using K = H3Cfg<FPAD>;
   constexpr int G8 = FPAD / 8;
-  for (int64_t it = tid; it < (int64_t)kpad * G8; it += 1024) {
+  const float mxc = meta[1];
+  int ex = 0;
+  if (mxc > 0.f) frexpf(mxc, &ex);
+  const float s = ldexpf(1.f, -ex);
+  const int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (it == 0) meta[0] = s;
+  if (it < (int64_t)kpad * G8) {
     const int c = (int)(it / G8), g8 = (int)(it % G8);
     const int fe = g8 * 8;
     halfx8 hi, lo;
@@ -110,8 +116,8 @@ __global__ __launch_bounds__(1024) void h3_pack_centroids(const float* __restric
     const int64_t base = ((((int64_t)chunk * (K::CB / 32) + cb) * K::KS + ks) * 2) * 64 * 8;
     *reinterpret_cast<halfx8*>(image + base + (int64_t)lane * 8) = hi;
     *reinterpret_cast<halfx8*>(image + base + 64 * 8 + (int64_t)lane * 8) = lo;
-  }
-  for (int c = tid; c < kpad; c += 1024) {
+  } else if (it < (int64_t)kpad * (G8 + 1)) {
+    const int c = (int)(it - (int64_t)kpad * G8);
     if (c < k) {
       float acc = 0.f;
       for (int i = 0; i < f; ++i) {
@@ -629,7 +635,7 @@ HA_EXPORT int64_t ha_h3_workspace_bytes(int k, int f) {
   if (fpad < 0 || k <= 0) return -1;
   const int cb = fpad >= 128 ? 64 : 128;
   const int64_t kpad = (int64_t)(k + cb - 1) / cb * cb;
-  return kpad * fpad * 2 * 2 + kpad * 4 + 16;
+  return kpad * fpad * 2 * 2 + kpad * 4 + 16;  // image + u + meta {s_C, max|c|}
 }
 
 HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f, const float* C, int k, int64_t ldc,
@@ -647,7 +653,10 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
 #define HA_H3(FP)                                                                                           \
   case FP: {                                                                                                \
     using KC = H3Cfg<FP>;                                                                                   \
-    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3(1), dim3(1024), 0, s, C, k, f, ldc, kpad, image, u, meta); \
+    hipMemsetAsync(meta, 0, 2 * sizeof(float), s);                                                          \
+    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
+                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
     const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                         \
     hipLaunchKernelGGL((h3_assign_p<FP, 2, true, 2>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u,  \

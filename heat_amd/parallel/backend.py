@@ -58,6 +58,9 @@ def ensure_initialized() -> bool:
         ndev = torch.cuda.device_count()
         torch.cuda.set_device(local % ndev)
     timeout = datetime.timedelta(seconds=int(os.environ.get("HEAT_COMM_TIMEOUT", "1800")))
+    # watchdog: a collective that does not complete within the timeout aborts the communicator
+    # and raises on every rank instead of hanging the job
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout, **kwargs)
     _INITIALISED_BY_US = True
     atexit.register(shutdown)

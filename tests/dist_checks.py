@@ -720,3 +720,24 @@ def check_partial_h5_dataset():
     got = torch.cat(seen).sort().values
     lo = comm.rank * (n // comm.size)
     assert got.numel() >= 16 and float(got.min()) >= lo and float(got.max()) < lo + n // comm.size
+
+
+def check_collective_guard():
+    """A failure on one rank surfaces on every rank (no deadlock in the next collective)."""
+    from heat_amd.parallel import RemoteRankError, collective_guard
+
+    comm = ht.MPI_WORLD
+    raised = None
+    try:
+        with collective_guard(comm):
+            if comm.rank == comm.size - 1:
+                raise ValueError("bad input on the last rank")
+    except ValueError:
+        raised = "own"
+    except RemoteRankError as e:
+        raised = "remote"
+        assert e.rank == comm.size - 1
+    assert raised == ("own" if comm.rank == comm.size - 1 else "remote")
+    with collective_guard(comm):
+        pass
+    assert int(ht.sum(ht.arange(10, split=0)).item()) == 45  # the world is still usable
