@@ -5,6 +5,7 @@ tensors; also the numerics oracle of the tests).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import NamedTuple, Optional, Tuple
 
 import torch
@@ -12,7 +13,7 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare"]
+__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep"]
 
 _NUM_CUS = {}
 
@@ -338,6 +339,40 @@ def lasso_prepare(X: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         return XT, colsq
     XT = X.t().contiguous()
     return XT, (XT * XT).sum(1)
+
+
+class LassoSweep:
+    """A reusable coordinate-descent sweep over fixed (XT, r, theta, colsq) buffers.
+
+    On a single device the sweep's 2n+1 launches are captured ONCE into a hipGraph
+    (``torch.cuda.CUDAGraph``) and replayed, so a sweep costs one graph launch instead of
+    2n+1 kernel launches plus the per-call Python/ctypes overhead. Distributed sweeps (a scalar
+    all-reduce per coordinate) and host tensors run :func:`lasso_epoch` directly."""
+
+    def __init__(self, XT: torch.Tensor, r: torch.Tensor, theta: torch.Tensor, colsq: torch.Tensor, lam: float,
+                 m_global: int, allreduce=None, use_graph: bool = True):
+        self.args = (XT, r, theta, colsq, lam, m_global, allreduce)
+        self.graph = None
+        self.use_graph = (use_graph and allreduce is None and XT.is_cuda and use_native(XT)
+                          and XT.dtype == torch.float32 and XT.shape[0] >= 2
+                          and os.environ.get("HEAT_AMD_NO_GRAPHS", "0") != "1")
+
+    def __call__(self) -> None:
+        if not self.use_graph:
+            lasso_epoch(*self.args)
+            return
+        if self.graph is None:
+            side = torch.cuda.Stream(device=self.args[0].device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                lasso_epoch(*self.args)  # this call's sweep (and the warm-up torch requires)
+            torch.cuda.current_stream().wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                lasso_epoch(*self.args)  # captured, not executed
+            self.graph = g
+            return
+        self.graph.replay()
 
 
 def lasso_epoch(XT: torch.Tensor, r: torch.Tensor, theta: torch.Tensor, colsq: torch.Tensor, lam: float,

@@ -97,9 +97,11 @@ class Lasso(RegressionMixin, BaseEstimator):
             x.comm.Allreduce(MPI.IN_PLACE, t, MPI.SUM)
 
         i = 0
+        sweep = ops.LassoSweep(XT, r, theta, colsq, float(self.__lam), m, allreduce if dist else None,
+                               use_graph=self.max_iter >= 3)  # capture pays off from the 3rd sweep
         for i in range(self.max_iter):
             theta_old = theta.clone()
-            ops.lasso_epoch(XT, r, theta, colsq, float(self.__lam), m, allreduce if dist else None)
+            sweep()
             if self.tol is not None:
                 diff = float(torch.sqrt(torch.mean((theta - theta_old) ** 2)))
                 if diff < self.tol:

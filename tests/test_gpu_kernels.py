@@ -222,3 +222,18 @@ def test_lasso_prepare(m, n):
     XT, colsq = ops.lasso_prepare(X)
     assert torch.equal(XT, X.t().contiguous())
     assert torch.allclose(colsq.double(), (X.double() ** 2).sum(0), rtol=1e-5)
+
+
+def test_lasso_graph_replay_matches_eager(gpu, monkeypatch):
+    import heat_amd as ht
+
+    ht.random.seed(4)
+    x = ht.random.randn(20000, 12)
+    y = ht.matmul(x, ht.random.randn(12, 1)) + 0.05 * ht.random.randn(20000, 1)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("HEAT_AMD_NO_GRAPHS", flag)
+        est = ht.regression.Lasso(lam=0.01, max_iter=20, tol=None)
+        est.fit(x, y)
+        res.append(est.theta.larray.clone())
+    assert torch.allclose(res[0], res[1], atol=1e-5)
