@@ -109,25 +109,31 @@ __global__ __launch_bounds__(256, 2) void cdist_l2(const float* __restrict__ X, 
   }
 }
 
-// L1 distance: VALU, 64x64 outputs per workgroup, 4x4 per thread, features staged through LDS
-constexpr int LB = 64, LK = 32;
+// Difference-based (exact) distances on the VALU, 64x64 outputs per workgroup: thread (tr, tc)
+// owns rows tr + 16u and the 4 CONSECUTIVE columns 4tc..4tc+3, so the Y operand is one aligned
+// ds_read_b128 per feature, the squared-difference accumulation runs on packed fp32
+// (v_pk_add_f32 / v_pk_fma_f32: two pairs per instruction) and the output rows leave as 16-byte
+// stores (16 lanes = 256 contiguous bytes).  XCD-banded tile order as in the MFMA kernels.
 // OP 0: sum |x-y| ; OP 1: sqrt(sum (x-y)^2) ; OP 2: sum (x-y)^2 ; OP 3: exp(-scale * sum (x-y)^2)
-// (the exact, cancellation-free L2 family used when quadratic_expansion=False)
+constexpr int LB = 64, LK = 32, LYS = LB + 4;
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
 template <int OP>
 __global__ __launch_bounds__(256) void cdist_vk(const float* __restrict__ X, int64_t m, const float* __restrict__ Y,
                                                 int64_t n, int f, int64_t ldx, int64_t ldy, float* __restrict__ C,
-                                                int64_t ldc, float scale) {
+                                                int64_t ldc, float scale, int64_t per_xcd, int vec_out) {
   __shared__ float sx[LK][LB + 1];
-  __shared__ float sy[LK][LB + 1];
+  __shared__ __attribute__((aligned(16))) float sy[LK][LYS];
   const int tid = threadIdx.x;
   const int64_t tiles_n = (n + LB - 1) / LB;
-  const int64_t row0 = (blockIdx.x / tiles_n) * LB, col0 = (blockIdx.x % tiles_n) * LB;
-  const int tr = tid / 16, tc = tid % 16;  // 16x16 threads, 4x4 outputs each
-  float acc[4][4];
+  const int64_t tiles = ((m + LB - 1) / LB) * tiles_n;
+  const int64_t t = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  if (t >= tiles) return;
+  const int64_t row0 = (t / tiles_n) * LB, col0 = (t % tiles_n) * LB;
+  const int tr = tid / 16, tc = tid % 16;
+  floatx2 acc[4][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+  for (int a = 0; a < 4; ++a) acc[a][0] = acc[a][1] = (floatx2)(0.f);
   for (int k0 = 0; k0 < f; k0 += LK) {
     for (int e = tid; e < LB * LK; e += 256) {
       const int r = e / LK, c = e % LK;
@@ -138,33 +144,43 @@ __global__ __launch_bounds__(256) void cdist_vk(const float* __restrict__ X, int
     __syncthreads();
     const int kk = (f - k0) < LK ? (f - k0) : LK;
     for (int k = 0; k < kk; ++k) {
-      float a[4], b[4];
+      const floatx4 b = *reinterpret_cast<const floatx4*>(&sy[k][4 * tc]);
+      const floatx2 b01 = {b[0], b[1]}, b23 = {b[2], b[3]};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a[u] = sx[k][tr + 16 * u];
-        b[u] = sy[k][tc + 16 * u];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float d = a[u] - b[v];
-          if (OP == 0) acc[u][v] += fabsf(d);
-          else acc[u][v] = fmaf(d, d, acc[u][v]);
+        const float av = sx[k][tr + 16 * u];
+        const floatx2 a2 = {av, av};
+        const floatx2 d0 = a2 - b01, d1 = a2 - b23;
+        if (OP == 0) {
+          acc[u][0] += __builtin_elementwise_abs(d0);
+          acc[u][1] += __builtin_elementwise_abs(d1);
+        } else {
+          acc[u][0] = __builtin_elementwise_fma(d0, d0, acc[u][0]);
+          acc[u][1] = __builtin_elementwise_fma(d1, d1, acc[u][1]);
         }
+      }
     }
     __syncthreads();
   }
+  const int64_t col = col0 + 4 * tc;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int64_t row = row0 + tr + 16 * u;
+    if (row >= m) continue;
+    float o[4] = {acc[u][0][0], acc[u][0][1], acc[u][1][0], acc[u][1][1]};
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int64_t col = col0 + tc + 16 * v;
-      float r = acc[u][v];
-      if (OP == 1) r = sqrtf(r);
-      else if (OP == 3) r = __expf(-r * scale);
-      if (row < m && col < n) C[row * ldc + col] = r;
+      if (OP == 1) o[v] = __builtin_amdgcn_sqrtf(o[v]);
+      else if (OP == 3) o[v] = __expf(-o[v] * scale);
+    }
+    float* cp = C + row * ldc + col;
+    if (vec_out && col + 3 < n) {
+      const floatx4 ov = {o[0], o[1], o[2], o[3]};
+      __builtin_nontemporal_store(ov, reinterpret_cast<floatx4*>(cp));
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (col + v < n) cp[v] = o[v];
     }
   }
 }
@@ -179,13 +195,15 @@ HA_EXPORT int ha_cdist(const float* X, int64_t m, const float* Y, int64_t n, int
   hipStream_t s = (hipStream_t)stream;
   if (mode >= 3) {
     const int64_t tiles = ((m + LB - 1) / LB) * ((n + LB - 1) / LB);
-    if (tiles > 0x7fffffffLL) return HA_UNSUPPORTED;
-    const dim3 g((unsigned)tiles), b(256);
+    const int64_t per_xcd = (tiles + 7) / 8;
+    if (per_xcd * 8 > 0x7fffffffLL) return HA_UNSUPPORTED;
+    const int vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+    const dim3 g((unsigned)(per_xcd * 8)), b(256);
     switch (mode) {
-      case 3: hipLaunchKernelGGL(cdist_vk<0>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
-      case 4: hipLaunchKernelGGL(cdist_vk<1>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
-      case 5: hipLaunchKernelGGL(cdist_vk<2>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
-      case 6: hipLaunchKernelGGL(cdist_vk<3>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale); break;
+      case 3: hipLaunchKernelGGL(cdist_vk<0>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 4: hipLaunchKernelGGL(cdist_vk<1>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 5: hipLaunchKernelGGL(cdist_vk<2>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 6: hipLaunchKernelGGL(cdist_vk<3>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
       default: return HA_BAD_ARG;
     }
     return ha_launch_status();
