@@ -640,6 +640,23 @@ class DNDarray:
                 new_split = self._out_split(key, adv, gout)
             return DNDarray(res.reshape(gout), gout, self.dtype, new_split, self.device, self.comm, True)
 
+        if not adv and any(k is None for k in key):
+            # new axes: index without them, then insert unit dims into the local result
+            r = self.__getitem__(tuple(k for k in key if k is not None))
+            out_pos, dim_pos, new_axes = 0, [], []
+            for k in key:
+                if k is None:
+                    new_axes.append(out_pos)
+                    out_pos += 1
+                elif not isinstance(k, int):
+                    dim_pos.append(out_pos)
+                    out_pos += 1
+            lshape = list(r.larray.shape)
+            for a in new_axes:
+                lshape.insert(a, 1)
+            split = dim_pos[r.split] if r.split is not None else None
+            return DNDarray(r.larray.reshape(lshape), gout, self.dtype, split, self.device, self.comm, r.balanced)
+
         s = self.split
         ks = key[s]
         n_adv = sum(1 for k in key if isinstance(k, torch.Tensor))

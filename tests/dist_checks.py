@@ -741,3 +741,70 @@ def check_collective_guard():
     with collective_guard(comm):
         pass
     assert int(ht.sum(ht.arange(10, split=0)).item()) == 45  # the world is still usable
+
+
+def check_getitem_setitem_semantics():
+    """Split propagation and local shapes of __getitem__/__setitem__ (the reference's rules,
+    heat/core/dndarray.py:661-1549; cases from its bug reports #730/#825)."""
+    comm = ht.MPI_WORLD
+    p = comm.size
+    # assigning a smaller split array into an interior window
+    for split, win, setshape in ((0, (slice(1, -1), slice(1, -1)), (100, 100)),
+                                 (1, (slice(-30, None), slice(1, -1)), (30, 100)),
+                                 (1, (slice(1, -1), slice(None, 20)), (100, 20))):
+        a = ht.ones((102, 102), split=split)
+        a[win] = ht.zeros(setshape, split=split)
+        assert bool(ht.all(a[win] == 0))
+        ref = np.ones((102, 102), np.float32)
+        ref[win] = 0
+        assert_array_equal(a, ref, check_split_chunks=False)
+    # split of a result after integer indexing
+    a = ht.ones((10, 25, 30), split=1)
+    if p > 1:
+        assert a[0].split == 0
+        assert a[:, 0, :].split is None
+        assert a[:, :, 0].split == 1
+    # scalar get / set, numpy and torch integer keys
+    a = ht.zeros((13, 5), split=0)
+    a[10, np.array(0)] = 1
+    assert float(a[10, 0].item()) == 1 and a[10, 0].dtype == ht.float32
+    a = ht.zeros((13, 5), split=0)
+    a[10] = 1
+    b = a[torch.tensor(10)]
+    assert bool((b == 1).all()) and b.gshape == (5,) and b.dtype == ht.float32
+    a[-1] = 2
+    assert bool((a[-1] == 2).all())
+    # slices keep the split and are not rebalanced
+    a = ht.zeros((13, 5), split=0)
+    a[1:4] = 1
+    s_ = a[1:4]
+    assert bool((s_ == 1).all()) and s_.gshape == (3, 5) and s_.split == 0
+    counts = a.comm.counts_displs_shape((13, 5), 0)[0]
+    lo = sum(counts[: comm.rank])
+    mine = max(0, min(lo + counts[comm.rank], 4) - max(lo, 1))
+    assert s_.lshape == (mine, 5)
+    b = a[1:4, np.int64(1)]
+    assert b.gshape == (3,) and b.split == 0 and bool((b == 1).all())
+    c = ht.zeros((13, 5), split=0)
+    c[8:12, ht.array(1)] = 1
+    b = c[8:12, np.int64(1)]
+    assert b.gshape == (4,) and b.split == 0 and bool((b == 1).all())
+    # boolean mask keeps the split axis, values equal numpy
+    data = np.arange(24, dtype=np.float32).reshape(6, 4)
+    for split in (None, 0, 1):
+        x = ht.array(data, split=split)
+        m = x > 10
+        got = x[m]
+        assert np.array_equal(np.sort(got.numpy()), data[data > 10])
+        x[m] = -1
+        ref = data.copy()
+        ref[ref > 10] = -1
+        assert_array_equal(x, ref, check_split_chunks=False)
+    # advanced (list) indexing along the split axis and step slices
+    for split in (None, 0, 1):
+        x = ht.array(data, split=split)
+        assert_array_equal(x[[4, 0, 5]], data[[4, 0, 5]], check_split_chunks=False)
+        assert_array_equal(x[::-2], data[::-2], check_split_chunks=False)
+        assert_array_equal(x[1:5:2, ::3], data[1:5:2, ::3], check_split_chunks=False)
+        assert_array_equal(x[..., 1], data[..., 1], check_split_chunks=False)
+        assert_array_equal(x[None, 2], data[None, 2], check_split_chunks=False)
