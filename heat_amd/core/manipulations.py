@@ -217,9 +217,26 @@ def _at_least_2d_col(a: DNDarray) -> DNDarray:
 
 
 def column_stack(arrays: Sequence[DNDarray]) -> DNDarray:
-    """Stack 1-D arrays as columns (2-D arrays are concatenated along axis 1)."""
-    arrays = [_at_least_2d_col(a) for a in arrays]
-    return concatenate(arrays, axis=1)
+    """Stack 1-D arrays as columns; 2-D arrays are concatenated along axis 1 (reference
+    manipulations.py:92). A distributed 1-D array becomes a column split like the 2-D operands:
+    along axis 1 when they are split there (the reference's rule), along the rows otherwise (the
+    reference raises for that mix)."""
+    arrays = list(arrays)
+    if any(a.ndim > 2 for a in arrays):
+        raise ValueError("Arrays must be 1-D or 2-D")
+    if all(a.ndim == 1 for a in arrays):
+        return stack(arrays, axis=1)
+    col_split = 1 if any(a.ndim == 2 and a.split == 1 for a in arrays) else 0
+    out = []
+    for a in arrays:
+        if a.ndim == 1:
+            c = _at_least_2d_col(a)
+            if c.split is not None and c.split != col_split:
+                c = resplit(c, col_split)
+            out.append(c)
+        else:
+            out.append(a)
+    return concatenate(out, axis=1)
 
 
 def hstack(arrays: Sequence[DNDarray]) -> DNDarray:

@@ -808,3 +808,46 @@ def check_getitem_setitem_semantics():
         assert_array_equal(x[1:5:2, ::3], data[1:5:2, ::3], check_split_chunks=False)
         assert_array_equal(x[..., 1], data[..., 1], check_split_chunks=False)
         assert_array_equal(x[None, 2], data[None, 2], check_split_chunks=False)
+
+
+def check_manipulations_more():
+    """The remaining manipulation / statistics functions against NumPy on every split axis."""
+    rng = _rng(21)
+    a3 = rng.normal(size=(4, 6, 5)).astype(np.float32)
+    a2 = rng.normal(size=(6, 4)).astype(np.float32)
+    v = rng.normal(size=(6,)).astype(np.float32)
+    for split in for_splits(a3):
+        x = ht.array(a3, split=split)
+        assert_array_equal(ht.moveaxis(x, 0, -1), np.moveaxis(a3, 0, -1), check_split_chunks=False)
+        assert_array_equal(ht.swapaxes(x, 0, 2), np.swapaxes(a3, 0, 2), check_split_chunks=False)
+        assert_array_equal(ht.rot90(x, 1, (0, 1)), np.rot90(a3, 1, (0, 1)), check_split_chunks=False)
+        assert_array_equal(ht.rot90(x, -1, (1, 2)), np.rot90(a3, -1, (1, 2)), check_split_chunks=False)
+        assert_array_equal(ht.ravel(x), np.ravel(a3), check_split_chunks=False)
+        for got, ref in zip(ht.dsplit(x, 5), np.dsplit(a3, 5)):
+            assert_array_equal(got, ref, check_split_chunks=False)
+        for got, ref in zip(ht.hsplit(x, [2, 5]), np.hsplit(a3, [2, 5])):
+            assert_array_equal(got, ref, check_split_chunks=False)
+        for got, ref in zip(ht.vsplit(x, 2), np.vsplit(a3, 2)):
+            assert_array_equal(got, ref, check_split_chunks=False)
+        assert ht.shape(x) == a3.shape
+    for split in for_splits(a2):
+        x = ht.array(a2, split=split)
+        assert_array_equal(ht.fliplr(x), np.fliplr(a2), check_split_chunks=False)
+        assert_array_equal(ht.flipud(x), np.flipud(a2), check_split_chunks=False)
+        y = ht.array(a2 * 2, split=split)
+        assert_array_equal(ht.maximum(x, y), np.maximum(a2, a2 * 2), check_split_chunks=False)
+        assert_array_equal(ht.minimum(x, y), np.minimum(a2, a2 * 2), check_split_chunks=False)
+        vs = ht.array(v, split=0 if split is not None else None)
+        assert_array_equal(ht.column_stack((x, vs)), np.column_stack((a2, v)), check_split_chunks=False)
+        assert_array_equal(ht.row_stack((x, x)), np.vstack((a2, a2)), check_split_chunks=False)
+    ints = rng.integers(0, 7, size=50)
+    for split in (None, 0):
+        xi = ht.array(ints, split=split)
+        assert_array_equal(ht.bincount(xi), np.bincount(ints))
+        w = ht.array(np.linspace(0, 1, 50, dtype=np.float32), split=split)
+        assert_array_equal(ht.bincount(xi, weights=w, minlength=10),
+                           np.bincount(ints, weights=np.linspace(0, 1, 50, dtype=np.float32), minlength=10),
+                           rtol=1e-5)
+        xf = ht.array(ints.astype(np.float32), split=split)
+        h = ht.histc(xf, bins=7, min=0, max=7)
+        assert_array_equal(h, np.histogram(ints, bins=7, range=(0, 7))[0].astype(np.float32))
