@@ -42,16 +42,17 @@ def _torch_data(dndarray: DNDarray, summarize: bool) -> torch.Tensor:
     edge = torch._tensor_str.PRINT_OPTS.edgeitems
     s = dndarray.split
     t = dndarray.larray
-    # reduce every non-split dimension to its edge items locally
+    # reduce every summarised dimension to edge+1 leading and edge trailing items: the gathered
+    # tensor stays larger than 2*edge along it, so torch's formatter still prints the "..." there
     for d in range(t.dim()):
         if d != s and t.shape[d] > 2 * edge:
-            idx = torch.cat([torch.arange(edge), torch.arange(t.shape[d] - edge, t.shape[d])]).to(t.device)
+            idx = torch.cat([torch.arange(edge + 1), torch.arange(t.shape[d] - edge, t.shape[d])]).to(t.device)
             t = t.index_select(d, idx)
     n = dndarray.gshape[s]
     counts, displs = dndarray.counts_displs()
     me = dndarray.comm.rank
     if n > 2 * edge:
-        keep = [i for i in range(counts[me]) if displs[me] + i < edge or displs[me] + i >= n - edge]
+        keep = [i for i in range(counts[me]) if displs[me] + i < edge + 1 or displs[me] + i >= n - edge]
         t = t.index_select(s, torch.tensor(keep, dtype=torch.int64, device=t.device))
     return dndarray.comm.allgather_tensor(t.contiguous(), s)
 
@@ -61,10 +62,6 @@ def _tensor_str(dndarray: DNDarray, indent: int) -> str:
     data = _torch_data(dndarray, summarize)
     if dndarray.comm.rank != 0:
         return ""
-    if summarize and dndarray.is_distributed():
-        # the gathered edges form a small tensor; re-insert the summary marks by printing it as
-        # a tensor of the edge items only
-        pass
     if data.dim() == 0:
         return torch._tensor_str._scalar_str(data, torch._tensor_str._Formatter(data)) if hasattr(
             torch._tensor_str, "_scalar_str") else str(data.item())

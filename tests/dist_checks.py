@@ -851,3 +851,34 @@ def check_manipulations_more():
         xf = ht.array(ints.astype(np.float32), split=split)
         h = ht.histc(xf, bins=7, min=0, max=7)
         assert_array_equal(h, np.histogram(ints, bins=7, range=(0, 7))[0].astype(np.float32))
+
+
+def check_printing():
+    """``str(DNDarray)`` matches the reference's format (printed on rank 0 only)."""
+    import math
+
+    comm = ht.MPI_WORLD
+    try:
+        s = str(ht.array([], dtype=ht.int64, device="cpu"))
+        assert comm.rank != 0 or s == "DNDarray([], dtype=ht.int64, device=cpu:0, split=None)"
+        s = str(ht.array(42, device="cpu"))
+        assert comm.rank != 0 or s == "DNDarray(42, dtype=ht.int64, device=cpu:0, split=None)"
+        s = str(ht.arange(2 * 3 * 4, device="cpu").reshape((2, 3, 4)))
+        assert comm.rank != 0 or s == ("DNDarray([[[ 0,  1,  2,  3],\n           [ 4,  5,  6,  7],\n"
+                                       "           [ 8,  9, 10, 11]],\n\n          [[12, 13, 14, 15],\n"
+                                       "           [16, 17, 18, 19],\n           [20, 21, 22, 23]]], dtype=ht.int32, "
+                                       "device=cpu:0, split=None)")
+        s = str(ht.arange(12 * 13 * 14, split=0, device="cpu").reshape((12, 13, 14)))
+        if comm.rank == 0:
+            assert s.startswith("DNDarray([[[   0,    1,    2,  ...,   11,   12,   13],\n")
+            assert s.endswith("[2170, 2171, 2172,  ..., 2181, 2182, 2183]]], dtype=ht.int32, device=cpu:0, "
+                              "split=0)")
+        ht.set_printoptions(precision=2)
+        s = str(ht.arange(0.5, 2 * 3 * 4 + 0.5, split=0, device="cpu").reshape((2, 3, 4)))
+        assert comm.rank != 0 or "[20.50, 21.50, 22.50, 23.50]]], dtype=ht.float32, device=cpu:0, split=0)" in s
+        ht.set_printoptions(profile="full")
+        assert ht.get_printoptions()["threshold"] == math.inf
+        ht.set_printoptions(profile="short")
+        assert ht.get_printoptions()["precision"] == 2 and ht.get_printoptions()["edgeitems"] == 2
+    finally:
+        ht.set_printoptions(profile="default")
