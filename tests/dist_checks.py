@@ -882,3 +882,44 @@ def check_printing():
         assert ht.get_printoptions()["precision"] == 2 and ht.get_printoptions()["edgeitems"] == 2
     finally:
         ht.set_printoptions(profile="default")
+
+
+def check_random_counter_semantics():
+    """Threefry stream properties (reference core/tests/test_random.py): reseeding reproduces,
+    consecutive calls differ, 64-bit counter overflow continues the stream, a 128-bit overflow
+    wraps to the beginning, and values do not depend on shape / split / process count."""
+    seed = 12345
+    ht.random.seed(seed)
+    a = ht.random.rand(2, 5, 7, 3, split=0)
+    assert a.dtype == ht.float32 and a.larray.dtype == torch.float32
+    b = ht.random.rand(2, 5, 7, 3, split=0)
+    assert not bool(ht.equal(a, b))
+    ht.random.seed(seed)
+    assert bool(ht.equal(a, ht.random.rand(2, 5, 7, 3, dtype=ht.float32, split=0)))
+    ht.random.set_state(("Threefry", seed, 0xFFFFFFFFFFFFFFF0))
+    a = ht.random.rand(2, 3, 4, 5, split=0).numpy().ravel()
+    ht.random.set_state(("Threefry", seed, 0x10000000000000000))
+    b = ht.random.rand(2, 44, split=0).numpy().ravel()
+    assert a.dtype == np.float32 and np.array_equal(a[32:], b)
+    ht.random.set_state(("Threefry", seed, 0x100000000))
+    a = ht.random.rand(2, 44)
+    ht.random.seed(seed)
+    assert not bool(ht.equal(a, ht.random.rand(2, 44)))
+    ht.random.seed(seed)
+    a = ht.random.rand(2, 34, split=0).numpy().ravel()
+    ht.random.set_state(("Threefry", seed, 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFF0))
+    b = ht.random.rand(2, 50, split=0).numpy().ravel()
+    assert np.array_equal(a, b[32:])
+    ht.random.seed(seed)
+    a = ht.random.rand(2, 50, split=0).numpy().ravel()
+    ht.random.seed(seed)
+    assert np.array_equal(a, ht.random.rand(100, split=None).numpy())
+    ht.random.seed(seed)
+    a = ht.random.randn(3, 5, 2, 9, split=3)
+    ht.random.seed(seed)
+    assert bool(ht.equal(a, ht.random.randn(3, 5, 2, 9, split=3)))
+    ht.random.seed(seed)
+    ri = ht.random.randint(-5, 9, (40,), split=0, dtype=ht.int64).numpy()
+    assert ri.min() >= -5 and ri.max() < 9
+    p = ht.random.permutation(30)
+    assert sorted(p.numpy().tolist()) == list(range(30))
