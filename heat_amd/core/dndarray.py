@@ -205,8 +205,9 @@ class DNDarray:
         return self.__split
 
     @property
-    def stride(self) -> Tuple[int, ...]:
-        return tuple(self.__array.stride())
+    def stride(self):
+        """The local tensor's ``stride`` method (torch-like usage: ``x.stride()``)."""
+        return self.__array.stride
 
     @property
     def strides(self) -> Tuple[int, ...]:

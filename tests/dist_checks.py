@@ -923,3 +923,75 @@ def check_random_counter_semantics():
     assert ri.min() >= -5 and ri.max() < 9
     p = ht.random.permutation(30)
     assert sorted(p.numpy().tolist()) == list(range(30))
+
+
+def check_dndarray_properties():
+    """DNDarray attributes and helpers (reference core/tests/test_dndarray.py)."""
+    comm = ht.MPI_WORLD
+    p, me = comm.size, comm.rank
+    # halos along a column split
+    data_np = np.arange(1, 3 * 2 * p + 1, dtype=np.float32).reshape(2, 3 * p)
+    x = ht.array(data_np, split=1)
+    x.get_halo(2)
+    counts, displs = x.counts_displs()
+    if p > 1:
+        if me < p - 1:
+            nxt = data_np[:, displs[me + 1]: displs[me + 1] + 2]
+            assert np.array_equal(x.halo_next.cpu().numpy(), nxt)
+        else:
+            assert x.halo_next is None
+        if me > 0:
+            prv = data_np[:, displs[me] - 2: displs[me]]
+            assert np.array_equal(x.halo_prev.cpu().numpy(), prv)
+        else:
+            assert x.halo_prev is None
+        extra = (2 if me > 0 else 0) + (2 if me < p - 1 else 0)
+        assert tuple(x.array_with_halos.shape) == (2, counts[me] + extra)
+    for bad, exc in (("wrong", TypeError), (-99, ValueError)):
+        try:
+            x.get_halo(bad)
+            raise AssertionError("expected {}".format(exc))
+        except exc:
+            pass
+    # metadata
+    y = ht.zeros((7, 4, 3), split=1, dtype=ht.float64)
+    assert y.gnumel == 84 and y.size == 84 and y.ndim == 3 and len(y) == 7
+    assert y.nbytes == y.gnbytes == 84 * 8
+    assert y.lnbytes == y.larray.numel() * 8
+    assert y.lnumel == y.larray.numel()
+    c, d = y.counts_displs()
+    assert sum(c) == 4 and list(d) == [sum(c[:r]) for r in range(p)]
+    assert tuple(y.lshape_map[:, 1].tolist()) == tuple(c)
+    assert y.is_balanced() and y.balanced
+    assert y.is_distributed() == (p > 1)
+    assert y.stride() == y.larray.stride() and len(y.strides) == 3
+    # item / casts / tolist / numpy
+    z = ht.array([[3.5]], split=0)
+    assert z.item() == 3.5 and float(z) == 3.5 and int(z) == 3 and bool(z) and complex(z) == 3.5 + 0j
+    assert ht.array([[1, 2], [3, 4]], split=0).tolist() == [[1, 2], [3, 4]]
+    a = ht.arange(10, split=0)
+    assert a.astype(ht.float64).dtype == ht.float64 and a.astype(ht.float64, copy=False).dtype == ht.float64
+    # lloc: local indexing
+    loc = a.lloc[0:1]
+    assert tuple(loc.shape) == (min(1, a.lshape[0]),)
+    # fill_diagonal on a split matrix
+    m = ht.zeros((5, 5), split=0)
+    m.fill_diagonal(2)
+    assert_array_equal(m, np.eye(5, dtype=np.float32) * 2)
+    # unbalanced -> balance, redistribute, lshape_map
+    b = ht.arange(3 * p + 2, split=0)[2:]
+    b.balance_()
+    assert b.is_balanced()
+    assert_array_equal(b, np.arange(2, 3 * p + 2))
+    if p > 1:
+        target = torch.tensor([[3 * p - 2 * (p - 1)] + [2] * (p - 1)]).T if False else None
+        tm = b.lshape_map.clone()
+        tm[:, 0] = torch.tensor([3 * p - (p - 1)] + [1] * (p - 1))
+        b.redistribute_(lshape_map=b.lshape_map, target_map=tm)
+        assert b.lshape[0] == int(tm[me, 0])
+        assert_array_equal(b, np.arange(2, 3 * p + 2), check_split_chunks=False)
+    # bitwise dunders
+    i1 = ht.array([0b1100, 0b1010], split=0)
+    i2 = ht.array([0b1010, 0b0110], split=0)
+    assert (i1 & i2).tolist() == [8, 2] and (i1 | i2).tolist() == [14, 14] and (i1 ^ i2).tolist() == [6, 12]
+    assert (~i1).tolist() == [~12, ~10] and (i1 << 1).tolist() == [24, 20] and (i1 >> 2).tolist() == [3, 2]
