@@ -50,3 +50,42 @@ def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None
         msg = "\n".join("----- rank {} -----\n{}".format(r, outs[r][-6000:]) for r in failed)
         raise AssertionError("distributed test {} failed on ranks {}\n{}".format(target, failed, msg))
     return outs
+
+
+def run_distributed_batch(module: str, names, nprocs: int, timeout: int = 1200):
+    """Run the check functions ``names`` of ``module`` in one job of ``nprocs`` ranks; returns
+    {name: (ok, error)} (checks missing from the report - a job that died - count as failed)."""
+    import json
+    import tempfile
+
+    port = _free_port()
+    fd, out_path = tempfile.mkstemp(suffix=".jsonl")
+    os.close(fd)
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "WORLD_SIZE": str(nprocs), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(nprocs),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HEAT_COMM_BACKEND": "gloo",
+                    "HEAT_COMM_TIMEOUT": "120", "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "",
+                    "OMP_NUM_THREADS": "1", "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        procs.append(subprocess.Popen([sys.executable, "-m", "tests._dist_batch_runner", out_path, module] + list(names),
+                                      cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            out = b"timeout"
+        logs.append(out.decode(errors="replace"))
+    res = {}
+    with open(out_path) as f:
+        for line in f:
+            rec = json.loads(line)
+            res[rec["name"]] = (rec["ok"], rec["error"])
+    os.unlink(out_path)
+    tail = "\n".join(l[-2000:] for l in logs)
+    for n in names:
+        res.setdefault(n, (False, "job ended before this check ran:\n" + tail))
+    return res
