@@ -995,3 +995,30 @@ def check_dndarray_properties():
     i2 = ht.array([0b1010, 0b0110], split=0)
     assert (i1 & i2).tolist() == [8, 2] and (i1 | i2).tolist() == [14, 14] and (i1 ^ i2).tolist() == [6, 12]
     assert (~i1).tolist() == [~12, ~10] and (i1 << 1).tolist() == [24, 20] and (i1 >> 2).tolist() == [3, 2]
+
+
+def check_linalg_more():
+    """Norms with every ord, vecdot, projection, transpose axes, trace offsets, batched matmul."""
+    rng = _rng(31)
+    a = rng.standard_normal((8, 6))
+    b3 = rng.standard_normal((3, 8, 6))
+    u, w = rng.standard_normal(6), rng.standard_normal(6)
+    for s in (None, 0, 1):
+        A = ht.array(a, split=s)
+        for o in (1, -1, 2, -2, np.inf, -np.inf, "fro", "nuc"):
+            got = float(ht.linalg.matrix_norm(A, ord=o).item())
+            assert abs(got - np.linalg.norm(a, ord=o)) < 1e-8 * max(1.0, abs(got)), (o, got)
+        for o in (None, 1, 3, np.inf, -np.inf, 0):
+            for ax in (0, 1):
+                assert_array_equal(ht.linalg.vector_norm(A, axis=ax, ord=o), np.linalg.norm(a, axis=ax, ord=o),
+                                   rtol=1e-7, check_split_chunks=False)
+        assert_array_equal(ht.transpose(A), a.T, check_split_chunks=False)
+        assert abs(ht.trace(A, offset=2) - np.trace(a, offset=2)) < 1e-9
+        assert_array_equal(ht.linalg.vecdot(A, A, axis=1), (a * a).sum(1), rtol=1e-9, check_split_chunks=False)
+    for s in (None, 0, 2):
+        B3 = ht.array(b3, split=s)
+        assert_array_equal(ht.transpose(B3, (2, 0, 1)), b3.transpose(2, 0, 1), check_split_chunks=False)
+    U, W = ht.array(u, split=0), ht.array(w, split=0)
+    pr = ht.linalg.projection(U, W)
+    assert_array_equal(pr, (u @ w) / (w @ w) * w, rtol=1e-9)
+    assert_array_equal(ht.linalg.vecdot(U, W), np.array(u @ w), rtol=1e-9)

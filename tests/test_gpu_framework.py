@@ -46,3 +46,42 @@ def test_profiling_counts_native_kernels(gpu):
     finally:
         profiling.disable()
     assert c["kmeans_assign"]["calls"] >= 3 and c["kmeans_assign"]["ms"] > 0
+
+
+def test_data_parallel_on_gpu(gpu):
+    """DataParallel + DataParallelOptimizer with a CUDA model (bucketed gradient hooks on the
+    device); one rank: the step equals plain SGD."""
+    import torch
+    import heat_amd as ht
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4)).to(dev)
+    opt = ht.optim.DataParallelOptimizer(torch.optim.SGD(net.parameters(), lr=0.1), blocking=True)
+    dp = ht.nn.DataParallel(net, ht.MPI_WORLD, opt, blocking_parameter_updates=True)
+    ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4)).to(dev)
+    ref.load_state_dict(net.state_dict())
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    x = torch.randn(64, 16, device=dev)
+    y = torch.randint(0, 4, (64,), device=dev)
+    for _ in range(3):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(dp(x), y).backward()
+        opt.step()
+        ref_opt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(x), y).backward()
+        ref_opt.step()
+    for p, q in zip(net.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, atol=1e-6)
+
+
+def test_mnist_example_on_gpu(gpu):
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, os.path.join(root, "examples", "nn", "mnist.py"), "--epochs", "2",
+                          "--samples", "2048"], capture_output=True, text=True, timeout=600, cwd=root)
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert "epoch 1" in res.stdout
