@@ -237,13 +237,19 @@ _CDIST_EXACT = {"euclidean": 4, "sqeuclidean": 5, "gaussian": 6, "manhattan": 3}
 
 class PackedRows(NamedTuple):
     """Rows split into fp16 hi/lo planes (power-of-two row scale) + {|x|^2, 1/scale} for the
-    fp16x3 cdist kernel (``csrc/cdist_f16x3.hip``). Row slices of both tensors stay valid."""
-    planes: torch.Tensor  # [n, 2 * fpad] float16
-    aux: torch.Tensor     # [n, 2] float32
+    fp16x3 cdist kernels (``csrc/cdist_f16x3.hip``), in the fragment-blocked layout: rows padded
+    to a multiple of 128, each 32-row block stored as the 1 KB MFMA operand fragments of its
+    16-feature k-steps. ``rows(lo, hi)`` views a row range starting at a multiple of 128."""
+    planes: torch.Tensor  # [padded_rows, 2 * fpad] float16 (blocked, not row-major)
+    aux: torch.Tensor     # [padded_rows, 2] float32
     f: int
+    n: int                # live rows
 
     def rows(self, lo: int, hi: int) -> "PackedRows":
-        return PackedRows(self.planes[lo:hi], self.aux[lo:hi], self.f)
+        hi = min(hi, self.n)
+        if lo % 128:
+            raise ValueError("packed row slices must start at a multiple of 128")
+        return PackedRows(self.planes[lo:], self.aux[lo:], self.f, max(0, hi - lo))
 
 
 def cdist_pack(X: torch.Tensor) -> PackedRows:
@@ -251,17 +257,22 @@ def cdist_pack(X: torch.Tensor) -> PackedRows:
     L = lib()
     n, f = X.shape
     fpad = L.ha_cdist_h3_fpad(f)
+    rows = L.ha_cdist_h3_rows(n)
     Xc = X if X.stride(-1) == 1 else X.contiguous()
-    planes = torch.empty((n, 2 * fpad), dtype=torch.float16, device=X.device)
-    aux = torch.empty((n, 2), dtype=torch.float32, device=X.device)
+    planes = torch.empty((rows, 2 * fpad), dtype=torch.float16, device=X.device)
+    aux = torch.empty((rows, 2), dtype=torch.float32, device=X.device)
     check(L.ha_cdist_h3_pack(_ptr(Xc), n, f, Xc.stride(0), _ptr(planes), _ptr(aux),
                              ctypes.c_void_p(stream_ptr(X.device))), "ha_cdist_h3_pack")
-    return PackedRows(planes, aux, f)
+    return PackedRows(planes, aux, f, n)
 
 
 def _cdist_h3(px: PackedRows, py: PackedRows, mode: int, scale: float, C: torch.Tensor) -> None:
-    m, n = px.planes.shape[0], py.planes.shape[0]
+    m, n = px.n, py.n
+    if px.f != py.f:
+        raise ValueError("packed operands have different feature counts")
     if m and n:
+        if C.stride(1) != 1 or C.shape[0] < m or C.shape[1] < n:
+            raise ValueError("cdist output must be row-contiguous and at least {} x {}".format(m, n))
         check(lib().ha_cdist_h3(_ptr(px.planes), _ptr(px.aux), m, _ptr(py.planes), _ptr(py.aux), n, px.f, _ptr(C),
                                 C.stride(0), mode, ctypes.c_float(scale), ctypes.c_void_p(stream_ptr(C.device))),
               "ha_cdist_h3")

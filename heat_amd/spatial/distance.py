@@ -163,6 +163,7 @@ def cdist_stream(X: DNDarray, Y: Optional[DNDarray], consume: Callable[[torch.Te
         Y = X
     if X.split not in (None, 0) or Y.split not in (None, 0):
         raise NotImplementedError("Splittings other than 0 or None currently not supported.")
+    tile = max(128, tile // 128 * 128)  # packed operands are sliced at multiples of 128 rows
     x = X.larray if X.larray.dtype == torch.float32 else X.larray.float()
     y = Y.larray if Y.larray.dtype == torch.float32 else Y.larray.float()
     comm = X.comm

@@ -132,7 +132,8 @@ def test_cdist(metric, m, n, f, exact):
 
 @pytest.mark.parametrize("precision", ["f16x3", "fp32"])
 @pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian"])
-@pytest.mark.parametrize("m,n,f", [(100, 50, 3), (1000, 777, 18), (257, 300, 128), (300, 129, 200), (40, 2000, 1000)])
+@pytest.mark.parametrize("m,n,f", [(100, 50, 3), (1000, 777, 18), (513, 640, 64), (130, 1100, 96), (257, 300, 128),
+                                   (300, 129, 200), (40, 2000, 1000)])
 @pytest.mark.parametrize("scale", [1.0, 1e-3, 1e3])
 def test_cdist_expansion(metric, m, n, f, precision, scale):
     """Quadratic-expansion kernels: squared distances within fp32-GEMM rounding of the exact ones."""
@@ -167,8 +168,27 @@ def test_cdist_stream_matches_full(gpu):
     def consume(d, i, j):
         got[i: i + d.shape[0], j: j + d.shape[1]] = d
 
-    ht.spatial.cdist_stream(x, x, consume, tile=1024)
-    assert torch.allclose(got, full, atol=1e-5)
+    for tile in (1024, 1000):  # 1000 is rounded down to a multiple of 128 rows
+        got.zero_()
+        ht.spatial.cdist_stream(x, x, consume, tile=tile)
+        assert torch.allclose(got, full, atol=1e-5)
+
+
+def test_cdist_packed_row_slices(gpu):
+    """Packed operands sliced at multiples of 128 rows == packing the slice itself."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    X = torch.randn(1000, 128, generator=g).to(dev)
+    Y = torch.randn(700, 128, generator=g).to(dev)
+    px, py = ops.cdist_pack(X), ops.cdist_pack(Y)
+    assert px.planes.shape[0] == 1024 and px.n == 1000
+    full = ops.cdist(X, Y, packed_x=px, packed_y=py)
+    part = ops.cdist(X[256:900], Y[384:], packed_x=px.rows(256, 900), packed_y=py.rows(384, 700))
+    assert torch.allclose(part, full[256:900, 384:], atol=1e-6)
+    with pytest.raises(ValueError):
+        px.rows(100, 200)
 
 
 def test_threefry_bit_exact():
