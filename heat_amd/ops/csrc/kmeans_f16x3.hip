@@ -131,326 +131,15 @@ __global__ __launch_bounds__(256) void h3_pack_centroids(const float* __restrict
   }
 }
 
-// EPI = false is a timing-only ablation (tools/microbench): MFMAs without the argmin epilogue.
-template <int FPAD, int NPB_ = 2, bool EPI = true>
-__global__ __launch_bounds__(256, 2) void h3_assign(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
-                                                   int64_t n, const _Float16* __restrict__ image,
-                                                   const float* __restrict__ u, const float* __restrict__ meta,
-                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
-  using K = H3Cfg<FPAD, NPB_>;
-  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
-  constexpr int BUF_B = CHUNK_H * 2 + CB * 4;      // bytes per buffer: image + u
-  constexpr int STG = CHUNK_H * 2 / 16 / 256;      // 16-byte pieces staged per thread per chunk
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
-
-  halfx8 bhi[NPB][KS], blo[NPB][KS];
-  float sx[NPB], nsx[NPB], xsq[NPB];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    int64_t row = pbase + pb * 32 + j;
-    row = row < n ? row : n - 1;
-    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
-    float q = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
-      blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
-        q = fmaf(xv, xv, q);
-      }
-    }
-    sx[pb] = sxv[row];
-    nsx[pb] = -sx[pb];
-    xsq[pb] = q;
-  }
-  float best[NPB];
-  int btile[NPB];
-  float sv[NPB][16];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    best[pb] = -__builtin_huge_valf();
-    btile[pb] = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
-  }
-
-  {
-    const floatx4* src = reinterpret_cast<const floatx4*>(image);
-    floatx4* dst = reinterpret_cast<floatx4*>(smem);
-#pragma unroll
-    for (int i = 0; i < STG; ++i) dst[tid + 256 * i] = src[tid + 256 * i];
-    if (tid < CB / 4) reinterpret_cast<floatx4*>(smem + CHUNK_H * 2)[tid] = reinterpret_cast<const floatx4*>(u)[tid];
-  }
-  __syncthreads();
-
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const bool more = ch + 1 < nchunks;
-    floatx4 stg[STG];
-    floatx4 stn = {0.f, 0.f, 0.f, 0.f};
-    if (more) {
-      const floatx4* src = reinterpret_cast<const floatx4*>(image + (int64_t)(ch + 1) * CHUNK_H);
-#pragma unroll
-      for (int i = 0; i < STG; ++i) stg[i] = src[tid + 256 * i];
-      if (tid < CB / 4) stn = reinterpret_cast<const floatx4*>(u + (ch + 1) * CB)[tid];
-    }
-    const unsigned char* buf = smem + (ch & 1) * BUF_B;
-    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
-    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
-#pragma unroll 1
-    for (int cb = 0; cb < CB / 32; ++cb) {
-      floatx16 acc[NPB];
-#pragma unroll
-      for (int pb = 0; pb < NPB; ++pb) acc[pb] = (floatx16)(0.f);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
-        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
-        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
-#pragma unroll
-        for (int pb = 0; pb < NPB; ++pb) {
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[pb], 0, 0, 0);
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[pb], 0, 0, 0);
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[pb], 0, 0, 0);
-        }
-      }
-      // accumulator reg r holds centroid row (r&3) + 8(r>>2) + 4h of this 32-block
-      if (!EPI) {
-#pragma unroll
-        for (int pb = 0; pb < NPB; ++pb) best[pb] = fmaxf(best[pb], acc[pb][0] + acc[pb][15]);
-        continue;
-      }
-      floatx4 cn[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) cn[g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
-      const int tile = ch * (CB / 32) + cb;
-#pragma unroll
-      for (int pb = 0; pb < NPB; ++pb) {
-        // w = D - s_x u_c (= -v) on packed FMAs, maximised; the tile's 16 values are kept when
-        // its max improves, so the index search runs once per point at the end instead of in a
-        // (nearly always taken) per-tile branch.
-        const floatx2 sx2 = {nsx[pb], nsx[pb]};
-        float w[16];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
-          const floatx2 a2 = {acc[pb][2 * q], acc[pb][2 * q + 1]};
-          const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
-          w[2 * q] = r2[0];
-          w[2 * q + 1] = r2[1];
-        }
-        float m = w[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
-        const bool imp = m > best[pb];
-        best[pb] = imp ? m : best[pb];
-        btile[pb] = imp ? tile : btile[pb];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
-      }
-    }
-    if (more) {
-      unsigned char* nb = smem + ((ch + 1) & 1) * BUF_B;
-      floatx4* dst = reinterpret_cast<floatx4*>(nb);
-#pragma unroll
-      for (int i = 0; i < STG; ++i) dst[tid + 256 * i] = stg[i];
-      if (tid < CB / 4) reinterpret_cast<floatx4*>(nb + CHUNK_H * 2)[tid] = stn;
-    }
-    __syncthreads();
-  }
-
-  const float sC = meta[0];
-  int bidx[NPB];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    int bi = 15;
-#pragma unroll
-    for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
-    bidx[pb] = btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
-  }
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    const float ob = __shfl_xor(best[pb], 32, 64);
-    const int oi = __shfl_xor(bidx[pb], 32, 64);
-    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
-    if (ob > best[pb] || (ob == best[pb] && oi < bidx[pb])) {
-      best[pb] = ob;
-      bidx[pb] = oi;
-    }
-    const int64_t row = pbase + pb * 32 + j;
-    if (h == 0 && row < n) {
-      labels[row] = bidx[pb];
-      if (mind) {
-        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
-        const float isx = 1.f / sx[pb];
-        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
-      }
-    }
-  }
-}
-
-// Variant: the centroid chunk is staged by LDS-DMA (global_load_lds_dwordx4; the packed image is
-// lane-linear, 1 KB per wave instruction) into ONE buffer, which frees the 32 staging VGPRs and half
-// the LDS so 3 workgroups share a CU and hide each other's staging.
-template <int FPAD, int NPB_ = 2, bool EPI = true, int MINB = 3>
-__global__ __launch_bounds__(256, MINB) void h3_assign_g(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
-                                                   int64_t n, const _Float16* __restrict__ image,
-                                                   const float* __restrict__ u, const float* __restrict__ meta,
-                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
-  using K = H3Cfg<FPAD, NPB_>;
-  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
-
-  halfx8 bhi[NPB][KS], blo[NPB][KS];
-  float sx[NPB], nsx[NPB], xsq[NPB];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    int64_t row = pbase + pb * 32 + j;
-    row = row < n ? row : n - 1;
-    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
-    float q = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
-      blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
-        q = fmaf(xv, xv, q);
-      }
-    }
-    sx[pb] = sxv[row];
-    nsx[pb] = -sx[pb];
-    xsq[pb] = q;
-  }
-  float best[NPB];
-  int btile[NPB];
-  float sv[NPB][16];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    best[pb] = -__builtin_huge_valf();
-    btile[pb] = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
-  }
-
-  constexpr int PIECES = CHUNK_H * 2 / 1024;  // 1 KB (64 lanes x 16 B) per DMA instruction
-  for (int ch = 0; ch < nchunks; ++ch) {
-    {
-      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
-#pragma unroll
-      for (int pc = wave; pc < PIECES; pc += 4)
-        __builtin_amdgcn_global_load_lds(src + pc * 1024,
-                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
-      if (wave == 0 && lane < CB / 4)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H * 2), 16, 0, 0);
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-    }
-    const unsigned char* buf = smem;
-    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
-    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
-#pragma unroll 1
-    for (int cb = 0; cb < CB / 32; ++cb) {
-      floatx16 acc[NPB];
-#pragma unroll
-      for (int pb = 0; pb < NPB; ++pb) acc[pb] = (floatx16)(0.f);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
-        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
-        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
-#pragma unroll
-        for (int pb = 0; pb < NPB; ++pb) {
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[pb], 0, 0, 0);
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[pb], 0, 0, 0);
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[pb], 0, 0, 0);
-        }
-      }
-      // accumulator reg r holds centroid row (r&3) + 8(r>>2) + 4h of this 32-block
-      if (!EPI) {
-#pragma unroll
-        for (int pb = 0; pb < NPB; ++pb) best[pb] = fmaxf(best[pb], acc[pb][0] + acc[pb][15]);
-        continue;
-      }
-      floatx4 cn[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) cn[g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
-      const int tile = ch * (CB / 32) + cb;
-#pragma unroll
-      for (int pb = 0; pb < NPB; ++pb) {
-        // w = D - s_x u_c (= -v) on packed FMAs, maximised; the tile's 16 values are kept when
-        // its max improves, so the index search runs once per point at the end instead of in a
-        // (nearly always taken) per-tile branch.
-        const floatx2 sx2 = {nsx[pb], nsx[pb]};
-        float w[16];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
-          const floatx2 a2 = {acc[pb][2 * q], acc[pb][2 * q + 1]};
-          const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
-          w[2 * q] = r2[0];
-          w[2 * q + 1] = r2[1];
-        }
-        float m = w[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
-        const bool imp = m > best[pb];
-        best[pb] = imp ? m : best[pb];
-        btile[pb] = imp ? tile : btile[pb];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
-      }
-    }
-    __syncthreads();  // every wave is done with the buffer before the next chunk's DMA
-  }
-
-  const float sC = meta[0];
-  int bidx[NPB];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    int bi = 15;
-#pragma unroll
-    for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
-    bidx[pb] = btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
-  }
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    const float ob = __shfl_xor(best[pb], 32, 64);
-    const int oi = __shfl_xor(bidx[pb], 32, 64);
-    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
-    if (ob > best[pb] || (ob == best[pb] && oi < bidx[pb])) {
-      best[pb] = ob;
-      bidx[pb] = oi;
-    }
-    const int64_t row = pbase + pb * 32 + j;
-    if (h == 0 && row < n) {
-      labels[row] = bidx[pb];
-      if (mind) {
-        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
-        const float isx = 1.f / sx[pb];
-        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
-      }
-    }
-  }
-}
-
-// Software-pipelined variant of h3_assign_g: the argmax epilogue of tile t-1 (VALU) is issued in the
-// same basic block as the MFMAs of tile t (ping-pong accumulators), and sched_group_barrier pins
-// an MFMA / VALU interleave, so the epilogue fills the MFMA issue gaps instead of stalling the
-// matrix pipe once per tile.
+// Assignment kernel. A wave keeps NPB 32-point blocks (hi/lo fragments) in registers; the packed
+// centroid image is staged chunk by chunk into LDS by LDS-DMA (global_load_lds_dwordx4: the image is
+// stored in fragment order, so the copy is lane-linear). Software-pipelined: the argmax epilogue
+// of tile t-1 (VALU) is issued in the same basic block as the MFMAs of tile t (ping-pong
+// accumulators), and sched_group_barrier pins an MFMA / VALU interleave, so the epilogue fills
+// the MFMA issue gaps instead of stalling the matrix pipe once per tile.
+// Measured alternatives (tools/microbench/h3_bench.hip, n=12.5M, k=1024, f=64): register-staged
+// double buffer 4.39 ms, unpipelined LDS-DMA 4.03 ms, this kernel 4.10 ms with 1 LDS buffer and
+// 4.10 ms with 2 (DMA of chunk c+1 under chunk c: no gain, the loop is not load-latency bound).
 template <int FPAD, int NPB_ = 2, bool EPI = true, int MINB = 3>
 __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                    int64_t n, const _Float16* __restrict__ image,
@@ -650,16 +339,18 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
   float* meta = u + kpad;
   const _Float16* p = (const _Float16*)planes;
+  // FPAD 128 keeps one 32-point block per wave (two spill: 4.62 -> 4.20 ms at f=100, k=1024, n=6.25M)
 #define HA_H3(FP)                                                                                           \
   case FP: {                                                                                                \
-    using KC = H3Cfg<FP>;                                                                                   \
+    constexpr int NPB = FP >= 128 ? 1 : 2, MINB = FP >= 128 ? 3 : 2;                                        \
+    using KC = H3Cfg<FP, NPB>;                                                                              \
     hipMemsetAsync(meta, 0, 2 * sizeof(float), s);                                                          \
     hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
     const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                         \
-    hipLaunchKernelGGL((h3_assign_p<FP, 2, true, 2>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u,  \
+    hipLaunchKernelGGL((h3_assign_p<FP, NPB, true, MINB>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, \
                        meta, kpad / KC::CB, labels, mind);                                                 \
     break;                                                                                                  \
   }
