@@ -39,6 +39,31 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         # "exact": bit-exact fp32 (f32-input MFMA) assignment
         self.precision = "fast"
         self._pack_cache = None
+        # certified one-term assignment (ops.kmeans_assign(certified=True)) while it pays: every
+        # certified call posts its re-check count to the host without a sync; once more than
+        # CERT_MAX_RECHECK of the points needed the 3-term re-run, the full kernel takes over
+        # until the points change
+        self._certify = True
+        self._cert_probe = None
+
+    CERT_MAX_RECHECK = 0.25
+
+    def _assign_labels(self, X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+        """int32 nearest-centroid labels of the local points (native fused kernels)."""
+        packed = self._packed(X) if X.dtype == torch.float32 else None
+        probe = self._cert_probe
+        if probe is not None and probe[1].query():
+            self._certify = probe[0].item() <= self.CERT_MAX_RECHECK * probe[2]
+            self._cert_probe = probe = None
+        certified = packed is not None and self._certify
+        labels, _ = ops.kmeans_assign(X, C, want_mind=False, packed=packed, certified=certified)
+        if certified and probe is None and X.shape[0] > 0:
+            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            host.copy_(ops.kmeans_assign.last_rechecked.reshape(1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._cert_probe = (host, ev, X.shape[0])
+        return labels
 
     def _packed(self, X: torch.Tensor):
         """fp16x3 planes of the local points, cached while X is unchanged (None: exact path)."""
@@ -47,6 +72,7 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         key = ops.kernels._points_key(X)
         if self._pack_cache is None or self._pack_cache.key != key:
             self._pack_cache = None
+            self._certify, self._cert_probe = True, None
             self._pack_cache = ops.kmeans_pack_points(X)
         return self._pack_cache
 
@@ -138,8 +164,7 @@ class _KCluster(ClusteringMixin, BaseEstimator):
     def _assign_to_cluster(self, x: DNDarray) -> DNDarray:
         """(n, 1) int64 labels of the nearest centroid (split like ``x``)."""
         X = x.larray
-        labels, _ = ops.kmeans_assign(X, self._cluster_centers.larray.to(X.device), want_mind=False,
-                                      packed=self._packed(X) if X.dtype == torch.float32 else None)
+        labels = self._assign_labels(X, self._cluster_centers.larray.to(X.device))
         lab = labels.to(torch.int64).reshape(-1, 1)
         return DNDarray(lab, (x.gshape[0], 1), ht.int64, x.split, x.device, x.comm, x.balanced)
 

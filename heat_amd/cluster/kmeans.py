@@ -38,8 +38,7 @@ class KMeans(_KCluster):
     def _centroid_step(self, X: torch.Tensor, C: torch.Tensor, comm, distributed: bool):
         """One Lloyd step on the local block: returns (new centroids, int32 labels)."""
         k = C.shape[0]
-        labels, _ = ops.kmeans_assign(X, C, want_mind=False,
-                                      packed=self._packed(X) if X.dtype == torch.float32 else None)
+        labels = self._assign_labels(X, C)
         sums, counts = ops.kmeans_update(X, labels, k)
         packed = torch.cat([sums.reshape(-1).double(), counts.double()])
         if distributed:

@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void h3_pack_centroids(const float* __restrict
         acc = fmaf(x, x, acc);
       }
       u[c] = 0.5f * s * acc;
+      atomicMax(reinterpret_cast<unsigned int*>(meta + 2), __float_as_uint(0.5f * s * acc));  // u_max (>= 0)
     } else {
       u[c] = __builtin_huge_valf();
     }
@@ -140,11 +141,17 @@ __global__ __launch_bounds__(256) void h3_pack_centroids(const float* __restrict
 // Measured alternatives (tools/microbench/h3_bench.hip, n=12.5M, k=1024, f=64): register-staged
 // double buffer 4.39 ms, unpipelined LDS-DMA 4.03 ms, this kernel 4.10 ms with 1 LDS buffer and
 // 4.10 ms with 2 (DMA of chunk c+1 under chunk c: no gain, the loop is not load-latency bound).
-template <int FPAD, int NPB_ = 2, bool EPI = true, int MINB = 3>
+//
+// IND (the re-check pass of the certified filter below): the points are rows[0 .. *rcount) of the
+// planes, and a grid of a few workgroups per CU strides over them (the count is only known on the
+// device).
+template <int FPAD, int NPB_ = 2, bool EPI = true, int MINB = 3, bool IND = false>
 __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                    int64_t n, const _Float16* __restrict__ image,
                                                    const float* __restrict__ u, const float* __restrict__ meta,
-                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind) {
+                                                   int nchunks, int* __restrict__ labels, float* __restrict__ mind,
+                                                   const int* __restrict__ rows = nullptr,
+                                                   const int* __restrict__ rcount = nullptr) {
   using K = H3Cfg<FPAD, NPB_>;
   constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -152,14 +159,19 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+  const int64_t cnt = IND ? (int64_t)*rcount : n;
+  for (int64_t blk = blockIdx.x; blk * K::PTS_PER_WG < cnt; blk += IND ? gridDim.x : cnt) {
+  const int64_t pbase = blk * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
 
   halfx8 bhi[NPB][KS], blo[NPB][KS];
   float sx[NPB], nsx[NPB], xsq[NPB];
+  int64_t prow[NPB];
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
-    int64_t row = pbase + pb * 32 + j;
-    row = row < n ? row : n - 1;
+    const int64_t idx = pbase + pb * 32 + j;
+    const int64_t ci = idx < cnt ? idx : cnt - 1;
+    const int64_t row = IND ? (int64_t)rows[ci] : ci;
+    prow[pb] = idx < cnt ? row : -1;
     const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
     float q = 0.f;
 #pragma unroll
@@ -280,14 +292,187 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
       best[pb] = ob;
       bidx[pb] = oi;
     }
-    const int64_t row = pbase + pb * 32 + j;
-    if (h == 0 && row < n) {
+    const int64_t row = prow[pb];
+    if (h == 0 && row >= 0) {
       labels[row] = bidx[pb];
       if (mind) {
         // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
         const float isx = 1.f / sx[pb];
         mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
       }
+    }
+  }
+  }  // point blocks
+}
+
+// Certified one-term filter ("h1"). Scores use hi_c . hi_x only (ONE MFMA per k-step instead of
+// three), the kernel tracks each point's best AND runner-up score, and a point is assigned here
+// only if its best score beats the runner-up by more than twice a rigorous bound E on the
+// hi-only error; every other point is appended to `amb_rows` and re-run through the 3-term kernel
+// (IND mode of h3_assign_p). In the scaled space (|x_s|_inf, |c_s|_inf < 1), with a, b the fp16
+// rounding errors of x_s, c_s (|a_i| <= 2^-11 |x_s,i| or 2^-25 in fp16's subnormal range):
+//   |x_s.c_s - hi_x.hi_c| <= sum |x_i b_i| + |a_i c_i| + |a_i b_i| <= 2^-10 (1 + 2^-11) |x_s| |c_s| + f 2^-24
+// fp16 x fp16 products are exact in fp32; the fp32 accumulation, the fp32 |c|^2 and the epilogue
+// FMA add <= (f + 2) 2^-24 (|x_s||c_s| + s_x u_max); f <= 128 gives
+//   E = 1.01 * 2^-10 |x_s| c_max + 2^-16 (|x_s| c_max + s_x u_max) + 2^-16,
+// with |x_s| bounded from the hi plane (|x_s| <= |hi_x| (1 + 2^-10)) and c_max = max_c |c_s|.
+// The runner-up is exact without a per-value second-best update: per lane it is the larger of the
+// second-largest TILE maximum (one med3 per tile) and the second-largest value of the best tile
+// (whose 16 values are kept anyway to recover the index).
+template <int FPAD, int NPB_ = 2, int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+                                                 int64_t n, const _Float16* __restrict__ image,
+                                                 const float* __restrict__ u, const float* __restrict__ meta,
+                                                 int nchunks, int* __restrict__ labels, int* __restrict__ amb_rows,
+                                                 int* __restrict__ amb_count) {
+  using K = H3Cfg<FPAD, NPB_>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  constexpr float NINF = -__builtin_huge_valf();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+
+  halfx8 bhi[NPB][KS];
+  float nsx[NPB], hsq[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    int64_t row = pbase + pb * 32 + j;
+    row = row < n ? row : n - 1;
+    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) q = fmaf((float)bhi[pb][ks][i], (float)bhi[pb][ks][i], q);
+    }
+    nsx[pb] = -sxv[row];
+    hsq[pb] = q;
+  }
+  float best[NPB], sec[NPB];
+  int btile[NPB];
+  float sv[NPB][16];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    best[pb] = NINF;
+    sec[pb] = NINF;
+    btile[pb] = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[pb][r] = NINF;
+  }
+
+  // only the hi half of every (cb, ks) fragment pair is staged: piece 2q of the chunk -> LDS q
+  constexpr int PIECES = CHUNK_H * 2 / 1024 / 2;
+  floatx16 acc[2][NPB];
+  floatx4 cnr[2][4];
+  int ptile = -1;
+  auto epilogue = [&](const floatx16 (&ac)[NPB], const floatx4 (&cn)[4], int tile) {
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      const floatx2 sx2 = {nsx[pb], nsx[pb]};
+      float w[16];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+        const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
+        const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+        w[2 * q] = r2[0];
+        w[2 * q + 1] = r2[1];
+      }
+      float m = w[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
+      sec[pb] = __builtin_amdgcn_fmed3f(best[pb], sec[pb], m);
+      const bool imp = m > best[pb];
+      best[pb] = imp ? m : best[pb];
+      btile[pb] = imp ? tile : btile[pb];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
+    }
+  };
+  for (int ch = 0; ch < nchunks; ++ch) {
+    {
+      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+#pragma unroll
+      for (int pc = wave; pc < PIECES; pc += 4)
+        __builtin_amdgcn_global_load_lds(src + 2 * pc * 1024,
+                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+    const _Float16* img = reinterpret_cast<const _Float16*>(smem);
+    const float* ub = reinterpret_cast<const float*>(smem + CHUNK_H);
+#pragma unroll
+    for (int cb = 0; cb < CB / 32; ++cb) {
+      const int cur = cb & 1;
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) acc[cur][pb] = (floatx16)(0.f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const halfx8 ahi = *reinterpret_cast<const halfx8*>(img + ((cb * KS + ks) * 64 + lane) * 8);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb)
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cnr[cur][g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+      if (ptile >= 0) epilogue(acc[cur ^ 1], cnr[cur ^ 1], ptile);
+      ptile = ch * (CB / 32) + cb;
+#pragma unroll
+      for (int i = 0; i < KS * NPB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // then up to 12 VALU
+      }
+    }
+    __syncthreads();
+  }
+  if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], cnr[((CB / 32) - 1) & 1], ptile);
+
+  const float sC = meta[0], umax = meta[2];
+  const float cmax = sqrtf(2.f * sC * umax);
+  int* const cnt = amb_count;
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    float t1 = NINF, t2 = NINF;
+    int bi = 15;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      t2 = __builtin_amdgcn_fmed3f(t1, t2, sv[pb][r]);
+      t1 = fmaxf(t1, sv[pb][r]);
+    }
+#pragma unroll
+    for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
+    int bidx = btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+    float s2 = fmaxf(sec[pb], t2);
+    const float ob = __shfl_xor(best[pb], 32, 64);
+    const float os = __shfl_xor(s2, 32, 64);
+    const int oi = __shfl_xor(bidx, 32, 64);
+    const float xn = sqrtf(hsq[pb] + __shfl_xor(hsq[pb], 32, 64)) * (1.f + 0x1p-10f);
+    s2 = fmaxf(fminf(best[pb], ob), fmaxf(s2, os));
+    float b = best[pb];
+    if (ob > b || (ob == b && oi < bidx)) {
+      b = ob;
+      bidx = oi;
+    }
+    const float xc = xn * cmax;
+    const float E = 1.01f * 0x1p-10f * xc + 0x1p-16f * (xc - nsx[pb] * umax) + 0x1p-16f;
+    const int64_t row = pbase + pb * 32 + j;
+    const bool live = h == 0 && row < n;
+    const bool amb = live && !(b - s2 > 2.f * E);
+    if (live) labels[row] = bidx;
+    // wave-aggregated append of the uncertain points
+    const unsigned long long m = __ballot(amb);
+    if (m) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(cnt, (int)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (amb) amb_rows[base + (int)__popcll(m & ((1ull << lane) - 1ull))] = (int)row;
     }
   }
 }
@@ -324,7 +509,7 @@ HA_EXPORT int64_t ha_h3_workspace_bytes(int k, int f) {
   if (fpad < 0 || k <= 0) return -1;
   const int cb = fpad >= 128 ? 64 : 128;
   const int64_t kpad = (int64_t)(k + cb - 1) / cb * cb;
-  return kpad * fpad * 2 * 2 + kpad * 4 + 16;  // image + u + meta {s_C, max|c|}
+  return kpad * fpad * 2 * 2 + kpad * 4 + 16;  // image + u + meta {s_C, max|c|_inf, u_max, -}
 }
 
 HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f, const float* C, int k, int64_t ldc,
@@ -344,7 +529,7 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
   case FP: {                                                                                                \
     constexpr int NPB = FP >= 128 ? 1 : 2, MINB = FP >= 128 ? 3 : 2;                                        \
     using KC = H3Cfg<FP, NPB>;                                                                              \
-    hipMemsetAsync(meta, 0, 2 * sizeof(float), s);                                                          \
+    hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
     hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
@@ -363,5 +548,63 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
       return HA_UNSUPPORTED;
   }
 #undef HA_H3
+  return ha_launch_status();
+}
+
+// Certified one-term assignment: h1_filter over all points, then the 3-term kernel over the points
+// it could not certify. amb_rows: int32[n] scratch; amb_count: one int32, zeroed here, holds the
+// number of re-checked points afterwards. Labels are identical to ha_h3_assign's up to points
+// whose two best centroids are within the 3-term kernel's own rounding of each other.
+HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_t n, int f, const float* C, int k,
+                                     int64_t ldc, void* workspace, int* labels, int* amb_rows, int* amb_count,
+                                     void* stream) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || k <= 0) return HA_UNSUPPORTED;
+  if (n <= 0) return HA_OK;
+  if (n > INT32_MAX) return HA_BAD_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int cb = fpad >= 128 ? 64 : 128;
+  const int kpad = (k + cb - 1) / cb * cb;
+  _Float16* image = (_Float16*)workspace;
+  float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
+  float* meta = u + kpad;
+  const _Float16* p = (const _Float16*)planes;
+  hipMemsetAsync(amb_count, 0, sizeof(int), s);
+#define HA_H1(FP)                                                                                           \
+  case FP: {                                                                                                \
+    constexpr int NPB = FP >= 128 ? 1 : 2, MINB = FP >= 128 ? 3 : 2;                                        \
+    constexpr int NPB1 = FP >= 128 ? 1 : 2, MINB1 = 2;                                                      \
+    using KC = H3Cfg<FP, NPB>;                                                                              \
+    using K1 = H3Cfg<FP, NPB1>;                                                                             \
+    hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
+    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
+                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
+    const size_t lds1 = (size_t)K1::CHUNK_H + K1::CB * 4;                                                   \
+    const unsigned blocks1 = (unsigned)((n + K1::PTS_PER_WG - 1) / K1::PTS_PER_WG);                        \
+    hipLaunchKernelGGL((h1_filter<FP, NPB1, MINB1>), dim3(blocks1), dim3(256), lds1, s, p, sx, n, image, u, meta, \
+                       kpad / K1::CB, labels, amb_rows, amb_count);                                        \
+    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                \
+    const int64_t maxb = (n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG;                                        \
+    const unsigned blocks = (unsigned)(maxb < (int64_t)ncu * MINB ? maxb : (int64_t)ncu * MINB);            \
+    hipLaunchKernelGGL((h3_assign_p<FP, NPB, true, MINB, true>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, \
+                       meta, kpad / KC::CB, labels, (float*)nullptr, (const int*)amb_rows, (const int*)amb_count); \
+    break;                                                                                                  \
+  }
+  switch (fpad) {
+    HA_H1(16)
+    HA_H1(32)
+    HA_H1(64)
+    HA_H1(128)
+    default:
+      return HA_UNSUPPORTED;
+  }
+#undef HA_H1
   return ha_launch_status();
 }

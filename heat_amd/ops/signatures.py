@@ -16,6 +16,8 @@ SIGNATURES = {
     "ha_h3_workspace_bytes": (c_int64, [c_int, c_int]),
     "ha_h3_assign": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p,
                              c_void_p, c_void_p]),
+    "ha_h3_assign_certified": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "ha_cdist_h3_fpad": (c_int, [c_int]),
     "ha_cdist_h3_rows": (c_int64, [c_int64]),
     "ha_cdist_h3_pack": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p]),

@@ -58,6 +58,41 @@ def test_kmeans_assign_f16x3(n, k, f, scale):
     assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-4 * scale * scale * f)
 
 
+@pytest.mark.parametrize("n,k,f", [(1000, 7, 3), (5000, 300, 32), (70000, 1024, 64), (3333, 100, 100),
+                                   (777, 65, 128), (40000, 16, 18)])
+@pytest.mark.parametrize("data", ["normal", "near_centroids", "ties"])
+def test_kmeans_assign_certified(n, k, f, data):
+    """One-term filter + 3-term re-check: same minimality guarantee as the full fp16x3 kernel."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + 7 * k + f)
+    C = torch.randn(k, f, generator=g)
+    if data == "normal":
+        X = torch.randn(n, f, generator=g)
+    elif data == "near_centroids":   # tight clusters: mostly clear wins, a few far points
+        X = C[torch.randint(0, k, (n,), generator=g)] + 0.05 * torch.randn(n, f, generator=g)
+    else:                            # exact duplicates of centroids -> exact ties everywhere
+        C[1::2] = C[0::2][: C[1::2].shape[0]]
+        X = C[torch.randint(0, k, (n,), generator=g)].clone()
+    X, C = X.to(dev), C.to(dev)
+    packed = ops.kmeans_pack_points(X)
+    lab, mind = ops.kmeans_assign(X, C, want_mind=False, packed=packed, certified=True)
+    assert mind is None
+    nre = int(ops.kmeans_assign.last_rechecked.item())
+    assert 0 <= nre <= n
+    Xd, Cd = X.double(), C.double()
+    d = torch.cdist(Xd, Cd) ** 2
+    ref_min, _ = d.min(1)
+    chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+    tol = 2e-6 * ((Xd * Xd).sum(1) + (Cd * Cd).sum(1).max())
+    assert torch.all(chosen - ref_min <= tol), (chosen - ref_min - tol).max()
+    full, _ = ops.kmeans_assign(X, C, want_mind=True, packed=packed)
+    assert (lab == full).float().mean() > 0.999
+    if data == "near_centroids":
+        assert nre < n // 10, nre
+
+
 def test_kmeans_fast_matches_exact_fit(gpu):
     import heat_amd as ht
 
