@@ -15,7 +15,12 @@ def main():
     p.add_argument("--cols", type=int, default=4096)
     p.add_argument("--trials", type=int, default=3)
     p.add_argument("--ops", default="matmul,gram,qr_r,qr")
+    p.add_argument("--precision", default="highest", choices=["highest", "high"],
+                   help="torch float32 matmul precision: 'high' runs the fp16x3 split GEMM")
     a = p.parse_args()
+    import torch
+
+    torch.set_float32_matmul_precision(a.precision)
     dev = setup()
     m, n = a.rows_per_gpu * ht.MPI_WORLD.size, a.cols
     ht.random.seed(5)
@@ -24,17 +29,17 @@ def main():
     if "matmul" in ops:
         B = ht.random.randn(n, n, device=dev)
         t = timed(lambda: ht.matmul(A, B), a.trials)
-        report("linalg", {"op": "matmul A@B", "m": m, "n": n}, t, {"gflops": 2.0 * m * n * n / 1e9})
+        report("linalg", {"op": "matmul A@B", "m": m, "n": n, "precision": a.precision}, t, {"gflops": 2.0 * m * n * n / 1e9})
         del B
     if "gram" in ops:
         t = timed(lambda: ht.matmul(A.T, A), a.trials)
-        report("linalg", {"op": "gram A^T A", "m": m, "n": n}, t, {"gflops": 2.0 * m * n * n / 1e9})
+        report("linalg", {"op": "gram A^T A", "m": m, "n": n, "precision": a.precision}, t, {"gflops": 2.0 * m * n * n / 1e9})
     if "qr_r" in ops:
         t = timed(lambda: ht.linalg.qr(A, calc_q=False), a.trials)
-        report("linalg", {"op": "tsqr R", "m": m, "n": n}, t, {"gflops": (2.0 * m * n * n - 2.0 * n ** 3 / 3) / 1e9})
+        report("linalg", {"op": "tsqr R", "m": m, "n": n, "precision": a.precision}, t, {"gflops": (2.0 * m * n * n - 2.0 * n ** 3 / 3) / 1e9})
     if "qr" in ops:
         t = timed(lambda: ht.linalg.qr(A), a.trials)
-        report("linalg", {"op": "tsqr Q,R", "m": m, "n": n}, t, {"gflops": (4.0 * m * n * n - 4.0 * n ** 3 / 3) / 1e9})
+        report("linalg", {"op": "tsqr Q,R", "m": m, "n": n, "precision": a.precision}, t, {"gflops": (4.0 * m * n * n - 4.0 * n ** 3 / 3) / 1e9})
 
 
 if __name__ == "__main__":

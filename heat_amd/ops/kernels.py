@@ -13,7 +13,8 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep"]
+__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
+           "split_planes"]
 
 _NUM_CUS = {}
 
@@ -443,3 +444,107 @@ def lasso_epoch(XT: torch.Tensor, r: torch.Tensor, theta: torch.Tensor, colsq: t
             new = torch.where(rho < -lam, rho + lam, torch.where(rho > lam, rho - lam, torch.zeros_like(rho)))
         theta[j] = new
         r -= (new - old) * xj
+
+
+# ------------------------------------------------------------------------------- fp16x3 split GEMM
+def split_planes(X: torch.Tensor, axis: int, pattern: str, contract_dim: int):
+    """fp16x3 operand of :func:`gemm_f16x3` (see ``csrc/gemm_split.hip``).
+
+    ``X`` is a logical 2-D fp32 operand whose dimension ``1 - contract_dim`` carries the power-of-two
+    scales; the result is the logical operand with the contraction dimension tripled into the
+    segments named by ``pattern`` ("hhl": hi, hi, lo; "hlh": hi, lo, hi), laid out in X's own
+    memory order (row- or column-major) so the split streams coalesced. Returns (planes, int32
+    exponents, non-finite flag tensor)."""
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(X.device))
+    colmajor = X.stride(0) == 1 and X.stride(1) != 1
+    P = X.t() if colmajor else (X if X.stride(1) == 1 else X.contiguous())
+    if P.stride(1) != 1:
+        P = P.contiguous()
+    R, C = P.shape
+    # physical axis carrying the scales
+    scale_dim = 1 - contract_dim
+    phys_axis = (1 - scale_dim) if colmajor else scale_dim
+    ex = torch.empty(R if phys_axis == 0 else C, dtype=torch.int32, device=X.device)
+    flag = torch.zeros(1, dtype=torch.int32, device=X.device)
+    # physical contraction axis = the one that is not the scale axis
+    pc = 1 - phys_axis
+    if pc == 1:
+        out = torch.empty((R, 3 * C), dtype=torch.float16, device=X.device)
+        seg = [out[:, i * C:(i + 1) * C] for i in range(3)]
+    else:
+        out = torch.empty((3 * R, C), dtype=torch.float16, device=X.device)
+        seg = [out[i * R:(i + 1) * R] for i in range(3)]
+    h0, h1, lo = (seg[0], seg[1], seg[2]) if pattern == "hhl" else (seg[0], seg[2], seg[1])
+    rc = 2
+    if phys_axis == 0:   # per-row scales: absmax and split fused (one wave per row)
+        rc = L.ha_split3_rows(_ptr(P), R, C, P.stride(0), _ptr(h0), _ptr(h1), _ptr(lo), out.stride(0), _ptr(ex),
+                              _ptr(flag), st)
+    if rc == 2:
+        mx = torch.empty(ex.shape[0], dtype=torch.float32, device=X.device)
+        check(L.ha_split_absmax(_ptr(P), R, C, P.stride(0), phys_axis, _ptr(mx), _ptr(flag), st),
+              "ha_split_absmax")
+        rc = L.ha_split3(_ptr(P), R, C, P.stride(0), phys_axis, _ptr(mx), _ptr(h0), _ptr(h1), _ptr(None),
+                         _ptr(lo), out.stride(0), _ptr(ex), st)
+    check(rc, "ha_split3")
+    return (out.t() if colmajor else out), ex, flag
+
+
+def _is_gram(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """a is the transposed view of a row-major b (X^T X)."""
+    return (a.data_ptr() == b.data_ptr() and a.shape == (b.shape[1], b.shape[0]) and b.stride(1) == 1
+            and a.stride() == (b.stride(1), b.stride(0)))
+
+
+def _split_gram(X: torch.Tensor):
+    """Both operands of X^T X from one split: column scales of X, buffer W = [h; h; l; h]
+    (4 planes instead of 6, one absmax and one split pass instead of two each)."""
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(X.device))
+    R, C = X.shape
+    mx = torch.empty(C, dtype=torch.float32, device=X.device)
+    ex = torch.empty(C, dtype=torch.int32, device=X.device)
+    flag = torch.zeros(1, dtype=torch.int32, device=X.device)
+    check(L.ha_split_absmax(_ptr(X), R, C, X.stride(0), 1, _ptr(mx), _ptr(flag), st), "ha_split_absmax")
+    W = torch.empty((4 * R, C), dtype=torch.float16, device=X.device)
+    check(L.ha_split3(_ptr(X), R, C, X.stride(0), 1, _ptr(mx), _ptr(W[:R]), _ptr(W[R:2 * R]), _ptr(W[3 * R:]),
+                      _ptr(W[2 * R:3 * R]), C, _ptr(ex), st), "ha_split3")
+    return W[R:].t(), W[:3 * R], ex, flag
+
+
+def gemm_f16x3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 ``a @ b`` on the FP16 matrix cores: both operands split into fp16 hi/lo planes with
+    power-of-two row (a) / column (b) scales, ONE fp16-in/fp32-out library GEMM over the tripled
+    contraction (hi.hi + hi.lo + lo.hi), exact ldexp unscaling. Accuracy of an fp32 GEMM (errors
+    <= ~2^-21 |a||b| per product, fp32 accumulation), ~2.7x its speed on MI355X. Operands holding
+    inf/nan go to the fp32 GEMM (one host sync per call for that check). ``out``: a row-major
+    fp32 [M, N] tensor (e.g. a row block of a larger result) the GEMM writes directly."""
+    def fallback():
+        if out is None:
+            return torch.matmul(a, b)
+        return torch.mm(a, b, out=out)
+
+    if not (a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32 \
+            or a.dim() != 2 or b.dim() != 2:
+        return fallback()
+    M, K = a.shape
+    N = b.shape[1]
+    if M == 0 or N == 0 or K == 0:
+        return fallback()
+    if out is not None and (out.shape != (M, N) or out.dtype != torch.float32 or out.stride(1) != 1):
+        raise ValueError("gemm_f16x3: out must be a row-major float32 [M, N] tensor")
+    if _is_gram(a, b):
+        A3, B3, ea, fa = _split_gram(b)
+        eb, fb = ea, fa
+    else:
+        A3, ea, fa = split_planes(a, 0, "hhl", 1)
+        B3, eb, fb = split_planes(b, 1, "hlh", 0)
+    if int((fa + fb).item()) != 0:
+        return fallback()
+    if out is None:
+        C = torch.mm(A3, B3, out_dtype=torch.float32)
+    else:
+        C = torch.mm(A3, B3, out_dtype=torch.float32, out=out)
+    check(lib().ha_split_unscale(_ptr(C), M, N, C.stride(0), _ptr(ea), _ptr(eb),
+                                 ctypes.c_void_p(stream_ptr(a.device))), "ha_split_unscale")
+    return C

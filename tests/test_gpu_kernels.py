@@ -292,3 +292,111 @@ def test_lasso_graph_replay_matches_eager(gpu, monkeypatch):
         est.fit(x, y)
         res.append(est.theta.larray.clone())
     assert torch.allclose(res[0], res[1], atol=1e-5)
+
+
+@pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 512, 768), (4099, 130, 65), (64, 4096, 64),
+                                   (2048, 2048, 2048)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+@pytest.mark.parametrize("scale", ["unit", "rows", "tiny", "huge"])
+def test_gemm_f16x3(m, k, n, layout, scale):
+    """fp16x3 split GEMM within fp32-GEMM error of the fp64 product, for every operand memory order
+    and for rows/columns spanning many orders of magnitude."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(m + k + n)
+    A = torch.randn(m, k, generator=g)
+    B = torch.randn(k, n, generator=g)
+    if scale == "rows":      # per-row / per-column magnitudes over 2^-40 .. 2^40, plus zero rows/cols
+        A *= torch.pow(2.0, torch.randint(-40, 40, (m, 1), generator=g).float())
+        B *= torch.pow(2.0, torch.randint(-40, 40, (1, n), generator=g).float())
+        A[::17] = 0
+        B[:, ::13] = 0
+    elif scale == "tiny":
+        A *= 1e-20
+        B *= 1e-10
+    elif scale == "huge":
+        A *= 1e18
+        B *= 1e15
+    A, B = A.to(dev), B.to(dev)
+    if layout[0] == "t":
+        A = A.t().contiguous().t()
+    if layout[1] == "t":
+        B = B.t().contiguous().t()
+    C = ops.gemm_f16x3(A, B)
+    assert C.dtype == torch.float32 and C.shape == (m, n)
+    ref = A.double() @ B.double()
+    # split error (<= 2^-21 per product) + fp32 accumulation over the tripled contraction (3k u)
+    bound = (A.double().abs() @ B.double().abs()) * (2.0 ** -20 + 3 * k * 2.0 ** -24) + 1e-300
+    err = (C.double() - ref).abs()
+    assert torch.all(err <= bound), (err / bound).max()
+    # same error class as the library fp32 GEMM
+    e32 = ((A @ B).double() - ref).abs().max()
+    if scale == "unit":
+        assert err.max() <= 8 * e32 + 1e-6
+
+
+def test_gemm_f16x3_nonfinite_falls_back(gpu):
+    from heat_amd import ops
+
+    A = torch.randn(256, 128, device="cuda")
+    B = torch.randn(128, 64, device="cuda")
+    A[3, 5] = float("nan")
+    B[7, 9] = float("inf")
+    C = ops.gemm_f16x3(A, B)
+    ref = A @ B
+    assert torch.equal(torch.isnan(C), torch.isnan(ref))
+    assert torch.allclose(C[~torch.isnan(ref)], ref[~torch.isnan(ref)], rtol=1e-5, atol=1e-4)
+
+
+def test_matmul_split_precision(gpu):
+    """ht.matmul / ht.linalg.qr honour torch's float32 matmul precision ("high" -> split GEMM)."""
+    import heat_amd as ht
+    from heat_amd.core.linalg import basics
+
+    ht.random.seed(2)
+    a = ht.random.randn(4096, 1024, split=0)
+    b = ht.random.randn(1024, 512)
+    ref = a.larray.double() @ b.larray.double()
+    old = torch.get_float32_matmul_precision()
+    calls = []
+    orig = basics._leaf_mm
+
+    def spy(x, y):
+        calls.append(basics._split_gemm_ok(x, y))
+        return orig(x, y)
+
+    basics._leaf_mm = spy
+    try:
+        torch.set_float32_matmul_precision("high")
+        c = ht.matmul(a, b).larray
+        q, r = ht.linalg.qr(a)
+    finally:
+        torch.set_float32_matmul_precision(old)
+        basics._leaf_mm = orig
+    assert any(calls)
+    assert torch.allclose(c.double(), ref, rtol=1e-5, atol=1e-3)
+    qr = q.larray.double() @ r.larray.double()
+    assert torch.allclose(qr, a.larray.double(), atol=1e-4)
+    qd = q.larray.double()
+    assert torch.allclose(qd.T @ qd, torch.eye(qd.shape[1], dtype=torch.float64, device="cuda"), atol=1e-4)
+
+
+@pytest.mark.parametrize("m,n", [(5000, 300), (131, 64), (20000, 1024)])
+def test_gemm_f16x3_gram(m, n):
+    """X^T X from one shared split (the QR / Gram path) == the generic split GEMM == fp64."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(m)
+    X = (torch.randn(m, n, generator=g) * torch.pow(2.0, torch.randint(-20, 20, (1, n), generator=g).float())).to(dev)
+    assert ops.kernels._is_gram(X.t(), X)
+    G = ops.gemm_f16x3(X.t(), X)
+    ref = X.double().t() @ X.double()
+    bound = (X.double().abs().t() @ X.double().abs()) * (2.0 ** -20 + 3 * m * 2.0 ** -24)
+    err = (G.double() - ref).abs()
+    assert torch.all(err <= bound)
+    # relative to the diagonal (no cancellation): same error class as the library fp32 GEMM
+    d = ref.diagonal()
+    e32 = (((X.t() @ X).double() - ref).abs().diagonal() / d).max()
+    assert (err.diagonal() / d).max() <= 8 * e32 + 1e-7
