@@ -86,9 +86,9 @@ class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
             nonlocal best_d, best_y
             if tb.shape[0] == 0 or nq == 0:
                 return
-            d = ops.cdist(q.float(), tb.float(), "sqeuclidean", exact=True)
+            # fused distance + running top-k kernel (no nq x nt matrix); exact distances of the picks
             kk = min(k, tb.shape[0])
-            dv, di = torch.topk(d, kk, dim=1, largest=False)
+            dv, di = ops.knn_topk(q.float(), tb.float(), kk)
             cand_d = torch.cat([best_d, dv], dim=1)
             cand_y = torch.cat([best_y, yb[di.reshape(-1)].reshape(nq, kk, -1)], dim=1)
             sel_d, sel = torch.topk(cand_d, k, dim=1, largest=False)

@@ -1,6 +1,7 @@
 """
 Build the native CDNA4 kernel library in-tree:
-``hipcc --offload-arch=gfx950 -O3 -shared -fPIC heat_amd/ops/csrc/*.hip -> heat_amd/ops/_lib/libheat_amd_kernels.so``.
+``hipcc --offload-arch=gfx950 -O3 -fPIC -c`` per ``heat_amd/ops/csrc/*.hip`` (in parallel), linked into
+``heat_amd/ops/_lib/libheat_amd_kernels.so``.
 
 The library exports a plain C ABI (``ha_*`` functions taking device pointers and a ``hipStream_t``)
 and is loaded with ctypes after torch, so it shares torch's HIP runtime (same SONAME
@@ -15,6 +16,7 @@ import shutil
 import subprocess
 import sys
 import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -53,16 +55,28 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
     fd, tmp = tempfile.mkstemp(suffix=".so", dir=LIBDIR)
     os.close(fd)
-    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-value",
-           "-Wno-unused-result", "-I" + CSRC] + sources() + ["-o", tmp]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    try:
+    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result",
+             "-I" + CSRC]
+    objdir = tempfile.mkdtemp(prefix="ha_obj_")
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, capture_output=not verbose)
+
+    # one hipcc per source in parallel (the template-heavy kernel files dominate a serial build)
+    objs = [os.path.join(objdir, os.path.basename(src) + ".o") for src in sources()]
+    jobs = max(1, min(len(objs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    try:
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(lambda so: run([hipcc()] + flags + ["-c", so[0], "-o", so[1]]), zip(sources(), objs)))
+        run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", tmp])
     except subprocess.CalledProcessError as e:
         os.unlink(tmp)
         msg = e.stderr.decode() if e.stderr else ""
         raise RuntimeError("building the native kernels failed:\n" + msg) from e
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     os.replace(tmp, LIBPATH)
     return LIBPATH
 

@@ -477,6 +477,140 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
   }
 }
 
+
+// k nearest "centroids" (KNN: the training points) of every point, the same fp16x3 scores as the
+// assignment (score = x.c - |c|^2/2 in the scaled space, larger = nearer) with a running top-KN
+// list per lane instead of a running max: no n x m distance matrix. A lane keeps its KN best
+// (score, index) sorted in registers; a tile's 16 candidates are only inserted where they beat
+// the lane's current KN-th best (after the first tiles nearly never: ~KN ln(m) insertions per
+// point), so the epilogue is a max + compare per tile in the common case. The two lane halves
+// (disjoint centroid halves of the same point) merge their lists at the end. Output: KN squared
+// distances (ascending) and int32 indices per point; -1 / +inf where fewer than KN exist.
+template <int KN>
+__device__ __forceinline__ void topk_insert(float (&tv)[KN], int (&ti)[KN], float v, int id) {
+#pragma unroll
+  for (int s = KN - 1; s >= 1; --s) {
+    const bool ap = v > tv[s - 1];
+    const bool ac = v > tv[s];
+    tv[s] = ap ? tv[s - 1] : (ac ? v : tv[s]);
+    ti[s] = ap ? ti[s - 1] : (ac ? id : ti[s]);
+  }
+  const bool a0 = v > tv[0];
+  tv[0] = a0 ? v : tv[0];
+  ti[0] = a0 ? id : ti[0];
+}
+
+template <int FPAD, int KN>
+__global__ __launch_bounds__(256, 2) void h3_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+                                                  int64_t n, const _Float16* __restrict__ image,
+                                                  const float* __restrict__ u, const float* __restrict__ meta,
+                                                  int nchunks, int cps, int kout, float* __restrict__ dist,
+                                                  int* __restrict__ idx) {
+  using K = H3Cfg<FPAD, 1>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, CHUNK_H = K::CHUNK_H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t p = (int64_t)blockIdx.x * K::PTS_PER_WG + wave * 32 + j;
+  const int64_t row = p < n ? p : n - 1;
+
+  halfx8 bhi[KS], blo[KS];
+  const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+  float q = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bhi[ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+    blo[ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xv = (float)bhi[ks][i] + (float)blo[ks][i];
+      q = fmaf(xv, xv, q);
+    }
+  }
+  const float sx = sxv[row];
+  const float nsx = -sx;
+  float tv[KN];
+  int ti[KN];
+#pragma unroll
+  for (int s = 0; s < KN; ++s) {
+    tv[s] = -__builtin_huge_valf();
+    ti[s] = -1;
+  }
+  constexpr int PIECES = CHUNK_H * 2 / 1024;
+  // blockIdx.y: a range of centroid chunks (split over the centroids when the points alone cannot
+  // fill the GPU); partial lists go to slice blockIdx.y of the outputs
+  const int ch0 = blockIdx.y * cps;
+  const int ch1 = ch0 + cps < nchunks ? ch0 + cps : nchunks;
+  dist += (int64_t)blockIdx.y * n * kout;
+  idx += (int64_t)blockIdx.y * n * kout;
+  for (int ch = ch0; ch < ch1; ++ch) {
+    {
+      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+#pragma unroll
+      for (int pc = wave; pc < PIECES; pc += 4)
+        __builtin_amdgcn_global_load_lds(src + pc * 1024,
+                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H * 2), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+    const _Float16* img = reinterpret_cast<const _Float16*>(smem);
+    const float* ub = reinterpret_cast<const float*>(smem + CHUNK_H * 2);
+#pragma unroll 2
+    for (int cb = 0; cb < CB / 32; ++cb) {
+      floatx16 acc = (floatx16)(0.f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
+        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
+        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[ks], acc, 0, 0, 0);
+      }
+      float w[16];
+      float m = -__builtin_huge_valf();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const floatx4 cn = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          w[4 * g + i] = fmaf(nsx, cn[i], acc[4 * g + i]);
+          m = fmaxf(m, w[4 * g + i]);
+        }
+      }
+      if (m > tv[KN - 1]) {
+        const int tbase = (ch * (CB / 32) + cb) * 32 + 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (w[r] > tv[KN - 1]) topk_insert<KN>(tv, ti, w[r], tbase + (r & 3) + 8 * (r >> 2));
+      }
+    }
+    __syncthreads();
+  }
+  // merge the partner half's list (disjoint candidates) into lane half 0
+#pragma unroll
+  for (int s = 0; s < KN; ++s) {
+    const float ov = __shfl_xor(tv[s], 32, 64);
+    const int oi = __shfl_xor(ti[s], 32, 64);
+    if (h == 0 && ov > tv[KN - 1]) topk_insert<KN>(tv, ti, ov, oi);
+  }
+  const float xs = q + __shfl_xor(q, 32, 64);  // all lanes: a shuffle from an inactive lane is undefined
+  if (h == 0 && p < n) {
+    const float isx = 1.f / sx, sC = meta[0];
+#pragma unroll
+    for (int s = 0; s < KN; ++s)
+      if (s < kout) {
+        const bool ok = ti[s] >= 0;
+        dist[p * kout + s] = ok ? fmaxf(xs * isx * isx - 2.f * tv[s] * isx / sC, 0.f) : __builtin_huge_valf();
+        idx[p * kout + s] = ti[s];
+      }
+  }
+}
+
 int h3_fpad(int f) { return f <= 16 ? 16 : f <= 32 ? 32 : f <= 64 ? 64 : f <= 128 ? 128 : -1; }
 
 }  // namespace
@@ -606,5 +740,63 @@ HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_
       return HA_UNSUPPORTED;
   }
 #undef HA_H1
+  return ha_launch_status();
+}
+
+// k nearest rows of C (m rows, e.g. KNN training points) for each of the n packed points:
+// dist [n, kout] squared distances ascending, idx [n, kout] int32 (row of C; -1 past m).
+// kout <= 16. workspace: ha_h3_workspace_bytes(m, f). splits > 1: the centroid chunks are divided
+// over `splits` workgroup columns and dist/idx hold `splits` partial [n, kout] lists (the caller
+// merges them); ha_h3_topk_chunks(m, f) gives the number of chunks to divide.
+HA_EXPORT int ha_h3_topk_chunks(int m, int f) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || m <= 0) return -1;
+  const int cb = fpad >= 128 ? 64 : 128;
+  return (m + cb - 1) / cb;
+}
+
+HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, const float* C, int m, int64_t ldc,
+                         void* workspace, int kout, int splits, float* dist, int* idx, void* stream) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || m <= 0 || kout <= 0 || kout > 16) return HA_UNSUPPORTED;
+  if (n <= 0) return HA_OK;
+  if (splits < 1 || splits > ha_h3_topk_chunks(m, f) || splits > 65535) return HA_BAD_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int cb = fpad >= 128 ? 64 : 128;
+  const int kpad = (m + cb - 1) / cb * cb;
+  _Float16* image = (_Float16*)workspace;
+  float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
+  float* meta = u + kpad;
+  const _Float16* p = (const _Float16*)planes;
+#define HA_TK_LAUNCH(FP, KN)                                                                                 \
+  hipLaunchKernelGGL((h3_topk<FP, KN>), dim3(blocks, splits), dim3(256), lds, s, p, sx, n, image, u, meta,      \
+                     kpad / KC::CB, (kpad / KC::CB + splits - 1) / splits, kout, dist, idx)
+#define HA_TK(FP)                                                                                            \
+  case FP: {                                                                                                 \
+    using KC = H3Cfg<FP, 1>;                                                                                 \
+    hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                           \
+    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, m, f, ldc, meta);                               \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),   \
+                       dim3(256), 0, s, C, m, f, ldc, kpad, image, u, meta);                                \
+    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                 \
+    const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                          \
+    if (kout <= 4)                                                                                           \
+      HA_TK_LAUNCH(FP, 4);                                                                                   \
+    else if (kout <= 8)                                                                                      \
+      HA_TK_LAUNCH(FP, 8);                                                                                   \
+    else                                                                                                     \
+      HA_TK_LAUNCH(FP, 16);                                                                                  \
+    break;                                                                                                   \
+  }
+  switch (fpad) {
+    HA_TK(16)
+    HA_TK(32)
+    HA_TK(64)
+    HA_TK(128)
+    default:
+      return HA_UNSUPPORTED;
+  }
+#undef HA_TK
+#undef HA_TK_LAUNCH
   return ha_launch_status();
 }

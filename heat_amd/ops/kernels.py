@@ -14,7 +14,7 @@ import torch.nn.functional as F
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes"]
+           "split_planes", "knn_topk"]
 
 _NUM_CUS = {}
 
@@ -141,6 +141,70 @@ def kmeans_assign(X: torch.Tensor, C: torch.Tensor, want_mind: bool = True,
 
 
 kmeans_assign.last_rechecked = None
+
+
+def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPoints] = None,
+             exact_distances: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The ``k`` nearest rows of ``T`` for every row of ``Q``: (squared distances [nq, k] ascending,
+    int64 row indices [nq, k]; +inf / -1 where T has fewer than k rows).
+
+    Device fp32 with k <= 16 and f <= 128: ONE fused kernel (fp16x3 MFMA scores + a running top-k
+    per point in registers, ``csrc/kmeans_f16x3.hip: h3_topk``), no nq x nt distance matrix. The
+    selected neighbours' distances are then recomputed exactly (difference form) and re-sorted
+    (``exact_distances``). Otherwise: distance tiles + torch.topk, in query blocks."""
+    nq, f = Q.shape
+    nt = T.shape[0]
+    dev = Q.device
+    if nq == 0 or nt == 0 or k <= 0:
+        return (torch.full((nq, max(k, 0)), float("inf"), device=dev),
+                torch.full((nq, max(k, 0)), -1, dtype=torch.int64, device=dev))
+    if use_native(Q) and Q.dtype == torch.float32 and T.dtype == torch.float32 and k <= 16 \
+            and lib().ha_h3_fpad(f) > 0 and nt < 2 ** 31 - 256:
+        L = lib()
+        if packed is None or packed.key != _points_key(Q):
+            packed = kmeans_pack_points(Q)
+        Tc = T if T.stride(-1) == 1 else T.contiguous()
+        ws = torch.empty(L.ha_h3_workspace_bytes(nt, f), dtype=torch.uint8, device=dev)
+        # fill the GPU: with few query blocks, divide the training chunks over workgroup columns
+        # (>= 4 waves of 128 queries per CU overall) and merge the partial lists
+        qblocks = (nq + 127) // 128
+        splits = max(1, min(L.ha_h3_topk_chunks(nt, f) // 4, (4 * num_cus(dev) + qblocks - 1) // qblocks))
+        dist = torch.empty((splits, nq, k), dtype=torch.float32, device=dev)
+        idx = torch.empty((splits, nq, k), dtype=torch.int32, device=dev)
+        check(L.ha_h3_topk(_ptr(packed.planes), _ptr(packed.sx), nq, f, _ptr(Tc), nt, Tc.stride(0), _ptr(ws), k,
+                           splits, _ptr(dist), _ptr(idx), ctypes.c_void_p(stream_ptr(dev))), "ha_h3_topk")
+        if splits == 1:
+            dist, idx = dist[0], idx[0].long()
+        else:
+            dist = dist.permute(1, 0, 2).reshape(nq, splits * k)
+            idx = idx.permute(1, 0, 2).reshape(nq, splits * k)
+            dist, sel = torch.topk(dist, k, dim=1, largest=False)
+            idx = torch.gather(idx, 1, sel).long()
+    else:
+        kk = min(k, nt)
+        step = max(1, (1 << 28) // max(nt, 1))
+        ds, ids = [], []
+        for q0 in range(0, nq, step):
+            d = cdist(Q[q0: q0 + step].float(), T.float(), "sqeuclidean", exact=True)
+            dv, di = torch.topk(d, kk, dim=1, largest=False)
+            ds.append(dv)
+            ids.append(di)
+        dist, idx = torch.cat(ds), torch.cat(ids)
+        if kk < k:
+            dist = torch.cat([dist, torch.full((nq, k - kk), float("inf"), device=dev)], 1)
+            idx = torch.cat([idx, torch.full((nq, k - kk), -1, dtype=torch.int64, device=dev)], 1)
+        return dist, idx
+    if exact_distances:
+        step = max(1, (1 << 26) // (k * f))
+        for q0 in range(0, nq, step):
+            ib = idx[q0: q0 + step]
+            nb = T[ib.clamp(min=0)].float()
+            d = ((Q[q0: q0 + step].float().unsqueeze(1) - nb) ** 2).sum(-1)
+            d = torch.where(ib >= 0, d, torch.full_like(d, float("inf")))
+            d, order = torch.sort(d, dim=1)
+            dist[q0: q0 + step] = d
+            idx[q0: q0 + step] = torch.gather(ib, 1, order)
+    return dist, idx
 
 
 def kmeans_update(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

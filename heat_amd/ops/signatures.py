@@ -5,6 +5,9 @@ c_void_p, c_int, c_int64, c_uint64, c_float, c_double = (ctypes.c_void_p, ctypes
                                                          ctypes.c_uint64, ctypes.c_float, ctypes.c_double)
 
 SIGNATURES = {
+    "ha_h3_topk": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p, c_int, c_int,
+                           c_void_p, c_void_p, c_void_p]),
+    "ha_h3_topk_chunks": (c_int, [c_int, c_int]),
     "ha_split_absmax": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "ha_split3": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_int64, c_void_p, c_void_p]),

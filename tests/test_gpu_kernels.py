@@ -400,3 +400,50 @@ def test_gemm_f16x3_gram(m, n):
     d = ref.diagonal()
     e32 = (((X.t() @ X).double() - ref).abs().diagonal() / d).max()
     assert (err.diagonal() / d).max() <= 8 * e32 + 1e-7
+
+
+@pytest.mark.parametrize("nq,nt,f", [(1000, 5000, 3), (777, 300, 18), (4096, 20000, 64), (300, 1000, 100),
+                                     (513, 129, 128), (50, 7, 16)])
+@pytest.mark.parametrize("k", [1, 5, 8, 16])
+def test_knn_topk(nq, nt, f, k):
+    """Fused distance + running top-k kernel == exact fp64 k nearest neighbours (up to near-ties)."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(nq + nt + f + k)
+    Q = torch.randn(nq, f, generator=g).to(dev)
+    T = torch.randn(nt, f, generator=g).to(dev)
+    dist, idx = ops.knn_topk(Q, T, k)
+    assert dist.shape == (nq, k) and idx.dtype == torch.int64
+    d = torch.cdist(Q.double(), T.double()) ** 2
+    kk = min(k, nt)
+    ref, _ = torch.topk(d, kk, dim=1, largest=False)
+    assert torch.allclose(dist[:, :kk].double(), ref, rtol=1e-5, atol=1e-5)
+    # the reported indices really are at the reported distances
+    assert torch.allclose(d.gather(1, idx[:, :kk]), dist[:, :kk].double(), rtol=1e-5, atol=1e-5)
+    if kk < k:
+        assert torch.all(idx[:, kk:] == -1) and torch.all(torch.isinf(dist[:, kk:]))
+    # the kernel's own (quadratic-expansion) distances, which also rank the split partial lists
+    draw, _ = ops.knn_topk(Q, T, k, exact_distances=False)
+    scale = (Q.double() ** 2).sum(1, keepdim=True) + (T.double() ** 2).sum(1).max()
+    assert torch.all((draw[:, :kk].double() - ref).abs() <= 1e-5 * scale)
+    # no duplicate neighbours
+    s, _ = idx[:, :kk].sort(1)
+    assert torch.all(s[:, 1:] != s[:, :-1])
+
+
+def test_knn_classifier_fused(gpu):
+    import heat_amd as ht
+
+    ht.random.seed(4)
+    X = ht.random.randn(3000, 8, split=0)
+    y = (X.larray[:, 0] > 0).long()
+    yd = ht.array(y, is_split=0)
+    knn = ht.classification.KNeighborsClassifier(n_neighbors=5)
+    knn.fit(X, yd)
+    pred = knn.predict(X[:500]).larray
+    Xd = X.larray.double()
+    d = torch.cdist(Xd[:500], Xd)
+    nn_idx = d.topk(5, largest=False).indices
+    ref = (y[nn_idx].sum(1) >= 3).long()
+    assert (pred.cpu() == ref.cpu()).float().mean() > 0.99
