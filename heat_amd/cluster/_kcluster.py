@@ -50,7 +50,9 @@ class _KCluster(ClusteringMixin, BaseEstimator):
 
     def _assign_labels(self, X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
         """int32 nearest-centroid labels of the local points (native fused kernels)."""
-        packed = self._packed(X) if X.dtype == torch.float32 else None
+        # the fp16x3 planes serve the MFMA kernels only (k <= 16 runs the exact VALU kernel)
+        packed = self._packed(X) if X.dtype == torch.float32 and not ops.kernels._small_k_ok(X, C.shape[0]) \
+            else None
         probe = self._cert_probe
         if probe is not None and probe[1].query():
             self._certify = probe[0].item() <= self.CERT_MAX_RECHECK * probe[2]

@@ -38,8 +38,12 @@ class KMeans(_KCluster):
     def _centroid_step(self, X: torch.Tensor, C: torch.Tensor, comm, distributed: bool):
         """One Lloyd step on the local block: returns (new centroids, int32 labels)."""
         k = C.shape[0]
-        labels = self._assign_labels(X, C)
-        sums, counts = ops.kmeans_update(X, labels, k)
+        fused = ops.kmeans_step_small(X, C)   # exact fp32: serves both precisions
+        if fused is not None:   # few clusters: assignment and sums in one pass over the points
+            labels, sums, counts = fused
+        else:
+            labels = self._assign_labels(X, C)
+            sums, counts = ops.kmeans_update(X, labels, k)
         packed = torch.cat([sums.reshape(-1).double(), counts.double()])
         if distributed:
             comm.Allreduce(MPI.IN_PLACE, packed, MPI.SUM)

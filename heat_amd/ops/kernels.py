@@ -14,7 +14,7 @@ import torch.nn.functional as F
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes", "knn_topk"]
+           "split_planes", "knn_topk", "kmeans_step_small"]
 
 _NUM_CUS = {}
 
@@ -76,10 +76,45 @@ def kmeans_pack_points(X: torch.Tensor) -> Optional[PackedPoints]:
     return PackedPoints(planes, sx, n, f, _points_key(X))
 
 
+def _small_k_ok(X: torch.Tensor, k: int) -> bool:
+    return (use_native(X) and X.dtype == torch.float32 and X.dim() == 2 and 0 < k <= 16
+            and 0 < X.shape[1] <= 64 and X.stride(-1) == 1)
+
+
+def _ks_step(X: torch.Tensor, C: torch.Tensor, want_mind: bool, update: bool):
+    L = lib()
+    n, f = X.shape
+    k = C.shape[0]
+    dev = X.device
+    Cc = C.to(device=dev, dtype=torch.float32)
+    Cc = Cc if Cc.stride(-1) == 1 else Cc.contiguous()
+    labels = torch.empty(n, dtype=torch.int32, device=dev)
+    mind = torch.empty(n, dtype=torch.float32, device=dev) if want_mind else None
+    ncu = num_cus(dev)
+    ws = torch.empty(max(1, L.ha_ks_workspace_floats(k, ncu)), dtype=torch.float32, device=dev)
+    sums = torch.empty((k, f), dtype=torch.float32, device=dev) if update else None
+    counts = torch.empty(k, dtype=torch.float32, device=dev) if update else None
+    check(L.ha_ks_step(_ptr(X), n, f, X.stride(0), _ptr(Cc), k, Cc.stride(0), _ptr(labels), _ptr(mind), _ptr(sums),
+                       _ptr(counts), _ptr(ws), ncu, ctypes.c_void_p(stream_ptr(dev))), "ha_ks_step")
+    return labels, mind, sums, counts
+
+
+def kmeans_step_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+    """One fused Lloyd pass for few clusters (k <= 16, f <= 64, device fp32): (int32 labels,
+    per-cluster sums [k, f], counts [k]) reading the points once; None where it does not apply."""
+    if not _small_k_ok(X, C.shape[0]):
+        return None
+    labels, _, sums, counts = _ks_step(X, C, want_mind=False, update=True)
+    return labels, sums, counts
+
+
 def kmeans_assign(X: torch.Tensor, C: torch.Tensor, want_mind: bool = True,
                   packed: Optional[PackedPoints] = None,
                   certified: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Nearest centroid (squared L2) of every row of X. Returns (int32 labels, min squared distance).
+
+    k <= 16 and f <= 64: exact fp32 VALU kernel (difference form, HBM-bound) whatever ``packed``
+    says.
 
     Device tensors, fused kernels with a running argmin (no n x k intermediate):
     ``packed`` given (from :func:`kmeans_pack_points`) -> fp16x3 split on the FP16 matrix cores
@@ -94,6 +129,12 @@ def kmeans_assign(X: torch.Tensor, C: torch.Tensor, want_mind: bool = True,
     if n == 0:
         return (torch.empty(0, dtype=torch.int32, device=X.device),
                 torch.empty(0, dtype=torch.float32, device=X.device) if want_mind else None)
+    if _small_k_ok(X, k):
+        # few clusters: exact VALU kernel over LDS-staged tiles, HBM-bound (csrc/kmeans_smallk.hip)
+        labels, mind, _, _ = _ks_step(X, C, want_mind=want_mind, update=False)
+        if certified:
+            kmeans_assign.last_rechecked = torch.zeros((), dtype=torch.int32, device=X.device)
+        return labels, mind
     if packed is not None and use_native(X):
         if packed.n != n or packed.f != f:
             raise ValueError("packed points do not match X")

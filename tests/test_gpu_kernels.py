@@ -447,3 +447,55 @@ def test_knn_classifier_fused(gpu):
     nn_idx = d.topk(5, largest=False).indices
     ref = (y[nn_idx].sum(1) >= 3).long()
     assert (pred.cpu() == ref.cpu()).float().mean() > 0.99
+
+
+@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (3000, 128), (777, 200), (100, 1), (300000, 60)])
+@pytest.mark.parametrize("k", [1, 3, 8, 16])
+def test_kmeans_step_small(n, f, k):
+    """Fused small-k Lloyd pass: labels == fp64 argmin, sums/counts == index_add of the points."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n * 3 + k + f)
+    X = torch.randn(n, f + 3, generator=g).to(dev)[:, :f]   # strided rows
+    for Xv in (X, X.contiguous()):
+        C = torch.randn(k, f, generator=g).to(dev)
+        res = ops.kmeans_step_small(Xv, C)
+        if f > 64:
+            assert res is None
+            continue
+        lab, sums, counts = res
+        d = torch.cdist(Xv.double(), C.double()) ** 2
+        chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+        assert torch.all(chosen - d.min(1).values <= 1e-5 * (1 + d.min(1).values))
+        ref = torch.zeros(k, f, dtype=torch.float64, device=dev).index_add_(0, lab.long(), Xv.double())
+        mag = torch.zeros(k, f, dtype=torch.float64, device=dev).index_add_(0, lab.long(), Xv.double().abs())
+        assert torch.all((sums.double() - ref).abs() <= 1e-6 * mag + 1e-6)
+        assert torch.equal(counts.long(), torch.bincount(lab.long(), minlength=k))
+
+
+@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (3000, 128), (777, 200)])
+@pytest.mark.parametrize("k", [1, 3, 8, 16])
+def test_kmeans_assign_small_k(n, f, k):
+    """k <= 16: exact VALU kernel, labels == fp64 argmin (ties -> lowest index), exact min distance."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + k + f)
+    X = torch.randn(n, f, generator=g).to(dev)
+    C = torch.randn(k, f, generator=g).to(dev)
+    if k > 1:
+        C[-1] = C[0]          # exact duplicate centroid: never chosen over index 0
+    lab, mind = ops.kmeans_assign(X, C)
+    d = torch.cdist(X.double(), C.double()) ** 2
+    ref_min, ref_lab = d.min(1)
+    chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+    assert torch.all(chosen - ref_min <= 1e-5 * (1 + ref_min))
+    assert (lab.long() == ref_lab).float().mean() > 0.9999
+    if k > 1:
+        assert not torch.any(lab == k - 1)
+    assert torch.allclose(mind.double(), ref_min, rtol=1e-5, atol=1e-5)
+    Xs = X[:, : max(1, f - 1)]   # strided rows (no 16-byte alignment): scalar path
+    lab2, _ = ops.kmeans_assign(Xs, C[:, : Xs.shape[1]].contiguous())
+    d2 = torch.cdist(Xs.double(), C[:, : Xs.shape[1]].double()) ** 2
+    assert (lab2.long() == d2.argmin(1)).float().mean() > 0.9999
