@@ -32,7 +32,8 @@ __all__ = ["enable", "disable", "enabled", "counters", "reset", "region", "log",
 _COLLECTIVES = ["Allreduce", "Iallreduce", "Bcast", "Ibcast", "Allgather", "Allgatherv", "Iallgather", "Iallgatherv",
                 "Alltoall", "Alltoallv", "Gatherv", "Scatterv", "Exscan", "Scan", "Reduce", "Send", "Recv", "Isend",
                 "Irecv", "exchange", "allgather_tensor", "Barrier", "bcast", "allgather", "allreduce"]
-_KERNELS = ["kmeans_assign", "kmeans_update", "moments", "cdist", "lasso_epoch"]
+_KERNELS = ["kmeans_assign", "kmeans_update", "kmeans_step_small", "moments", "cdist", "lasso_epoch", "knn_topk",
+            "gemm_f16x3"]
 
 _state = {"enabled": False, "timing": False, "originals": {}}
 _counters: Dict[str, Dict[str, float]] = defaultdict(lambda: {"calls": 0, "bytes": 0, "ms": 0.0})

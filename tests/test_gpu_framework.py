@@ -40,12 +40,16 @@ def test_profiling_counts_native_kernels(gpu):
     profiling.enable(timing=True)
     try:
         x = ht.random.randn(4096, 16, split=0)
-        km = ht.cluster.KMeans(n_clusters=8, init="random", max_iter=3)
+        km = ht.cluster.KMeans(n_clusters=8, init="random", max_iter=3)    # fused small-k pass
+        km.fit(x)
+        km = ht.cluster.KMeans(n_clusters=40, init="random", max_iter=3)   # MFMA assign + update
         km.fit(x)
         c = profiling.counters()
     finally:
         profiling.disable()
+    assert c["kmeans_step_small"]["calls"] >= 3 and c["kmeans_step_small"]["ms"] > 0
     assert c["kmeans_assign"]["calls"] >= 3 and c["kmeans_assign"]["ms"] > 0
+    assert c["kmeans_update"]["calls"] >= 3
 
 
 def test_data_parallel_on_gpu(gpu):
