@@ -18,6 +18,8 @@
 // conflict-free lane-linear ds_read_b128.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
@@ -611,6 +613,183 @@ __global__ __launch_bounds__(256, 2) void h3_topk(const _Float16* __restrict__ p
   }
 }
 
+// Resident-centroid assignment ("r"): ONE workgroup per CU (NW waves) stages up to RC centroid
+// chunks into LDS once (128 KB: 512 centroids at f = 64) and its waves then stream point blocks
+// through them with no further barrier or staging; per-wave point blocks are independent. k above
+// the resident capacity runs in phases over the centroid chunks, carrying each point's running
+// best (value, index) through global memory (the planes are re-read once per phase). Compared with
+// h3_assign_p (a workgroup per 256 points re-staging all k centroids chunk by chunk behind a
+// barrier), this removes the per-chunk DMA + barrier and the per-workgroup start-up: 2.27 vs
+// 2.52 ms at k = 512, 1.24 vs 1.39 ms at k = 200 (n = 12.5M, f = 64,
+// tools/microbench/resident_bench.py). In phases (k = 1024) it is no faster (4.32-4.42 vs 4.39 ms
+// alone, 5.28 vs 5.07 ms per full Lloyd step), so callers use it where the centroids fit. A
+// 16-wave NPB = 1 variant (4 waves/SIMD) was no faster either (4.45 ms): the loop is bound by the
+// MFMA + epilogue issue, not by latency.
+// first: no carried state; last: write labels (+ mind) instead of the carried state.
+// SGV > 0 pins an MFMA / SGV-VALU interleave with sched_group_barrier (measured 4: 4.60 ms, none
+// or 8: 4.32 ms at k = 1024; default none).
+template <int FPAD, int NPB_, int NW, int SGV = 0>
+__global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __restrict__ planes,
+                                                          const float* __restrict__ sxv, int64_t n,
+                                                          const _Float16* __restrict__ image,
+                                                          const float* __restrict__ u, const float* __restrict__ meta,
+                                                          int ch0, int nch, int first, int last,
+                                                          float* __restrict__ pbest, int* __restrict__ pidx,
+                                                          int* __restrict__ labels, float* __restrict__ mind) {
+  using K = H3Cfg<FPAD, NPB_>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  // ---- stage this phase's chunks (image by LDS-DMA, u by plain loads), once
+  {
+    const char* src = reinterpret_cast<const char*>(image + (int64_t)ch0 * CHUNK_H) + lane * 16;
+    const int pieces = nch * (CHUNK_H * 2 / 1024);
+    for (int pc = wave; pc < pieces; pc += NW)
+      __builtin_amdgcn_global_load_lds(src + (int64_t)pc * 1024,
+                                       (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
+    float* us = reinterpret_cast<float*>(smem + (size_t)nch * CHUNK_H * 2);
+    for (int e = tid; e < nch * CB; e += NW * 64) us[e] = u[ch0 * CB + e];
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const float* ubase = reinterpret_cast<const float*>(smem + (size_t)nch * CHUNK_H * 2);
+  const float sC = meta[0];
+
+  for (int64_t blk = (int64_t)blockIdx.x * NW + wave; blk * (NPB * 32) < n; blk += (int64_t)gridDim.x * NW) {
+    const int64_t pbase = blk * (NPB * 32);
+    halfx8 bhi[NPB][KS], blo[NPB][KS];
+    float sx[NPB], nsx[NPB], xsq[NPB];
+    int64_t prow[NPB];
+    float best[NPB];
+    int btile[NPB], pin[NPB];
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      const int64_t idx = pbase + pb * 32 + j;
+      const int64_t row = idx < n ? idx : n - 1;
+      prow[pb] = idx < n ? row : -1;
+      const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+      float q = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+        blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
+          q = fmaf(xv, xv, q);
+        }
+      }
+      sx[pb] = sxv[row];
+      nsx[pb] = -sx[pb];
+      xsq[pb] = q;
+      // carried best of the earlier phases (lower centroid indices win ties: strict > below)
+      best[pb] = first ? -__builtin_huge_valf() : pbest[row];
+      pin[pb] = first ? 0 : pidx[row];
+      btile[pb] = -1;
+    }
+    float sv[NPB][16];
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
+
+    floatx16 acc[2][NPB];
+    floatx4 cnr[2][4];
+    int ptile = -1;
+    auto epilogue = [&](const floatx16 (&ac)[NPB], const floatx4 (&cn)[4], int tile) {
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) {
+        const floatx2 sx2 = {nsx[pb], nsx[pb]};
+        float w[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+          const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
+          const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+          w[2 * q] = r2[0];
+          w[2 * q + 1] = r2[1];
+        }
+        float m = w[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
+        const bool imp = m > best[pb];
+        best[pb] = imp ? m : best[pb];
+        btile[pb] = imp ? tile : btile[pb];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[pb][r] = imp ? w[r] : sv[pb][r];
+      }
+    };
+    for (int ch = 0; ch < nch; ++ch) {
+      const _Float16* img = reinterpret_cast<const _Float16*>(smem + (size_t)ch * CHUNK_H * 2);
+      const float* ub = ubase + ch * CB;
+#pragma unroll
+      for (int cb = 0; cb < CB / 32; ++cb) {
+        const int cur = cb & 1;
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) acc[cur][pb] = (floatx16)(0.f);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
+          const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
+          const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
+#pragma unroll
+          for (int pb = 0; pb < NPB; ++pb) {
+            acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+            acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[cur][pb], 0, 0, 0);
+            acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) cnr[cur][g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+        if (ptile >= 0) epilogue(acc[cur ^ 1], cnr[cur ^ 1], ptile);
+        ptile = (ch0 + ch) * (CB / 32) + cb;
+        if constexpr (SGV > 0) {
+#pragma unroll
+          for (int i = 0; i < 3 * KS * NPB; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, SGV, 0);  // then up to SGV VALU
+          }
+        }
+      }
+    }
+    if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], cnr[((CB / 32) - 1) & 1], ptile);
+
+    int bidx[NPB];
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      int bi = 15;
+#pragma unroll
+      for (int r = 14; r >= 0; --r) bi = sv[pb][r] == best[pb] ? r : bi;
+      bidx[pb] = btile[pb] >= 0 ? btile[pb] * 32 + (bi & 3) + 8 * (bi >> 2) + 4 * h : pin[pb];
+    }
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      const float ob = __shfl_xor(best[pb], 32, 64);
+      const int oi = __shfl_xor(bidx[pb], 32, 64);
+      const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
+      if (ob > best[pb] || (ob == best[pb] && oi < bidx[pb])) {
+        best[pb] = ob;
+        bidx[pb] = oi;
+      }
+      const int64_t row = prow[pb];
+      if (h == 0 && row >= 0) {
+        if (last) {
+          labels[row] = bidx[pb];
+          if (mind) {
+            const float isx = 1.f / sx[pb];
+            mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
+          }
+        } else {
+          pbest[row] = best[pb];
+          pidx[row] = bidx[pb];
+        }
+      }
+    }
+  }
+}
+
 int h3_fpad(int f) { return f <= 16 ? 16 : f <= 32 ? 32 : f <= 64 ? 64 : f <= 128 ? 128 : -1; }
 
 }  // namespace
@@ -798,5 +977,70 @@ HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, 
   }
 #undef HA_TK
 #undef HA_TK_LAUNCH
+  return ha_launch_status();
+}
+
+// Resident-centroid assignment (h3_assign_r): chunks resident per phase and number of phases.
+constexpr int H3R_LDS = 128 * 1024;   // image budget per workgroup (+ u)
+constexpr int H3R_NW = 8;             // waves per workgroup (one workgroup per CU)
+
+HA_EXPORT int ha_h3r_phases(int k, int f) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || k <= 0) return -1;
+  const int cb = fpad >= 128 ? 64 : 128;
+  const int nchunks = (k + cb - 1) / cb;
+  const int rc = H3R_LDS / (cb * fpad * 4);
+  return (nchunks + rc - 1) / rc;
+}
+
+// scratch: n floats + n ints (carried best between phases; unused with one phase)
+HA_EXPORT int ha_h3_assign_r(const void* planes, const float* sx, int64_t n, int f, const float* C, int k,
+                             int64_t ldc, void* workspace, void* scratch, int num_cus, int* labels, float* mind,
+                             void* stream) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || k <= 0 || num_cus <= 0) return HA_UNSUPPORTED;
+  if (n <= 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int cb = fpad >= 128 ? 64 : 128;
+  const int kpad = (k + cb - 1) / cb * cb;
+  const int nchunks = kpad / cb;
+  const int rc = H3R_LDS / (cb * fpad * 4);
+  const int phases = (nchunks + rc - 1) / rc;
+  if (phases > 1 && !scratch) return HA_BAD_ARG;
+  _Float16* image = (_Float16*)workspace;
+  float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
+  float* meta = u + kpad;
+  const _Float16* p = (const _Float16*)planes;
+  float* pb = (float*)scratch;
+  int* pi = scratch ? (int*)((char*)scratch + n * sizeof(float)) : nullptr;
+  const int64_t blocks_needed = (n + 64 * H3R_NW - 1) / (64 * H3R_NW);
+  const unsigned grid = (unsigned)(blocks_needed < num_cus ? blocks_needed : num_cus);
+#define HA_H3R(FP)                                                                                          \
+  case FP: {                                                                                                \
+    constexpr int NPB = FP >= 128 ? 1 : 2;                                                                  \
+    using KC = H3Cfg<FP, NPB>;                                                                              \
+    hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
+    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
+                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
+    for (int ph = 0; ph < phases; ++ph) {                                                                   \
+      const int c0 = ph * rc, nc = nchunks - c0 < rc ? nchunks - c0 : rc;                                   \
+      const size_t lds = (size_t)nc * KC::CHUNK_H * 2 + (size_t)nc * KC::CB * 4;                            \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(h3_assign_r<FP, NPB, H3R_NW>),                      \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
+      hipLaunchKernelGGL((h3_assign_r<FP, NPB, H3R_NW>), dim3(grid), dim3(H3R_NW * 64), lds, s, p, sx, n, image, \
+                         u, meta, c0, nc, ph == 0, ph == phases - 1, pb, pi, labels, mind);                  \
+    }                                                                                                       \
+    break;                                                                                                  \
+  }
+  switch (fpad) {
+    HA_H3R(16)
+    HA_H3R(32)
+    HA_H3R(64)
+    HA_H3R(128)
+    default:
+      return HA_UNSUPPORTED;
+  }
+#undef HA_H3R
   return ha_launch_status();
 }

@@ -58,6 +58,32 @@ def test_kmeans_assign_f16x3(n, k, f, scale):
     assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-4 * scale * scale * f)
 
 
+@pytest.mark.parametrize("mode", ["resident_all", "chunked"])
+@pytest.mark.parametrize("n,k,f", [(5000, 300, 32), (70000, 1500, 64), (3333, 700, 100), (9000, 2100, 16)])
+def test_kmeans_assign_f16x3_kernels(n, k, f, mode, monkeypatch):
+    """Both fp16x3 assignment kernels: LDS-resident centroids (in phases past the LDS capacity,
+    carrying the running best through global memory) and chunk-staged; same labels and distances."""
+    from heat_amd import ops
+
+    dev = _dev()
+    monkeypatch.setattr(ops.kernels, "_H3_RESIDENT", mode == "resident_all")
+    monkeypatch.setattr(ops.kernels, "_H3_RESIDENT_ALL", mode == "resident_all")
+    g = torch.Generator(device="cpu").manual_seed(n + k + f)
+    X = torch.randn(n, f, generator=g).to(dev)
+    C = torch.randn(k, f, generator=g).to(dev)
+    C[k - 1] = C[3]          # exact duplicate: the lower index must win
+    packed = ops.kmeans_pack_points(X)
+    lab, mind = ops.kmeans_assign(X, C, packed=packed)
+    d = torch.cdist(X.double(), C.double()) ** 2
+    ref_min, ref_lab = d.min(1)
+    chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+    tol = 2e-6 * ((X.double() ** 2).sum(1) + (C.double() ** 2).sum(1).max())
+    assert torch.all(chosen - ref_min <= tol)
+    assert (lab.long() == ref_lab).float().mean() > 0.995
+    assert not torch.any(lab == k - 1)
+    assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-4 * f)
+
+
 @pytest.mark.parametrize("n,k,f", [(1000, 7, 3), (5000, 300, 32), (70000, 1024, 64), (3333, 100, 100),
                                    (777, 65, 128), (40000, 16, 18)])
 @pytest.mark.parametrize("data", ["normal", "near_centroids", "ties"])
