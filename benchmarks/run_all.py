@@ -14,14 +14,24 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-SUITE = {name: "benchmarks.{}.run".format(name)
-         for name in ("kmeans", "distance_matrix", "statistical_moments", "lasso", "linalg")}
+# name -> (module, extra arguments)
+SUITE = {
+    "kmeans": ("benchmarks.kmeans.run", []),
+    "kmeans_reference": ("benchmarks.kmeans.run", ["--case", "reference"]),   # k = 8, 30 iterations
+    "distance_matrix": ("benchmarks.distance_matrix.run", []),
+    "statistical_moments": ("benchmarks.statistical_moments.run", []),
+    "lasso": ("benchmarks.lasso.run", []),
+    "linalg": ("benchmarks.linalg.run", []),
+    "linalg_high": ("benchmarks.linalg.run", ["--precision", "high"]),       # fp16x3 split GEMM
+}
 QUICK = {
     "kmeans": ["--rows-per-gpu", "200000", "--trials", "2"],
+    "kmeans_reference": ["--rows-per-gpu", "200000", "--trials", "2"],
     "distance_matrix": ["--rows", "8000", "--trials", "2"],
     "statistical_moments": ["--rows-per-gpu", "10000", "--cols", "100", "--trials", "2"],
     "lasso": ["--rows", "100000", "--trials", "2"],
     "linalg": ["--rows-per-gpu", "20000", "--cols", "256", "--trials", "2"],
+    "linalg_high": ["--rows-per-gpu", "20000", "--cols", "256", "--trials", "2"],
 }
 
 
@@ -39,7 +49,8 @@ def main():
             for name in a.only.split(","):
                 port += 1
                 cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-                       "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", SUITE[name]]
+                       "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", SUITE[name][0]]
+                cmd += SUITE[name][1]
                 cmd += QUICK[name] if a.quick else []
                 print("#", " ".join(cmd), flush=True)
                 res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=a.timeout)

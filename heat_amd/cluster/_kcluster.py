@@ -39,14 +39,17 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         # "exact": bit-exact fp32 (f32-input MFMA) assignment
         self.precision = "fast"
         self._pack_cache = None
-        # certified one-term assignment (ops.kmeans_assign(certified=True)) while it pays: every
-        # certified call posts its re-check count to the host without a sync; once more than
-        # CERT_MAX_RECHECK of the points needed the 3-term re-run, the full kernel takes over
-        # until the points change
+        # certified one-term assignment (ops.kmeans_assign(certified=True)) while it pays: a
+        # certified call posts its re-check count to the host (pinned copy + event); the next call
+        # waits for that event (the previous iteration, normally finished) and decides. Once more
+        # than CERT_MAX_RECHECK of the points needed the 3-term re-run, the full kernel takes over
+        # until the points change; while it pays, it is re-checked every CERT_REPROBE calls.
         self._certify = True
         self._cert_probe = None
+        self._cert_calls = 0
 
     CERT_MAX_RECHECK = 0.25
+    CERT_REPROBE = 8
 
     def _assign_labels(self, X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
         """int32 nearest-centroid labels of the local points (native fused kernels)."""
@@ -54,12 +57,16 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         packed = self._packed(X) if X.dtype == torch.float32 and not ops.kernels._small_k_ok(X, C.shape[0]) \
             else None
         probe = self._cert_probe
-        if probe is not None and probe[1].query():
+        if probe is not None:
+            # an asynchronous fit loop runs ahead of the GPU: waiting here (for the previous
+            # iteration) is what makes the decision happen at all
+            probe[1].synchronize()
             self._certify = probe[0].item() <= self.CERT_MAX_RECHECK * probe[2]
             self._cert_probe = probe = None
         certified = packed is not None and self._certify
         labels, _ = ops.kmeans_assign(X, C, want_mind=False, packed=packed, certified=certified)
-        if certified and probe is None and X.shape[0] > 0:
+        self._cert_calls += 1
+        if certified and X.shape[0] > 0 and (self._cert_calls <= 2 or self._cert_calls % self.CERT_REPROBE == 0):
             host = torch.empty(1, dtype=torch.int32, pin_memory=True)
             host.copy_(ops.kernels.kmeans_assign.last_rechecked.reshape(1), non_blocking=True)  # unwrapped by profiling
             ev = torch.cuda.Event()
@@ -74,7 +81,7 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         key = ops.kernels._points_key(X)
         if self._pack_cache is None or self._pack_cache.key != key:
             self._pack_cache = None
-            self._certify, self._cert_probe = True, None
+            self._certify, self._cert_probe, self._cert_calls = True, None, 0
             self._pack_cache = ops.kmeans_pack_points(X)
         return self._pack_cache
 

@@ -19,6 +19,9 @@ run() {  # name timeout cmd...
   return $rc
 }
 run kmeans 300 python3 "$ROOT/bench.py" --steps 10 --warmup 2 &&
+run kmeans_reference 300 python3 -m benchmarks.kmeans.run --case reference --trials 2 &&
+run knn 300 python3 "$ROOT/tools/microbench/knn_bench.py" &&
+run linalg_high 400 python3 -m benchmarks.linalg.run --trials 1 --precision high &&
 run kmeans_exact 300 python3 -m benchmarks.kmeans.run --precision exact --trials 1 --iterations 5 &&
 run dist_susy 300 python3 -m benchmarks.distance_matrix.run --trials 3 &&
 run dist_tile 300 python3 "$ROOT/bench.py" --workload cdist --rows 262144 --steps 2 --warmup 1 &&
