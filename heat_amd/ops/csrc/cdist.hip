@@ -114,6 +114,10 @@ __global__ __launch_bounds__(256, 2) void cdist_l2(const float* __restrict__ X, 
 // ds_read_b128 per feature, the squared-difference accumulation runs on packed fp32
 // (v_pk_add_f32 / v_pk_fma_f32: two pairs per instruction) and the output rows leave as 16-byte
 // stores (16 lanes = 256 contiguous bytes).  XCD-banded tile order as in the MFMA kernels.
+// Measured alternative (SUSY 40k x 18): 128 x 128 tiles with 8 x 8 outputs per thread (x and y as
+// ds_read_b128, a quarter of the LDS cycles per output) ran 2.21 ms vs 2.25 ms, 1.80 ms with the
+// stores removed: the loop is VALU-bound (packed fp32 gives no issue-rate gain over 2 scalar ops
+// here), not LDS-bound, so the simpler 64 x 64 kernel stays.
 // OP 0: sum |x-y| ; OP 1: sqrt(sum (x-y)^2) ; OP 2: sum (x-y)^2 ; OP 3: exp(-scale * sum (x-y)^2)
 constexpr int LB = 64, LK = 32, LYS = LB + 4;
 typedef float floatx2 __attribute__((ext_vector_type(2)));
