@@ -34,6 +34,9 @@ def parse():
     p.add_argument("--rows", type=int, default=1_000_000, help="cdist: total rows (strong scaling)")
     p.add_argument("--k", type=int, default=1024)
     p.add_argument("--f", type=int, default=None, help="features (kmeans 64, cdist 128)")
+    p.add_argument("--precision", default="fast", choices=["fast", "exact"],
+                   help="kmeans: 'fast' = distances by a 3-term fp16 split on the matrix cores (fp32-GEMM "
+                        "accuracy, checked against fp64 in tests/test_gpu_kernels.py); 'exact' = fp32-input MFMA")
     p.add_argument("--with-reference", action="store_true",
                    help="also time a reference-style (heat 1.1 algorithm) iteration on torch-ROCm")
     return p.parse_args()
@@ -65,6 +68,7 @@ def main():
         ht.random.seed(1234)
         x = ht.random.randn(n, f, split=0, device=dev)
         km = ht.cluster.KMeans(n_clusters=k, init="random", max_iter=1, tol=None, random_state=42)
+        km.precision = args.precision
         for _ in range(args.warmup):
             km.step(x)
         sync()
@@ -81,9 +85,13 @@ def main():
         metric = "kmeans_iter_gflops"
         unit = "GFLOP/s"
         cfg = {"model": "kmeans k={} f={} float32 split=0 (assign+update+allreduce)".format(k, f),
+               "precision": args.precision,
                "global_batch": n, "seq_len": f, "parallelism": "dp{}".format(n_gpus), "k": k,
                "n_per_gpu": args.n_per_gpu}
         extra["iter_ms"] = ms
+        extra["precision"] = ("fp32 data and centroids; distance GEMM as a 3-term fp16 split with fp32 "
+                              "accumulation (fp32-GEMM accuracy)" if args.precision == "fast"
+                              else "fp32-input MFMA (exact fp32 products)")
         extra["tflops_per_gpu"] = value / n_gpus / 1e3
         if args.with_reference:
             extra["reference_impl_ms"] = reference_iteration(x, km, k)
