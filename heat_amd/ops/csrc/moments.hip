@@ -223,6 +223,22 @@ __global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int
     }
   }
   int64_t i = r0;
+  // 8 rows (128 B per thread) in flight: ~64-128 KB per CU at 2-4 workgroups per CU
+  if (VEC == 4) {
+    for (; i + 7 < r1; i += 8) {
+      floatx4 a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = *reinterpret_cast<const floatx4*>(x + (i + u) * ld + col0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = a[u][e] - K[e];
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
+    }
+  }
   for (; i + 3 < r1; i += 4) {
     if (VEC == 4) {
       floatx4 a[4];

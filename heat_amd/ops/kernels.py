@@ -334,7 +334,10 @@ def _moments_native(x: torch.Tensor, axis):
     elif outer == 1:
         ncols = inner
         col_blocks = max(1, (ncols + 1023) // 1024)
-        nchunks = max(1, min(65535, (8 * ncu + col_blocks - 1) // col_blocks, (red + 63) // 64))
+        # row chunks: ~2 workgroups per CU, 8 rows in flight per thread (1e6 x 1000, axis 0: 8 per
+        # CU 0.91 ms, 4 0.81 ms, 2 0.76 ms = 5.3 TB/s; fewer partials for the fp64 merge too)
+        cpc = int(os.environ.get("HEAT_MOM_COL_CHUNKS_PER_CU", "2"))
+        nchunks = max(1, min(65535, (cpc * ncu + col_blocks - 1) // col_blocks, (red + 63) // 64))
         part = torch.empty((nchunks, ncols, 3), dtype=torch.float64, device=x.device)
         check(L.ha_moments_cols(_ptr(x), red, ncols, ncols, nchunks, _ptr(part), s), "ha_moments_cols")
         N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 0)
