@@ -117,12 +117,87 @@ __global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x
   if (ty == 0 && c0 + tx < n) atomicAdd(&colsq[c0 + tx], sq);
 }
 
+// Narrow X (n <= 64 features, e.g. 16): one row per thread. A thread loads its whole row (16-byte
+// pieces when aligned, all issued before use) and writes feature j to xt[j][row]: consecutive
+// threads write consecutive rows, so every store instruction is 256 contiguous bytes. Column sums
+// of squares stay in registers over a grid-stride loop and leave with one atomic per (workgroup,
+// column). (The 64 x 64 tile kernel above keeps 3/4 of its lanes idle at n = 16: 1.03 ms at 1e7 x 16.)
+template <int NC, bool VEC>
+__global__ __launch_bounds__(256) void lasso_prepare_rows(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
+                                                          float* __restrict__ xt, int64_t ldxt,
+                                                          float* __restrict__ colsq) {
+  __shared__ float red[4][NC];
+  float sq[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) sq[j] = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256) {
+    float v[NC];
+    const float* xr = x + r * ldx;
+    if (VEC) {
+#pragma unroll
+      for (int q = 0; q < NC / 4; ++q) {
+        floatx4 p = {0.f, 0.f, 0.f, 0.f};
+        if (4 * q < n) p = *reinterpret_cast<const floatx4*>(xr + 4 * q);
+        v[4 * q] = p[0];
+        v[4 * q + 1] = p[1];
+        v[4 * q + 2] = p[2];
+        v[4 * q + 3] = p[3];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) v[j] = j < n ? xr[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (j < n) xt[(int64_t)j * ldxt + r] = v[j];
+      sq[j] = fmaf(v[j], v[j], sq[j]);
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const float s = ha_wave_sum(sq[j]);
+    if (lane == 0) red[wave][j] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < n) {
+    const int j = threadIdx.x;
+    atomicAdd(&colsq[j], (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]));
+  }
+}
+
 }  // namespace
 
 HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, float* xt, int64_t ldxt, float* colsq,
                                void* stream) {
   if (m <= 0 || n <= 0) return HA_OK;
   hipMemsetAsync(colsq, 0, sizeof(float) * (size_t)n, (hipStream_t)stream);
+  if (n <= 64) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+    int64_t blocks = (m + 255) / 256;
+    if (blocks > 8LL * ncu) blocks = 8LL * ncu;
+    const bool vec = n % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
+    hipStream_t s = (hipStream_t)stream;
+#define HA_LP(NC)                                                                                           \
+  if (vec)                                                                                                  \
+    hipLaunchKernelGGL((lasso_prepare_rows<NC, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, m, n, ldx, xt, \
+                       ldxt, colsq);                                                                        \
+  else                                                                                                      \
+    hipLaunchKernelGGL((lasso_prepare_rows<NC, false>), dim3((unsigned)blocks), dim3(256), 0, s, x, m, n, ldx, xt, \
+                       ldxt, colsq);
+    if (n <= 16) {
+      HA_LP(16)
+    } else if (n <= 32) {
+      HA_LP(32)
+    } else {
+      HA_LP(64)
+    }
+#undef HA_LP
+    return ha_launch_status();
+  }
   const int64_t gx = (m + 255) / 256;
   if (gx > 0x7fffffffLL || (n + 63) / 64 > 65535) return HA_UNSUPPORTED;
   hipLaunchKernelGGL(lasso_prepare, dim3((unsigned)gx, (unsigned)((n + 63) / 64)), dim3(256), 0, (hipStream_t)stream,

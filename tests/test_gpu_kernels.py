@@ -294,7 +294,7 @@ def test_kmeans_fit_gpu(gpu):
     assert km.labels_.shape == (2000, 1)
 
 
-@pytest.mark.parametrize("m,n", [(1000, 3), (70001, 16), (513, 130)])
+@pytest.mark.parametrize("m,n", [(1000, 3), (70001, 16), (513, 130), (300001, 20), (4097, 64), (100, 33)])
 def test_lasso_prepare(m, n):
     from heat_amd import ops
 
