@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import factories, types
+from . import _sample_sort
 from .communication import MPI
 from .dndarray import DNDarray, _chunk_counts, _partition_bounds
 from .stride_tricks import broadcast_shape, sanitize_axis, sanitize_shape
@@ -811,52 +812,6 @@ def dsplit(x: DNDarray, indices_or_sections) -> List[DNDarray]:
 # ---------------------------------------------------------------------------------------------
 # sorting, selection, uniqueness
 # ---------------------------------------------------------------------------------------------
-def _sort_1d_distributed(v: torch.Tensor, gidx: torch.Tensor, comm, n_total: int):
-    """Parallel sort by regular sampling of one column. Returns (values, global indices) of this
-    rank's balanced block of the globally sorted sequence."""
-    p, me = comm.size, comm.rank
-    vals, order = torch.sort(v, stable=True)
-    idx = gidx[order]
-    nloc = vals.numel()
-    # p-1 regular samples per rank (padded with +inf-like duplicates when short)
-    if nloc:
-        pos = (torch.arange(1, p, device=vals.device) * nloc) // p
-        samples = vals[pos.clamp(max=nloc - 1)]
-    else:
-        samples = vals.new_empty(0)
-    all_samples = comm.allgather_tensor(samples, 0)
-    all_samples, _ = torch.sort(all_samples)
-    m = all_samples.numel()
-    if m >= p - 1 and m > 0:
-        pick = (torch.arange(1, p, device=vals.device) * m) // p
-        pivots = all_samples[pick.clamp(max=m - 1)]
-    else:
-        pivots = all_samples
-    cuts = torch.searchsorted(vals, pivots, right=True).tolist() if pivots.numel() else []
-    edges = [0] + [int(c) for c in cuts] + [nloc]
-    edges = edges + [nloc] * (p + 1 - len(edges))
-    send_counts = [edges[i + 1] - edges[i] for i in range(p)]
-    all_counts = comm.allgather_tensor(torch.tensor(send_counts, dtype=torch.int64,
-                                                    device=comm._small_device()).unsqueeze(0), 0).cpu()
-    recv_counts = [int(all_counts[r, me]) for r in range(p)]
-    vb = [vals[edges[q]: edges[q + 1]] for q in range(p)]
-    ib = [idx[edges[q]: edges[q + 1]] for q in range(p)]
-    rv = comm.exchange(vb, [(c,) for c in recv_counts])
-    ri = comm.exchange(ib, [(c,) for c in recv_counts])
-    mv = torch.cat(rv)
-    mi = torch.cat(ri)
-    mv, o = torch.sort(mv, stable=True)
-    mi = mi[o]
-    # rebalance: rank r holds globally sorted positions [prefix_r, prefix_r + n_r)
-    held = [int(all_counts[:, q].sum()) for q in range(p)]
-    starts = np.concatenate(([0], np.cumsum(held[:-1])))
-    segs = [[(int(starts[r]), 0, held[r])] if held[r] else [] for r in range(p)]
-    tgt = _chunk_counts(n_total, p)
-    mv = _segment_exchange(mv, 0, comm, segs, tgt)
-    mi = _segment_exchange(mi, 0, comm, segs, tgt)
-    return mv, mi
-
-
 def _desc_key(col: torch.Tensor) -> torch.Tensor:
     """Order-reversing involution used to sort descending with an ascending sort."""
     if col.dtype == torch.bool:
@@ -886,25 +841,23 @@ def sort(a: DNDarray, axis: int = -1, descending: bool = False, out: Optional[DN
         return v, i
     t = a.larray.movedim(axis, -1)
     lead = tuple(t.shape[:-1])
-    cols = t.reshape(-1, t.shape[-1])
     counts, displs = a.counts_displs()
     me = a.comm.rank
     gidx = torch.arange(displs[me], displs[me] + counts[me], device=t.device, dtype=torch.int64)
     # the number of columns is the same on every rank (product of the non-split dims)
     ncols = int(np.prod([s for i, s in enumerate(a.gshape) if i != axis])) if a.ndim > 1 else 1
-    outs_v, outs_i = [], []
+    cols = t.reshape(ncols, t.shape[-1])
+    if cols.dtype == torch.bool:
+        cols = cols.to(torch.uint8)
     n = a.gshape[axis]
-    for c in range(ncols):
-        col = cols[c] if cols.shape[0] else t.new_empty(0)
-        key = _desc_key(col) if descending else col
-        mv, mi = _sort_1d_distributed(key, gidx, a.comm, n)
-        if descending:
-            mv = _desc_key(mv)  # the order-reversing maps below are involutions
-        outs_v.append(mv)
-        outs_i.append(mi)
     nloc = _chunk_counts(n, a.comm.size)[me]
-    v = torch.stack(outs_v) if outs_v else t.new_empty((0, nloc))
-    i = torch.stack(outs_i) if outs_i else torch.empty((0, nloc), dtype=torch.int64, device=t.device)
+    if ncols and n:
+        # all columns in one batched sample sort (the order-reversing keys are involutions)
+        v, i = _sample_sort.sort_columns(_desc_key(cols) if descending else cols, gidx, a.comm, n)
+        v = _desc_key(v) if descending else v
+    else:
+        v = cols.new_empty((ncols, nloc))
+        i = torch.empty((ncols, nloc), dtype=torch.int64, device=t.device)
     v = v.reshape(lead + (nloc,)).movedim(-1, axis).contiguous()
     i = i.reshape(lead + (nloc,)).movedim(-1, axis).contiguous()
     vd = DNDarray(v.to(a.larray.dtype), a.gshape, a.dtype, a.split, a.device, a.comm, True)

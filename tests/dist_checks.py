@@ -853,6 +853,37 @@ def check_manipulations_more():
         assert_array_equal(h, np.histogram(ints, bins=7, range=(0, 7))[0].astype(np.float32))
 
 
+def check_sort_batched():
+    """Sample sort of many columns at once along every split axis: values, stable global indices
+    (ties), descending order, integer / bool keys and ranks without rows; median/percentile."""
+    rng = _rng(33)
+    a = rng.integers(0, 5, size=(7, 3, 11)).astype(np.int64)  # many ties
+    f = rng.normal(size=(7, 3, 11)).astype(np.float32)
+    for split in for_splits(a):
+        for axis in range(3):
+            x = ht.array(a, split=split)
+            v, i = ht.sort(x, axis=axis)
+            assert_array_equal(v, np.sort(a, axis=axis, kind="stable"))
+            assert_array_equal(i, np.argsort(a, axis=axis, kind="stable"))
+            v, i = ht.sort(x, axis=axis, descending=True)
+            assert_array_equal(v, -np.sort(-a, axis=axis, kind="stable"))
+            assert_array_equal(i, np.argsort(-a, axis=axis, kind="stable"))
+            y = ht.array(f, split=split)
+            v, i = ht.sort(y, axis=axis, descending=True)
+            assert_array_equal(v, -np.sort(-f, axis=axis))
+            assert_array_equal(ht.median(y, axis=axis), np.median(f, axis=axis), check_split_chunks=False)
+            assert_array_equal(ht.percentile(y, [10.0, 75.0], axis=axis),
+                               np.percentile(f, [10.0, 75.0], axis=axis), check_split_chunks=False)
+        b = ht.array(a > 2, split=split)
+        v, i = ht.sort(b, axis=0)
+        assert_array_equal(v, np.sort(a > 2, axis=0, kind="stable"))
+        assert_array_equal(i, np.argsort(a > 2, axis=0, kind="stable"))
+    short = rng.normal(size=(2, 4)).astype(np.float32)  # fewer rows than ranks (p = 3)
+    v, i = ht.sort(ht.array(short, split=0), axis=0)
+    assert_array_equal(v, np.sort(short, axis=0))
+    assert_array_equal(i, np.argsort(short, axis=0, kind="stable"))
+
+
 def check_printing():
     """``str(DNDarray)`` matches the reference's format (printed on rank 0 only)."""
     import math
