@@ -342,8 +342,26 @@ class MPICommunication(Communication):
             acc = op.fold(acc, stacked[r])
         return acc
 
+    def _ipc_allreduce(self, t: torch.Tensor):
+        """The one-shot xGMI all-reduce (``parallel/ipc.py``) for small device SUMs when enabled
+        (``HEAT_IPC_ALLREDUCE=1``) on a node-local world communicator; None where it does not apply.
+        The decision depends only on SPMD-identical facts, so every rank takes the same path."""
+        from ..parallel import ipc
+
+        if not (ipc.enabled() and t.is_cuda and self.group is None and t.is_contiguous()
+                and t.dtype in (torch.float32, torch.float64, torch.int64)
+                and t.numel() * t.element_size() <= ipc.max_bytes()
+                and int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == dist.get_world_size() == self.size):
+            return None
+        ar = getattr(self, "_ipc", None)
+        if ar is None:
+            ar = self._ipc = ipc.IpcAllreduce(self, capacity_bytes=ipc.max_bytes())
+        return ar.allreduce_(t)
+
     def _reduce_tensor_async(self, t: torch.Tensor, op: Op):
         """All-reduce ``t`` in place (returns (work, finalize))."""
+        if op is MPI.SUM and self._ipc_allreduce(t) is not None:
+            return None, None  # stream-ordered on the current stream: nothing to wait for
         native = op.torch_op is not None and t.dtype != torch.bool and (not t.is_complex() or op is MPI.SUM)
         if native:
             contig = t if t.is_contiguous() else t.contiguous()

@@ -1,0 +1,153 @@
+// One-shot intra-node all-reduce over peer (xGMI) mappings of hipIpc-shared buffers (SURVEY N2:
+// the small-message path for the k-means k*f+k sums, moment triples, argmin packs and metadata
+// maps, where RCCL's ring/tree start-up dominates).
+//
+// Every rank owns one data buffer (two slots, alternating by call parity) and one signal buffer,
+// both exported with hipIpcGetMemHandle and mapped by every peer. One call = one kernel:
+//   block b copies its slice S_b of the input into its own slot, releases at system scope and
+//   writes the call's epoch into slot [b][rank] of every peer's signal buffer; it then waits until
+//   all peers' epochs for block b have arrived in its own signal buffer, acquires, and sums S_b of
+//   every rank's slot in rank order (bitwise identical results on all ranks) into the output.
+// The barrier is per block, so a block only waits for the peers' copies of ITS slice: no grid-wide
+// synchronisation and no dependence on which blocks are co-resident. Slot reuse is safe with two
+// slots: a rank writes a slot again two calls later, after a barrier for which every peer's block b
+// already finished reading it (kernels of one stream are ordered). Epochs only grow, and waits use
+// ">=", so a fast peer announcing the next epoch cannot starve a slow waiter.
+// Spins are bounded: on timeout the block records an error word in its own signal buffer and
+// continues (wrong sums, no hang); callers check it.
+#include "common.h"
+
+#include <cstring>
+
+namespace {
+
+constexpr int IPC_MAX_RANKS = 8;
+constexpr int IPC_MAX_BLOCKS = 64;
+constexpr int IPC_ERR_WORD = IPC_MAX_BLOCKS * IPC_MAX_RANKS;  // uint32 index of the error word
+
+struct PeerPtrs {
+  void* data[IPC_MAX_RANKS];
+  unsigned* sig[IPC_MAX_RANKS];
+};
+
+template <typename T, int W>
+__global__ __launch_bounds__(256) void ipc_allreduce(PeerPtrs pp, int rank, T* __restrict__ buf, int64_t n,
+                                                     int64_t chunk, int64_t slot_off, unsigned epoch,
+                                                     int64_t max_spins) {
+  const int b = blockIdx.x;
+  const int64_t lo = (int64_t)b * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  T* mine = reinterpret_cast<T*>(pp.data[rank]) + slot_off;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = buf[i];
+  __syncthreads();
+  if (threadIdx.x < W) {
+    // publish this block's slice, then announce it to peer threadIdx.x
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(pp.sig[threadIdx.x] + b * IPC_MAX_RANKS + rank, epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* flag = pp.sig[rank] + b * IPC_MAX_RANKS + threadIdx.x;
+    int64_t spins = 0;
+    while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (++spins > max_spins) {
+        __hip_atomic_store(pp.sig[rank] + IPC_ERR_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  const T* src[W];
+#pragma unroll
+  for (int r = 0; r < W; ++r) src[r] = reinterpret_cast<const T*>(pp.data[r]) + slot_off;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    T v[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) v[r] = src[r][i];  // all loads in flight before the sum
+    T s = v[0];
+#pragma unroll
+    for (int r = 1; r < W; ++r) s += v[r];
+    buf[i] = s;
+  }
+}
+
+template <typename T>
+int launch(const PeerPtrs& pp, int world, int rank, T* buf, int64_t n, int64_t slot_off, unsigned epoch,
+           int blocks, int64_t max_spins, hipStream_t s) {
+  const int64_t chunk = (n + blocks - 1) / blocks;
+  const int grid = (int)((n + chunk - 1) / chunk);
+#define HA_IPC(WN)                                                                                          \
+  case WN:                                                                                                  \
+    hipLaunchKernelGGL((ipc_allreduce<T, WN>), dim3(grid), dim3(256), 0, s, pp, rank, buf, n, chunk, slot_off, \
+                       epoch, max_spins);                                                                   \
+    break;
+  switch (world) {
+    HA_IPC(2) HA_IPC(3) HA_IPC(4) HA_IPC(5) HA_IPC(6) HA_IPC(7) HA_IPC(8)
+    default: return HA_UNSUPPORTED;
+  }
+#undef HA_IPC
+  return ha_launch_status();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------ C ABI
+HA_EXPORT int ha_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+HA_EXPORT int ha_ipc_max_ranks() { return IPC_MAX_RANKS; }
+HA_EXPORT int ha_ipc_max_blocks() { return IPC_MAX_BLOCKS; }
+HA_EXPORT int64_t ha_ipc_signal_bytes() { return (int64_t)(IPC_ERR_WORD + 64) * 4; }
+
+// Allocate an exportable device buffer (uncached when ``signal``, zero-filled) and its IPC handle.
+HA_EXPORT int ha_ipc_alloc(int64_t bytes, int signal, void** ptr, void* handle) {
+  if (bytes <= 0 || !ptr || !handle) return HA_BAD_ARG;
+  hipError_t e = signal ? hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached)
+                        : hipMalloc(ptr, (size_t)bytes);
+  if (e != hipSuccess && signal) e = hipMalloc(ptr, (size_t)bytes);
+  if (e != hipSuccess) return HA_LAUNCH;
+  if (hipMemset(*ptr, 0, (size_t)bytes) != hipSuccess) return HA_LAUNCH;
+  if (hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), *ptr) != hipSuccess) return HA_LAUNCH;
+  return HA_OK;
+}
+
+HA_EXPORT int ha_ipc_free(void* ptr) { return hipFree(ptr) == hipSuccess ? HA_OK : HA_LAUNCH; }
+
+HA_EXPORT int ha_ipc_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess ? HA_OK : HA_LAUNCH;
+}
+
+HA_EXPORT int ha_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? HA_OK : HA_LAUNCH; }
+
+// In-place SUM of ``buf`` (n elements, dtype 0 = float32, 1 = float64, 2 = int64) over ``world``
+// ranks. data/sig: the world's mapped buffer pointers (own ones included), slot_elems: elements
+// per slot; ``epoch`` must grow by one per call on every rank.
+HA_EXPORT int ha_ipc_allreduce(void* const* data, void* const* sig, int world, int rank, void* buf, int64_t n,
+                               int dtype, int64_t slot_elems, unsigned epoch, int blocks, int64_t max_spins,
+                               void* stream) {
+  if (world < 2 || world > IPC_MAX_RANKS || rank < 0 || rank >= world || n < 0 || n > slot_elems) return HA_BAD_ARG;
+  if (n == 0) return HA_OK;
+  blocks = blocks < 1 ? 1 : blocks > IPC_MAX_BLOCKS ? IPC_MAX_BLOCKS : blocks;
+  PeerPtrs pp{};
+  for (int r = 0; r < world; ++r) {
+    pp.data[r] = data[r];
+    pp.sig[r] = reinterpret_cast<unsigned*>(sig[r]);
+  }
+  const int64_t slot_off = (epoch & 1u) ? slot_elems : 0;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return launch<float>(pp, world, rank, (float*)buf, n, slot_off, epoch, blocks, max_spins, s);
+    case 1: return launch<double>(pp, world, rank, (double*)buf, n, slot_off, epoch, blocks, max_spins, s);
+    case 2: return launch<int64_t>(pp, world, rank, (int64_t*)buf, n, slot_off, epoch, blocks, max_spins, s);
+    default: return HA_UNSUPPORTED;
+  }
+}
+
+// Error word of this rank's signal buffer (1 after a barrier timed out); reset with clear != 0.
+HA_EXPORT int ha_ipc_error(void* sig, int clear) {
+  unsigned v = 0;
+  unsigned* w = reinterpret_cast<unsigned*>(sig) + IPC_ERR_WORD;
+  if (hipMemcpy(&v, w, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (clear && hipMemset(w, 0, 4) != hipSuccess) return -1;
+  return (int)v;
+}

@@ -22,15 +22,18 @@ def _free_port() -> int:
     return port
 
 
-def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None):
+def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None, keep_gpu: bool = False):
+    """``keep_gpu``: the ranks keep the visible GPU(s) (several ranks may share one device; the
+    control plane stays gloo)."""
     port = _free_port()
     procs = []
     for r in range(nprocs):
         env = dict(os.environ)
         env.update({"RANK": str(r), "WORLD_SIZE": str(nprocs), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(nprocs),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HEAT_COMM_BACKEND": "gloo",
-                    "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1",
-                    "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+                    "OMP_NUM_THREADS": "1", "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        if not keep_gpu:
+            env.update({"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
         if env_extra:
             env.update(env_extra)
         procs.append(subprocess.Popen([sys.executable, "-m", "tests._dist_runner", target], cwd=ROOT, env=env,

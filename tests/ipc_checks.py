@@ -1,0 +1,73 @@
+"""
+Rank bodies of the IPC all-reduce GPU test (``tests/test_gpu_ipc.py``): N processes share the
+box's one MI355X, exchange hipIpc handles over gloo and all-reduce through the mapped buffers.
+Every rank builds every rank's input from the same seed, so the exact expected sum (same
+rank-order fp summation as the kernel) is known locally.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+import heat_amd as ht
+from heat_amd.parallel.ipc import IpcAllreduce
+
+
+def _inputs(it: int, n: int, p: int, dtype):
+    g = torch.Generator().manual_seed(7919 * it + n)
+    full = torch.randn(p, n, generator=g, dtype=torch.float64)
+    if dtype == torch.int64:
+        full = (full * 1000).round()
+    full = full.to(dtype)
+    ref = full[0].clone()
+    for q in range(1, p):
+        ref += full[q]
+    return full, ref
+
+
+def check_ipc_allreduce():
+    comm = ht.MPI_WORLD
+    p, r = comm.size, comm.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ar = IpcAllreduce(comm, capacity_bytes=1 << 20, blocks=16, timeout_spins=2_000_000)
+    cases = ((torch.float32, 1), (torch.float32, 1000), (torch.float64, 66560), (torch.int64, 777),
+             (torch.float32, 262144), (torch.float64, 3))
+    for it in range(20):
+        for dtype, n in cases:
+            full, ref = _inputs(it, n, p, dtype)
+            t = full[r].clone().to(dev)
+            ar.allreduce_(t)
+            got = t.cpu()
+            assert torch.equal(got, ref), (it, dtype, n, (got.double() - ref.double()).abs().max().item())
+    # back-to-back calls without host synchronisation (slot reuse + epoch ordering)
+    ts = []
+    for it in range(50):
+        full, ref = _inputs(100 + it, 4096, p, torch.float32)
+        t = full[r].clone().to(dev)
+        ar.allreduce_(t)
+        ts.append((t, ref))
+    for t, ref in ts:
+        assert torch.equal(t.cpu(), ref)
+    assert ar.error() == 0, "an IPC barrier timed out"
+    ar.close()
+
+
+def check_ipc_through_communication():
+    """``MPICommunication.Allreduce`` routes small device SUMs through the IPC kernel when
+    HEAT_IPC_ALLREDUCE=1 (set by the test); results equal the rank-order sum."""
+    assert os.environ.get("HEAT_IPC_ALLREDUCE") == "1"
+    comm = ht.MPI_WORLD
+    p, r = comm.size, comm.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    for it in range(5):
+        full, ref = _inputs(500 + it, 1024 * 65 + 1024, p, torch.float64)
+        t = full[r].clone().to(dev)
+        comm.Allreduce(ht.MPI.IN_PLACE, t, ht.MPI.SUM)
+        assert torch.equal(t.cpu(), ref)
+    assert getattr(comm, "_ipc", None) is not None, "the IPC path was not taken"
+    # a distributed reduction of the op engine (sum over the split axis) on the device
+    x = ht.arange(4000, dtype=ht.float64, split=0, device="gpu")
+    assert x.larray.is_cuda
+    assert ht.sum(x).item() == 4000 * 3999 / 2
+    assert comm._ipc.error() == 0

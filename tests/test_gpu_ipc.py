@@ -1,0 +1,17 @@
+"""One-shot IPC all-reduce kernel (``ops/csrc/ipc_allreduce.hip``) with 2 and 3 processes sharing
+the box's GPU: handle exchange, per-block epoch barriers, slot reuse, bitwise rank-order sums."""
+import pytest
+
+from ._dist import run_distributed
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nprocs", [2, 3])
+def test_ipc_allreduce(gpu, nprocs):
+    run_distributed("tests.ipc_checks:check_ipc_allreduce", nprocs, timeout=110, keep_gpu=True)
+
+
+def test_ipc_through_communication(gpu):
+    run_distributed("tests.ipc_checks:check_ipc_through_communication", 2, timeout=110, keep_gpu=True,
+                    env_extra={"HEAT_IPC_ALLREDUCE": "1"})
