@@ -5,6 +5,7 @@ size is 1e7 rows (eurad); the feature count of that file is not in the repositor
 parameter (default 16).
 """
 import argparse
+import os
 
 from benchmarks import common  # noqa: F401
 from benchmarks.common import ht, report, setup, timed
@@ -27,7 +28,8 @@ def main():
         ht.regression.Lasso(lam=0.1, max_iter=a.iterations, tol=-1.0).fit(x, y)
 
     t = timed(fit, a.trials)
-    report("lasso", {"rows": a.rows, "features": a.features, "iterations": a.iterations}, t,
+    report("lasso", {"rows": a.rows, "features": a.features, "iterations": a.iterations,
+                     "solver": os.environ.get("HEAT_LASSO_SOLVER", "auto")}, t,
            {"GB_per_s": 4.0 * a.rows * a.features * 2 * a.iterations / 1e9})
 
 

@@ -14,7 +14,7 @@ import torch.nn.functional as F
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes", "knn_topk", "kmeans_step_small"]
+           "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd"]
 
 _NUM_CUS = {}
 
@@ -479,6 +479,81 @@ def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: fl
 
 
 # --------------------------------------------------------------------------------------------- lasso
+def lasso_gram(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Unnormalised augmented Gram matrix [X | y]^T [X | y] of the local rows, float64
+    [(n+1), (n+1)] (``csrc/lasso_gram.hip``: one pass, register accumulators, fp64 block partials).
+
+    Device fp32 with n + 1 <= 24 columns: the native kernel. Otherwise row blocks of fp32 GEMMs
+    accumulated in fp64 (host tensors: fp64 GEMM)."""
+    m, n = X.shape
+    dev = X.device
+    if m == 0:
+        return torch.zeros((n + 1, n + 1), dtype=torch.float64, device=dev)
+    if use_native(X) and X.dtype == torch.float32 and n + 1 <= lib().ha_lasso_gram_max_cols():
+        L = lib()
+        Xc = X if X.stride(-1) == 1 else X.contiguous()
+        yc = y.reshape(-1).to(torch.float32).contiguous()
+        blocks = L.ha_lasso_gram_blocks(m, num_cus(dev))
+        nc = n + 1
+        T = nc * (nc + 1) // 2
+        part = torch.empty((blocks, T), dtype=torch.float64, device=dev)
+        check(L.ha_lasso_gram(_ptr(Xc), m, n, Xc.stride(0), _ptr(yc), _ptr(part), blocks,
+                              ctypes.c_void_p(stream_ptr(dev))), "ha_lasso_gram")
+        tri = part.sum(0)
+        iu = torch.triu_indices(nc, nc, device=dev)
+        G = torch.zeros((nc, nc), dtype=torch.float64, device=dev)
+        G[iu[0], iu[1]] = tri
+        return G + torch.triu(G, 1).T
+    A = torch.cat([X, y.reshape(-1, 1).to(X.dtype)], dim=1)
+    if not A.is_cuda:
+        A = A.double()
+        return A.T @ A
+    G = torch.zeros((n + 1, n + 1), dtype=torch.float64, device=dev)
+    step = max(1, (1 << 20))
+    for r0 in range(0, m, step):
+        blk = A[r0: r0 + step].float()
+        G += (blk.T @ blk).double()
+    return G
+
+
+def lasso_cd(G: torch.Tensor, b: torch.Tensor, lam: float, max_iter: int, tol: Optional[float],
+             theta: torch.Tensor) -> int:
+    """Cyclic coordinate descent on the normal equations (``G`` = X^T X / m, ``b`` = X^T y / m,
+    float64), updating ``theta`` (float64, start values) in place with the reference's rule
+    (feature 0 = intercept, not thresholded); sweeps stop when the RMS change of theta drops
+    below ``tol``. Device: ONE single-wavefront kernel runs every sweep. Returns the sweep count."""
+    n = G.shape[0]
+    t = -1.0 if tol is None else float(tol)
+    if use_native(G) and n <= 2048:
+        L = lib()
+        Gc = G if G.stride(-1) == 1 else G.contiguous()
+        bc = b.contiguous()
+        it = torch.zeros(1, dtype=torch.int32, device=G.device)
+        check(L.ha_lasso_cd(_ptr(Gc), n, Gc.stride(0), _ptr(bc), ctypes.c_double(lam), int(max_iter),
+                            ctypes.c_double(t), _ptr(theta), _ptr(it), ctypes.c_void_p(stream_ptr(G.device))),
+              "ha_lasso_cd")
+        return int(it.item())
+    import numpy as np
+
+    g = G.detach().cpu().numpy()
+    bb = b.detach().cpu().numpy()
+    th = theta.detach().cpu().numpy().astype(np.float64).copy()
+    it = 0
+    while it < max_iter:
+        it += 1
+        d2 = 0.0
+        for j in range(n):
+            old = th[j]
+            rho = bb[j] - float(g[j] @ th) + g[j, j] * old
+            nw = rho if j == 0 else (rho + lam if rho < -lam else (rho - lam if rho > lam else 0.0))
+            th[j] = nw
+            d2 += (nw - old) ** 2
+        if t >= 0 and (d2 / n) ** 0.5 < t:
+            break
+    theta.copy_(torch.from_numpy(th))
+    return it
+
+
 def lasso_prepare(X: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """(X^T contiguous [n, m], sum of squares per column [n]) in one pass over X."""
     m, n = X.shape

@@ -5,9 +5,17 @@ Lasso regression by cyclic coordinate descent (reference ``heat/regression/lasso
 Same objective, same update rule (feature 0 is the intercept column and is not thresholded), but
 O(m n) per sweep instead of O(m n^2): the residual stays on the device and every coordinate is
 one fused native pass (``ops.lasso_epoch``) plus, for split data, one scalar all-reduce.
+
+Narrow problems (n <= 64 features, the tall-skinny regime the reference benchmarks) take the
+covariance form of the same update: rho_j = b_j - (G theta)_j + G_jj theta_j with G = X^T X / m,
+b = X^T y / m. One native pass over the rows builds [X | y]^T [X | y] (``ops.lasso_gram``), split
+data needs ONE fp64 all-reduce of that (n+1)^2 matrix per fit, and every sweep plus the convergence
+test runs in one single-wavefront kernel (``ops.lasso_cd``). ``HEAT_LASSO_SOLVER=sweep|gram``
+forces either form.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Union
 
 import torch
@@ -86,6 +94,18 @@ class Lasso(RegressionMixin, BaseEstimator):
             r0 = displs[x.comm.rank]
             yl = yl[r0: r0 + counts[x.comm.rank]]
         dist = x.is_distributed()
+        solver = os.environ.get("HEAT_LASSO_SOLVER", "auto")
+        if solver == "gram" or (solver == "auto" and n <= 64):
+            G = ops.lasso_gram(X, yl)                         # [n+1, n+1] fp64, local rows
+            if dist:
+                x.comm.Allreduce(MPI.IN_PLACE, G, MPI.SUM)
+            G = G / m
+            th = torch.zeros(n, dtype=torch.float64, device=X.device)
+            it = ops.lasso_cd(G[:n, :n], G[:n, n].contiguous(), float(self.__lam), int(self.max_iter), self.tol, th)
+            self.n_iter = it
+            self.__theta = DNDarray(th.to(tt).reshape(n, 1), (n, 1), ht.types.canonical_heat_type(tt), None, x.device,
+                                    x.comm, True)
+            return
         XT, colsq = ops.lasso_prepare(X)                       # [n, m_local]: features contiguous
         if dist:
             x.comm.Allreduce(MPI.IN_PLACE, colsq, MPI.SUM)

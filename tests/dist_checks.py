@@ -6,6 +6,7 @@ reference's ``assert_func_equal`` strategy, ``heat/core/tests/test_suites/basic_
 """
 from __future__ import annotations
 
+import os
 import numpy as np
 import torch
 
@@ -348,14 +349,23 @@ def check_lasso():
     w = np.array([0.5, 2.0, 0.0, -1.5, 0.0, 0.7], np.float32)
     y = (X @ w + 0.01 * rng.normal(size=m)).astype(np.float32)
     thetas = []
-    for split in (None, 0):
-        est = ht.regression.Lasso(lam=0.01, max_iter=200, tol=1e-7)
-        est.fit(ht.array(X, split=split), ht.array(y[:, None], split=split))
+    prev = os.environ.get("HEAT_LASSO_SOLVER")
+    for split, solver in ((None, "sweep"), (0, "sweep"), (None, "gram"), (0, "gram")):
+        os.environ["HEAT_LASSO_SOLVER"] = solver
+        try:
+            est = ht.regression.Lasso(lam=0.01, max_iter=200, tol=1e-7)
+            est.fit(ht.array(X, split=split), ht.array(y[:, None], split=split))
+        finally:
+            if prev is None:
+                os.environ.pop("HEAT_LASSO_SOLVER", None)
+            else:
+                os.environ["HEAT_LASSO_SOLVER"] = prev
         th = est.theta.numpy().ravel()
         thetas.append(th)
         pred = est.predict(ht.array(X, split=split)).numpy().ravel()
         assert np.sqrt(np.mean((pred - y) ** 2)) < 0.05
-    assert np.allclose(thetas[0], thetas[1], atol=1e-4)
+    for t in thetas[1:]:
+        assert np.allclose(thetas[0], t, atol=1e-4)
     assert abs(thetas[0][2]) < 0.02 and abs(thetas[0][4]) < 0.02       # sparsity of the zero weights
     assert np.allclose(thetas[0], w, atol=0.05)
 

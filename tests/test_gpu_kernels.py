@@ -305,6 +305,56 @@ def test_lasso_prepare(m, n):
     assert torch.allclose(colsq.double(), (X.double() ** 2).sum(0), rtol=1e-5)
 
 
+@pytest.mark.parametrize("m,n", [(1, 1), (1000, 3), (70001, 16), (300001, 23), (4097, 7), (100, 40)])
+def test_lasso_gram_matches_fp64(gpu, m, n):
+    from heat_amd import ops
+
+    g = torch.Generator().manual_seed(m + n)
+    X = torch.randn(m, n, generator=g)
+    y = torch.randn(m, generator=g)
+    G = ops.lasso_gram(X.cuda(), y.cuda()).cpu()
+    A = torch.cat([X, y[:, None]], 1).double()
+    ref = A.T @ A
+    assert torch.allclose(G, ref, rtol=1e-5, atol=1e-6 * m), (G - ref).abs().max()
+
+
+@pytest.mark.parametrize("n", [5, 64, 130])
+@pytest.mark.parametrize("tol", [None, 1e-6])
+def test_lasso_cd_device_matches_host(gpu, n, tol):
+    from heat_amd import ops
+
+    g = torch.Generator().manual_seed(n)
+    X = torch.randn(4 * n + 50, n, generator=g, dtype=torch.float64)
+    X /= X.pow(2).mean(0).sqrt()
+    y = X @ torch.randn(n, generator=g, dtype=torch.float64)
+    G = torch.cat([X, y[:, None]], 1)
+    G = G.T @ G / X.shape[0]
+    res = []
+    for dev in ("cpu", "cuda"):
+        Gd = G.to(dev)
+        th = torch.zeros(n, dtype=torch.float64, device=dev)
+        it = ops.lasso_cd(Gd[:n, :n], Gd[:n, n].contiguous(), 0.02, 25, tol, th)
+        res.append((it, th.cpu()))
+    assert res[0][0] == res[1][0]
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-9)
+
+
+def test_lasso_gram_solver_matches_sweep(gpu, monkeypatch):
+    import heat_amd as ht
+
+    ht.random.seed(5)
+    x = ht.random.randn(50000, 16)
+    x = x / ht.sqrt(ht.mean(x ** 2, axis=0))
+    y = ht.matmul(x, ht.random.randn(16, 1)) + 0.05 * ht.random.randn(50000, 1)
+    res = []
+    for solver in ("sweep", "gram"):
+        monkeypatch.setenv("HEAT_LASSO_SOLVER", solver)
+        est = ht.regression.Lasso(lam=0.01, max_iter=30, tol=None)
+        est.fit(x, y)
+        res.append(est.theta.larray.cpu().double())
+    assert torch.allclose(res[0], res[1], atol=2e-4), (res[0] - res[1]).abs().max()
+
+
 def test_lasso_graph_replay_matches_eager(gpu, monkeypatch):
     import heat_amd as ht
 
@@ -312,6 +362,7 @@ def test_lasso_graph_replay_matches_eager(gpu, monkeypatch):
     x = ht.random.randn(20000, 12)
     y = ht.matmul(x, ht.random.randn(12, 1)) + 0.05 * ht.random.randn(20000, 1)
     res = []
+    monkeypatch.setenv("HEAT_LASSO_SOLVER", "sweep")
     for flag in ("0", "1"):
         monkeypatch.setenv("HEAT_AMD_NO_GRAPHS", flag)
         est = ht.regression.Lasso(lam=0.01, max_iter=20, tol=None)

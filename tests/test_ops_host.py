@@ -42,3 +42,40 @@ def test_kmeans_update_host():
     ref = torch.zeros(7, 6, dtype=torch.float64).index_add_(0, lab.long(), X.double())
     assert torch.allclose(s.double(), ref, atol=1e-4)
     assert torch.equal(c.long(), torch.bincount(lab.long(), minlength=7))
+
+
+def _lasso_reference_loop(X, y, lam, max_iter, tol):
+    """The reference's data-form coordinate descent (heat/regression/lasso.py:121-175) in fp64 numpy."""
+    import numpy as np
+
+    m, n = X.shape
+    th = np.zeros(n)
+    it = 0
+    for it in range(1, max_iter + 1):
+        old_all = th.copy()
+        for j in range(n):
+            rho = np.mean(X[:, j] * (y - X @ th + th[j] * X[:, j]))
+            th[j] = rho if j == 0 else np.sign(rho) * max(abs(rho) - lam, 0.0)
+        if tol is not None and np.sqrt(np.mean((th - old_all) ** 2)) < tol:
+            break
+    return th, it
+
+
+def test_lasso_gram_cd_host_matches_reference_loop():
+    import numpy as np
+
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(800, 9))
+    X[:, 0] = 1.0
+    X /= np.sqrt((X ** 2).mean(0))
+    y = X @ rng.normal(size=9) + 0.1 * rng.normal(size=800)
+    G = ops.lasso_gram(torch.from_numpy(X).float(), torch.from_numpy(y).float())
+    A = np.concatenate([X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64)[:, None]], 1)
+    assert torch.allclose(G, torch.from_numpy(A.T @ A), rtol=1e-10)
+    G = G / 800
+    for tol in (None, 1e-6):
+        th = torch.zeros(9, dtype=torch.float64)
+        it = ops.lasso_cd(G[:9, :9], G[:9, 9].contiguous(), 0.05, 40, tol, th)
+        ref, rit = _lasso_reference_loop(A[:, :9], A[:, 9], 0.05, 40, tol)
+        assert it == rit
+        assert np.allclose(th.numpy(), ref, atol=1e-9)
