@@ -11,12 +11,50 @@
 namespace {
 
 constexpr int GRAM_BLOCK = 256;
+#define HA_GRAM_DEFAULT_UNROLL 1  // measured 1e7 x 16: U=1 0.285 ms, U=2 0.297, U=4 0.408 (2 blocks per CU)
 
 // Upper triangle of the augmented Gram [x_i | y_i]^T [x_i | y_i] over a grid-stride set of rows:
 // every thread keeps NC (NC + 1) / 2 fp32 accumulators in registers (rows of <= NC - 1 features
 // fit, one row = NC values loaded once), then wave shuffles + LDS reduce them to one fp64 partial
 // per workgroup. Columns: 0..n-1 = x, n = y, n+1..NC-1 = 0.
+// Loads one row (n features, then y, zero-padded to NC) into v; rows >= m load zeros, which add
+// nothing to any product.
 template <int NC>
+__device__ __forceinline__ void gram_load_row(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
+                                              const float* __restrict__ y, bool vec4, int64_t i, float (&v)[NC]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) v[c] = 0.f;
+  if (i >= m) return;
+  const float* row = x + i * ldx;
+  if (vec4) {
+#pragma unroll
+    for (int c = 0; c < NC; c += 4) {
+      if (c + 4 <= n) {
+        const floatx4 q = *reinterpret_cast<const floatx4*>(row + c);
+        v[c] = q[0];
+        if (c + 1 < NC) v[c + 1] = q[1];
+        if (c + 2 < NC) v[c + 2] = q[2];
+        if (c + 3 < NC) v[c + 3] = q[3];
+      } else {
+#pragma unroll
+        for (int e = c; e < c + 4 && e < NC; ++e) v[e] = e < n ? row[e] : 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) v[c] = c < n ? row[c] : 0.f;
+  }
+  const float yi = y[i];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) v[c] = c == n ? yi : v[c];
+}
+
+// Upper triangle of the augmented Gram [x_i | y_i]^T [x_i | y_i] over a grid-stride set of rows:
+// every thread keeps NC (NC + 1) / 2 fp32 accumulators in registers, then wave shuffles + LDS
+// reduce them to one fp64 partial per workgroup. Columns: 0..n-1 = x, n = y, n+1..NC-1 = 0.
+// The accumulators cap occupancy at 1-2 waves per SIMD, so each thread issues the loads of U rows
+// before the FMAs of any of them: U rows of HBM latency in flight per thread instead of one.
+template <int NC, int U>
 __global__ __launch_bounds__(GRAM_BLOCK) void lasso_gram(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
                                                          const float* __restrict__ y, double* __restrict__ partial) {
   constexpr int T = NC * (NC + 1) / 2;
@@ -25,35 +63,18 @@ __global__ __launch_bounds__(GRAM_BLOCK) void lasso_gram(const float* __restrict
   for (int t = 0; t < T; ++t) acc[t] = 0.f;
   const int64_t stride = (int64_t)gridDim.x * GRAM_BLOCK;
   const bool vec4 = ((ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-  for (int64_t i = (int64_t)blockIdx.x * GRAM_BLOCK + threadIdx.x; i < m; i += stride) {
-    const float* row = x + i * ldx;
-    float v[NC];
-    if (vec4) {
+  for (int64_t i = (int64_t)blockIdx.x * GRAM_BLOCK + threadIdx.x; i < m; i += U * stride) {
+    float v[U][NC];
 #pragma unroll
-      for (int c = 0; c < NC; c += 4) {
-        if (c + 4 <= n) {
-          const floatx4 q = *reinterpret_cast<const floatx4*>(row + c);
-          v[c] = q[0];
-          if (c + 1 < NC) v[c + 1] = q[1];
-          if (c + 2 < NC) v[c + 2] = q[2];
-          if (c + 3 < NC) v[c + 3] = q[3];
-        } else {
+    for (int u = 0; u < U; ++u) gram_load_row<NC>(x, m, n, ldx, y, vec4, i + u * stride, v[u]);
 #pragma unroll
-          for (int e = c; e < c + 4 && e < NC; ++e) v[e] = e < n ? row[e] : 0.f;
-        }
-      }
-    } else {
+    for (int u = 0; u < U; ++u) {
+      int t = 0;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) v[c] = c < n ? row[c] : 0.f;
+      for (int a = 0; a < NC; ++a)
+#pragma unroll
+        for (int b = a; b < NC; ++b, ++t) acc[t] = fmaf(v[u][a], v[u][b], acc[t]);
     }
-    const float yi = y[i];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) v[c] = c == n ? yi : v[c];
-    int t = 0;
-#pragma unroll
-    for (int a = 0; a < NC; ++a)
-#pragma unroll
-      for (int b = a; b < NC; ++b, ++t) acc[t] = fmaf(v[a], v[b], acc[t]);
   }
   __shared__ double sh[GRAM_BLOCK / 64][T];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -71,10 +92,19 @@ __global__ __launch_bounds__(GRAM_BLOCK) void lasso_gram(const float* __restrict
   }
 }
 
-// All sweeps of cyclic coordinate descent on (G, b) for n <= 64: G staged once in LDS, lane k keeps
-// theta_k in a register. Per coordinate: one LDS row read, a 64-lane fp64 butterfly sum, two lane
-// broadcasts and the reference's update; the sweep's RMS change of theta (< tol stops, like the
-// host loop) is accumulated uniformly so every lane leaves the loop together.
+__device__ __forceinline__ double ha_readlane_d(double v, int lane) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// All sweeps of cyclic coordinate descent on (G, b) for n <= 64 in one wavefront. Lane k keeps
+// theta_k and c_k = (G theta)_k in registers and G (symmetric) sits in LDS, so a coordinate is
+//   rho = b_j - c_j + G_jj theta_j  (three lane reads),  theta_j <- update,
+//   c_k += G_kj (theta_j' - theta_j) on every lane (one LDS row read that does not depend on the
+//   previous coordinate) -- no cross-lane reduction on the dependency chain. The sweep's RMS change
+// of theta (< tol stops, like the host loop) is wave-uniform, so all lanes leave together.
 __global__ __launch_bounds__(64) void lasso_cd_small(const double* __restrict__ G, int n, int ldg,
                                                      const double* __restrict__ b, double lam, int max_iter,
                                                      double tol, double* __restrict__ theta, int* __restrict__ n_iter) {
@@ -84,16 +114,20 @@ __global__ __launch_bounds__(64) void lasso_cd_small(const double* __restrict__ 
   double th = lane < n ? theta[lane] : 0.0;
   const double bl = lane < n ? b[lane] : 0.0;
   __syncthreads();
+  const double dl = g[lane][lane];
+  double c = 0.0;                                   // (G theta)_lane for the start values
+  for (int j = 0; j < n; ++j) c = fma(g[j][lane], ha_readlane_d(th, j), c);
   int it = 0;
   while (it < max_iter) {
     ++it;
     double d2 = 0.0;
     for (int j = 0; j < n; ++j) {
-      const double s = __shfl(ha_wave_sum_d(g[j][lane] * th), 0, 64);
-      const double old = __shfl(th, j, 64);
-      const double rho = __shfl(bl, j, 64) - s + g[j][j] * old;
+      const double old = ha_readlane_d(th, j);
+      const double rho = ha_readlane_d(bl, j) - ha_readlane_d(c, j) + ha_readlane_d(dl, j) * old;
       const double nw = j == 0 ? rho : (rho < -lam ? rho + lam : (rho > lam ? rho - lam : 0.0));
-      d2 += (nw - old) * (nw - old);
+      const double delta = nw - old;
+      d2 = fma(delta, delta, d2);
+      c = fma(g[j][lane], delta, c);  // unconditional: a uniform branch costs more than the FMA
       if (lane == j) th = nw;
     }
     if (tol >= 0.0 && sqrt(d2 / n) < tol) break;
@@ -146,14 +180,21 @@ HA_EXPORT int ha_lasso_gram_blocks(int64_t m, int ncu) {
   return (int)(want < 1 ? 1 : want < cap ? want : cap);
 }
 
+// unroll = rows whose loads each thread issues before their FMAs (1, 2 or 4; 0 = default).
 HA_EXPORT int ha_lasso_gram(const float* x, int64_t m, int n, int64_t ldx, const float* y, double* partial, int blocks,
-                            void* stream) {
+                            int unroll, void* stream) {
   const int nc = n + 1;
   if (n < 1 || nc > 24 || m < 1 || blocks < 1) return HA_BAD_ARG;
   hipStream_t s = (hipStream_t)stream;
-#define HA_G(NC)                                                                                       \
-  case NC:                                                                                             \
-    hipLaunchKernelGGL(lasso_gram<NC>, dim3(blocks), dim3(GRAM_BLOCK), 0, s, x, m, n, ldx, y, partial); \
+  if (unroll <= 0) unroll = HA_GRAM_DEFAULT_UNROLL;
+#define HA_G(NC)                                                                                                  \
+  case NC:                                                                                                        \
+    if (unroll >= 4)                                                                                              \
+      hipLaunchKernelGGL((lasso_gram<NC, 4>), dim3(blocks), dim3(GRAM_BLOCK), 0, s, x, m, n, ldx, y, partial);    \
+    else if (unroll == 2)                                                                                         \
+      hipLaunchKernelGGL((lasso_gram<NC, 2>), dim3(blocks), dim3(GRAM_BLOCK), 0, s, x, m, n, ldx, y, partial);    \
+    else                                                                                                          \
+      hipLaunchKernelGGL((lasso_gram<NC, 1>), dim3(blocks), dim3(GRAM_BLOCK), 0, s, x, m, n, ldx, y, partial);    \
     break;
   switch (nc) {
     HA_G(2) HA_G(3) HA_G(4) HA_G(5) HA_G(6) HA_G(7) HA_G(8) HA_G(9) HA_G(10) HA_G(11) HA_G(12) HA_G(13)

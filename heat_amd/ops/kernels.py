@@ -479,6 +479,10 @@ def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: fl
 
 
 # --------------------------------------------------------------------------------------------- lasso
+_GRAM_UNROLL = int(os.environ.get("HEAT_GRAM_UNROLL", "0"))   # rows in flight per thread (0: kernel default)
+_GRAM_BLOCKS_PER_CU = int(os.environ.get("HEAT_GRAM_BLOCKS_PER_CU", "0"))  # 0: kernel default (2 per CU)
+
+
 def lasso_gram(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     """Unnormalised augmented Gram matrix [X | y]^T [X | y] of the local rows, float64
     [(n+1), (n+1)] (``csrc/lasso_gram.hip``: one pass, register accumulators, fp64 block partials).
@@ -494,10 +498,12 @@ def lasso_gram(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         Xc = X if X.stride(-1) == 1 else X.contiguous()
         yc = y.reshape(-1).to(torch.float32).contiguous()
         blocks = L.ha_lasso_gram_blocks(m, num_cus(dev))
+        if _GRAM_BLOCKS_PER_CU > 0:
+            blocks = max(1, min(blocks, _GRAM_BLOCKS_PER_CU * num_cus(dev)))
         nc = n + 1
         T = nc * (nc + 1) // 2
         part = torch.empty((blocks, T), dtype=torch.float64, device=dev)
-        check(L.ha_lasso_gram(_ptr(Xc), m, n, Xc.stride(0), _ptr(yc), _ptr(part), blocks,
+        check(L.ha_lasso_gram(_ptr(Xc), m, n, Xc.stride(0), _ptr(yc), _ptr(part), blocks, _GRAM_UNROLL,
                               ctypes.c_void_p(stream_ptr(dev))), "ha_lasso_gram")
         tri = part.sum(0)
         iu = torch.triu_indices(nc, nc, device=dev)
