@@ -510,15 +510,22 @@ def lasso_gram(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         G = torch.zeros((nc, nc), dtype=torch.float64, device=dev)
         G[iu[0], iu[1]] = tri
         return G + torch.triu(G, 1).T
-    A = torch.cat([X, y.reshape(-1, 1).to(X.dtype)], dim=1)
-    if not A.is_cuda:
-        A = A.double()
+    if not X.is_cuda:
+        A = torch.cat([X, y.reshape(-1, 1).to(X.dtype)], dim=1).double()
         return A.T @ A
+    # wider device rows: per row block one X^T X GEMM + X^T y GEMV in fp32 (no [X | y] copy),
+    # accumulated across blocks in fp64
+    yv = y.reshape(-1).to(torch.float32)
     G = torch.zeros((n + 1, n + 1), dtype=torch.float64, device=dev)
-    step = max(1, (1 << 20))
+    step = 1 << 20
     for r0 in range(0, m, step):
-        blk = A[r0: r0 + step].float()
-        G += (blk.T @ blk).double()
+        xb = X[r0: r0 + step].float()
+        yb = yv[r0: r0 + step]
+        G[:n, :n] += (xb.T @ xb).double()
+        xy = (xb.T @ yb).double()
+        G[:n, n] += xy
+        G[n, :n] += xy
+        G[n, n] += torch.dot(yb.double(), yb.double())
     return G
 
 
