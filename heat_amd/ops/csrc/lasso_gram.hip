@@ -136,13 +136,23 @@ __global__ __launch_bounds__(64) void lasso_cd_small(const double* __restrict__ 
   if (lane == 0) *n_iter = it;
 }
 
-// Wider systems (64 < n <= 2048): theta in LDS, rows of G streamed from L2 (lane k owns k + 64 q).
+// Wider systems (64 < n <= 2048), same incremental form: c = G theta lives in LDS (lane k owns
+// k + 64 q), theta in LDS. Per coordinate: one LDS broadcast read of c_j, the update, then
+// c_k += G_jk delta over row j of G (L2-resident; its loads do not depend on the chain, so the
+// compiler issues them ahead). One wave: LDS ops complete in program order, no barriers needed.
 __global__ __launch_bounds__(64) void lasso_cd(const double* __restrict__ G, int n, int ldg,
                                                const double* __restrict__ b, double lam, int max_iter, double tol,
                                                double* __restrict__ theta, int* __restrict__ n_iter) {
   __shared__ double th[2048];
+  __shared__ double c[2048];
   const int lane = threadIdx.x;
   for (int k = lane; k < n; k += 64) th[k] = theta[k];
+  __syncthreads();
+  for (int k = lane; k < n; k += 64) {          // c = G theta for the start values (G symmetric)
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s = fma(G[(int64_t)j * ldg + k], th[j], s);
+    c[k] = s;
+  }
   __syncthreads();
   int it = 0;
   while (it < max_iter) {
@@ -150,16 +160,16 @@ __global__ __launch_bounds__(64) void lasso_cd(const double* __restrict__ G, int
     double d2 = 0.0;
     for (int j = 0; j < n; ++j) {
       const double* gj = G + (int64_t)j * ldg;
-      double s = 0.0;
-      for (int k = lane; k < n; k += 64) s = fma(gj[k], th[k], s);
-      s = __shfl(ha_wave_sum_d(s), 0, 64);
       const double old = th[j];
-      const double rho = b[j] - s + gj[j] * old;
+      const double rho = b[j] - c[j] + gj[j] * old;
       const double nw = j == 0 ? rho : (rho < -lam ? rho + lam : (rho > lam ? rho - lam : 0.0));
-      d2 += (nw - old) * (nw - old);
-      __syncthreads();  // every lane has read th[j] before it changes (one wave: a no-op barrier)
-      if (lane == 0) th[j] = nw;
-      __syncthreads();
+      const double delta = nw - old;
+      d2 = fma(delta, delta, d2);
+      if (delta != 0.0) {                         // uniform: skipped for coordinates that stay 0
+        for (int k = lane; k < n; k += 64) c[k] = fma(gj[k], delta, c[k]);
+        if (lane == 0) th[j] = nw;
+      }
+      __syncthreads();                            // one wave: orders the LDS writes (a no-op barrier)
     }
     if (tol >= 0.0 && sqrt(d2 / n) < tol) break;
   }

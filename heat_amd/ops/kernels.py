@@ -483,6 +483,44 @@ _GRAM_UNROLL = int(os.environ.get("HEAT_GRAM_UNROLL", "0"))   # rows in flight p
 _GRAM_BLOCKS_PER_CU = int(os.environ.get("HEAT_GRAM_BLOCKS_PER_CU", "0"))  # 0: kernel default (2 per CU)
 
 
+def _gram_blocked(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """[X | y]^T [X | y] in fp64 from fp32 GEMMs (the device path of ``lasso_gram`` beyond the
+    native kernel's column limit)."""
+    m, n = X.shape
+    dev = X.device
+    # wider device rows: X^T X as a batched split-K GEMM (rows grouped into nb slabs of r rows, one
+    # [n, r] x [r, n] product per slab: a plain X^T X has only (n / tile)^2 output tiles and leaves
+    # the chip idle), X^T y likewise; slab partials summed in fp32, row blocks accumulated in fp64.
+    # No [X | y] copy is materialised.
+    Xc = X if X.is_contiguous() else X.contiguous()
+    yv = y.reshape(-1).to(torch.float32)
+    G = torch.zeros((n + 1, n + 1), dtype=torch.float64, device=dev)
+    nb = max(1, min(256, (256 << 20) // (4 * n * n)))
+    step = max(nb * 1024, 1 << 20)
+    for r0 in range(0, m, step):
+        xb = Xc[r0: r0 + step].float()
+        yb = yv[r0: r0 + step]
+        rows = xb.shape[0]
+        r = rows // nb
+        if r >= 256:
+            x3 = xb[: nb * r].reshape(nb, r, n)
+            y3 = yb[: nb * r].reshape(nb, r, 1)
+            xtx = torch.bmm(x3.transpose(1, 2), x3).sum(0)
+            xy = torch.bmm(x3.transpose(1, 2), y3).sum(0).reshape(n)
+            xb, yb = xb[nb * r:], yb[nb * r:]
+        else:
+            xtx = torch.zeros((n, n), dtype=torch.float32, device=dev)
+            xy = torch.zeros(n, dtype=torch.float32, device=dev)
+        if xb.shape[0]:
+            xtx = xtx + xb.T @ xb
+            xy = xy + xb.T @ yb
+        G[:n, :n] += xtx.double()
+        G[:n, n] += xy.double()
+        G[n, :n] += xy.double()
+        G[n, n] += torch.dot(yv[r0: r0 + step].double(), yv[r0: r0 + step].double())
+    return G
+
+
 def lasso_gram(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     """Unnormalised augmented Gram matrix [X | y]^T [X | y] of the local rows, float64
     [(n+1), (n+1)] (``csrc/lasso_gram.hip``: one pass, register accumulators, fp64 block partials).
@@ -513,20 +551,7 @@ def lasso_gram(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     if not X.is_cuda:
         A = torch.cat([X, y.reshape(-1, 1).to(X.dtype)], dim=1).double()
         return A.T @ A
-    # wider device rows: per row block one X^T X GEMM + X^T y GEMV in fp32 (no [X | y] copy),
-    # accumulated across blocks in fp64
-    yv = y.reshape(-1).to(torch.float32)
-    G = torch.zeros((n + 1, n + 1), dtype=torch.float64, device=dev)
-    step = 1 << 20
-    for r0 in range(0, m, step):
-        xb = X[r0: r0 + step].float()
-        yb = yv[r0: r0 + step]
-        G[:n, :n] += (xb.T @ xb).double()
-        xy = (xb.T @ yb).double()
-        G[:n, n] += xy
-        G[n, :n] += xy
-        G[n, n] += torch.dot(yb.double(), yb.double())
-    return G
+    return _gram_blocked(X, y)
 
 
 def lasso_cd(G: torch.Tensor, b: torch.Tensor, lam: float, max_iter: int, tol: Optional[float],

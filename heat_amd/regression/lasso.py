@@ -10,8 +10,9 @@ Narrow problems (n <= 64 features, the tall-skinny regime the reference benchmar
 covariance form of the same update: rho_j = b_j - (G theta)_j + G_jj theta_j with G = X^T X / m,
 b = X^T y / m. One native pass over the rows builds [X | y]^T [X | y] (``ops.lasso_gram``), split
 data needs ONE fp64 all-reduce of that (n+1)^2 matrix per fit, and every sweep plus the convergence
-test runs in one single-wavefront kernel (``ops.lasso_cd``). ``HEAT_LASSO_SOLVER=sweep|gram``
-forces either form.
+test runs in one single-wavefront kernel (``ops.lasso_cd``). Wider device problems (n <= 2048)
+take the same form when a measured cost model (``_prefer_gram``) says the Gram GEMM is cheaper than
+max_iter data sweeps. ``HEAT_LASSO_SOLVER=sweep|gram`` forces either form.
 """
 from __future__ import annotations
 
@@ -27,6 +28,20 @@ from ..core.dndarray import DNDarray
 from .. import ops
 
 __all__ = ["Lasso"]
+
+
+def _prefer_gram(m_local: int, n: int, max_iter: int, device: bool) -> bool:
+    """Covariance vs sweep solver by a cost model with constants measured on one MI355X (1e7 rows,
+    n = 16 / 256: a sweep costs ~60 us per coordinate, one column pass at ~0.7 TB/s; the Gram pass
+    runs at ~4 TB/s (native, n < 24) or as a batched fp32 GEMM at ~130 TFLOP/s; device CD ~0.1 us
+    per coordinate plus n/64 L2 loads)."""
+    if n <= 64:
+        return True
+    if not device or n > 2048:
+        return False
+    sweep = max_iter * n * (4.0 * m_local / 0.7e12 + 3e-6)
+    gram = 2.0 * m_local * n * n / 1.3e14 + 4.0 * m_local * n / 4e12 + max_iter * n * (1e-7 + n / 64 * 2e-9)
+    return gram < sweep
 
 
 class Lasso(RegressionMixin, BaseEstimator):
@@ -95,7 +110,7 @@ class Lasso(RegressionMixin, BaseEstimator):
             yl = yl[r0: r0 + counts[x.comm.rank]]
         dist = x.is_distributed()
         solver = os.environ.get("HEAT_LASSO_SOLVER", "auto")
-        if solver == "gram" or (solver == "auto" and n <= 64):
+        if solver == "gram" or (solver == "auto" and _prefer_gram(m // x.comm.size, n, self.max_iter, X.is_cuda)):
             G = ops.lasso_gram(X, yl)                         # [n+1, n+1] fp64, local rows
             if dist:
                 x.comm.Allreduce(MPI.IN_PLACE, G, MPI.SUM)

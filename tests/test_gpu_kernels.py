@@ -318,7 +318,7 @@ def test_lasso_gram_matches_fp64(gpu, m, n):
     assert torch.allclose(G, ref, rtol=1e-5, atol=1e-6 * m), (G - ref).abs().max()
 
 
-@pytest.mark.parametrize("n", [5, 64, 130])
+@pytest.mark.parametrize("n", [5, 64, 65, 130, 700])
 @pytest.mark.parametrize("tol", [None, 1e-6])
 def test_lasso_cd_device_matches_host(gpu, n, tol):
     from heat_amd import ops
@@ -339,13 +339,14 @@ def test_lasso_cd_device_matches_host(gpu, n, tol):
     assert torch.allclose(res[0][1], res[1][1], atol=1e-9)
 
 
-def test_lasso_gram_solver_matches_sweep(gpu, monkeypatch):
+@pytest.mark.parametrize("n", [16, 200])
+def test_lasso_gram_solver_matches_sweep(gpu, monkeypatch, n):
     import heat_amd as ht
 
     ht.random.seed(5)
-    x = ht.random.randn(50000, 16)
+    x = ht.random.randn(50000, n)
     x = x / ht.sqrt(ht.mean(x ** 2, axis=0))
-    y = ht.matmul(x, ht.random.randn(16, 1)) + 0.05 * ht.random.randn(50000, 1)
+    y = ht.matmul(x, ht.random.randn(n, 1)) + 0.05 * ht.random.randn(50000, 1)
     res = []
     for solver in ("sweep", "gram"):
         monkeypatch.setenv("HEAT_LASSO_SOLVER", solver)

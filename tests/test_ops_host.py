@@ -79,3 +79,14 @@ def test_lasso_gram_cd_host_matches_reference_loop():
         ref, rit = _lasso_reference_loop(A[:, :9], A[:, 9], 0.05, 40, tol)
         assert it == rit
         assert np.allclose(th.numpy(), ref, atol=1e-9)
+
+
+def test_lasso_gram_blocked_matches_fp64():
+    from heat_amd.ops.kernels import _gram_blocked
+
+    g = torch.Generator().manual_seed(3)
+    for m, n in [(3000, 5), (70001, 130)]:
+        X, y = torch.randn(m, n, generator=g), torch.randn(m, generator=g)
+        A = torch.cat([X, y[:, None]], 1).double()
+        ref = A.T @ A
+        assert torch.allclose(_gram_blocked(X, y), ref, rtol=0, atol=1e-6 * ref.abs().max().item())
