@@ -136,17 +136,25 @@ __global__ __launch_bounds__(64) void lasso_cd_small(const double* __restrict__ 
   if (lane == 0) *n_iter = it;
 }
 
-// Wider systems (64 < n <= 2048), same incremental form: c = G theta lives in LDS (lane k owns
-// k + 64 q), theta in LDS. Per coordinate: one LDS broadcast read of c_j, the update, then
-// c_k += G_jk delta over row j of G (L2-resident; its loads do not depend on the chain, so the
-// compiler issues them ahead). One wave: LDS ops complete in program order, no barriers needed.
+// Wider systems (64 < n <= 2048), same incremental form: c = G theta, theta, b and diag(G) live in
+// LDS (lane k owns k + 64 q), so the per-coordinate dependency chain (c_j, b_j, G_jj, theta_j ->
+// update -> c) touches LDS only. Rows of G (n doubles each; L2 / MALL resident, ~1 us away) stream
+// through a register ring P rows deep: the row for coordinate t + P is requested when coordinate t
+// is done with its slot, so a fetch has P coordinate chains to land (fetching only one row ahead
+// measured ~1 us per coordinate: the wait for the row sat on the chain). Coordinates run over a
+// padded count np = P * ceil(n / P); padded slots fetch zeros and skip their update.
+// NQ = 64-lane column groups (n <= 64 NQ); P * NQ <= 64 keeps the ring within 128 VGPRs.
+template <int NQ, int P>
 __global__ __launch_bounds__(64) void lasso_cd(const double* __restrict__ G, int n, int ldg,
                                                const double* __restrict__ b, double lam, int max_iter, double tol,
                                                double* __restrict__ theta, int* __restrict__ n_iter) {
-  __shared__ double th[2048];
-  __shared__ double c[2048];
+  __shared__ double th[64 * NQ], c[64 * NQ], bs[64 * NQ], dg[64 * NQ];
   const int lane = threadIdx.x;
-  for (int k = lane; k < n; k += 64) th[k] = theta[k];
+  for (int k = lane; k < n; k += 64) {
+    th[k] = theta[k];
+    bs[k] = b[k];
+    dg[k] = G[(int64_t)k * ldg + k];
+  }
   __syncthreads();
   for (int k = lane; k < n; k += 64) {          // c = G theta for the start values (G symmetric)
     double s = 0.0;
@@ -154,22 +162,45 @@ __global__ __launch_bounds__(64) void lasso_cd(const double* __restrict__ G, int
     c[k] = s;
   }
   __syncthreads();
+  const int np = (n + P - 1) / P * P;
+  double ring[P][NQ];
+  auto fetch = [&](int j, double (&r)[NQ]) {
+    const double* gj = G + (int64_t)(j < n ? j : 0) * ldg;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int k = lane + 64 * q;
+      r[q] = (j < n && k < n) ? gj[k] : 0.0;
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < P; ++s) fetch(s, ring[s]);
   int it = 0;
   while (it < max_iter) {
     ++it;
     double d2 = 0.0;
-    for (int j = 0; j < n; ++j) {
-      const double* gj = G + (int64_t)j * ldg;
-      const double old = th[j];
-      const double rho = b[j] - c[j] + gj[j] * old;
-      const double nw = j == 0 ? rho : (rho < -lam ? rho + lam : (rho > lam ? rho - lam : 0.0));
-      const double delta = nw - old;
-      d2 = fma(delta, delta, d2);
-      if (delta != 0.0) {                         // uniform: skipped for coordinates that stay 0
-        for (int k = lane; k < n; k += 64) c[k] = fma(gj[k], delta, c[k]);
-        if (lane == 0) th[j] = nw;
+    for (int j0 = 0; j0 < np; j0 += P) {
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const int j = j0 + s;
+        if (j < n) {                              // uniform
+          const double old = th[j];
+          const double rho = bs[j] - c[j] + dg[j] * old;
+          const double nw = j == 0 ? rho : (rho < -lam ? rho + lam : (rho > lam ? rho - lam : 0.0));
+          const double delta = nw - old;
+          d2 = fma(delta, delta, d2);
+          if (delta != 0.0) {                     // uniform: skipped for coordinates that stay 0
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+              const int k = lane + 64 * q;
+              if (k < n) c[k] = fma(ring[s][q], delta, c[k]);
+            }
+            if (lane == 0) th[j] = nw;
+          }
+          __syncthreads();                        // one wave: orders the LDS writes (a no-op barrier)
+        }
+        const int jn = j + P < np ? j + P : j + P - np;   // the slot's next row (wraps into the next sweep)
+        fetch(jn, ring[s]);
       }
-      __syncthreads();                            // one wave: orders the LDS writes (a no-op barrier)
     }
     if (tol >= 0.0 && sqrt(d2 / n) < tol) break;
   }
@@ -221,8 +252,20 @@ HA_EXPORT int ha_lasso_cd(const double* G, int n, int ldg, const double* b, doub
   if (n <= 64)
     hipLaunchKernelGGL(lasso_cd_small, dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol,
                        theta, n_iter);
+  else if (n <= 128)
+    hipLaunchKernelGGL((lasso_cd<2, 8>), dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol,
+                       theta, n_iter);
+  else if (n <= 256)
+    hipLaunchKernelGGL((lasso_cd<4, 8>), dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol,
+                       theta, n_iter);
+  else if (n <= 512)
+    hipLaunchKernelGGL((lasso_cd<8, 8>), dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol,
+                       theta, n_iter);
+  else if (n <= 1024)
+    hipLaunchKernelGGL((lasso_cd<16, 4>), dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol,
+                       theta, n_iter);
   else
-    hipLaunchKernelGGL(lasso_cd, dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol, theta,
-                       n_iter);
+    hipLaunchKernelGGL((lasso_cd<32, 2>), dim3(1), dim3(64), 0, (hipStream_t)stream, G, n, ldg, b, lam, max_iter, tol,
+                       theta, n_iter);
   return ha_launch_status();
 }

@@ -318,7 +318,7 @@ def test_lasso_gram_matches_fp64(gpu, m, n):
     assert torch.allclose(G, ref, rtol=1e-5, atol=1e-6 * m), (G - ref).abs().max()
 
 
-@pytest.mark.parametrize("n", [5, 64, 65, 130, 700])
+@pytest.mark.parametrize("n", [5, 64, 65, 130, 700, 1500])
 @pytest.mark.parametrize("tol", [None, 1e-6])
 def test_lasso_cd_device_matches_host(gpu, n, tol):
     from heat_amd import ops
