@@ -490,15 +490,17 @@ def _gram_blocked(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     dev = X.device
     # wider device rows: X^T X as a batched split-K GEMM (rows grouped into nb slabs of r rows, one
     # [n, r] x [r, n] product per slab: a plain X^T X has only (n / tile)^2 output tiles and leaves
-    # the chip idle), X^T y likewise; slab partials summed in fp32, row blocks accumulated in fp64.
+    # the chip idle), X^T y likewise; slab partials summed in the data precision (fp32, or fp64 for
+    # fp64 data), row blocks accumulated in fp64.
     # No [X | y] copy is materialised.
     Xc = X if X.is_contiguous() else X.contiguous()
-    yv = y.reshape(-1).to(torch.float32)
+    cd_t = torch.float64 if X.dtype == torch.float64 else torch.float32   # fp64 data stays fp64
+    yv = y.reshape(-1).to(cd_t)
     G = torch.zeros((n + 1, n + 1), dtype=torch.float64, device=dev)
     nb = max(1, min(256, (256 << 20) // (4 * n * n)))
     step = max(nb * 1024, 1 << 20)
     for r0 in range(0, m, step):
-        xb = Xc[r0: r0 + step].float()
+        xb = Xc[r0: r0 + step].to(cd_t)
         yb = yv[r0: r0 + step]
         rows = xb.shape[0]
         r = rows // nb
@@ -509,8 +511,8 @@ def _gram_blocked(X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
             xy = torch.bmm(x3.transpose(1, 2), y3).sum(0).reshape(n)
             xb, yb = xb[nb * r:], yb[nb * r:]
         else:
-            xtx = torch.zeros((n, n), dtype=torch.float32, device=dev)
-            xy = torch.zeros(n, dtype=torch.float32, device=dev)
+            xtx = torch.zeros((n, n), dtype=cd_t, device=dev)
+            xy = torch.zeros(n, dtype=cd_t, device=dev)
         if xb.shape[0]:
             xtx = xtx + xb.T @ xb
             xy = xy + xb.T @ yb
