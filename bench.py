@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--precision", default="fast", choices=["fast", "exact"],
                    help="kmeans: 'fast' = distances by a 3-term fp16 split on the matrix cores (fp32-GEMM "
                         "accuracy, checked against fp64 in tests/test_gpu_kernels.py); 'exact' = fp32-input MFMA")
+    p.add_argument("--exact-steps", type=int, default=5,
+                   help="kmeans fast: also time this many steps of the exact fp32-MFMA path (0 = skip)")
     p.add_argument("--with-reference", action="store_true",
                    help="also time a reference-style (heat 1.1 algorithm) iteration on torch-ROCm")
     return p.parse_args()
@@ -60,7 +62,7 @@ def main():
             torch.cuda.synchronize()
 
     n_gpus = comm.size
-    extra = {}
+    extra = {"world_size_seen_by_rccl": rccl_world_size(comm)}
     scaling = "weak"
     if args.workload == "kmeans":
         args.n_per_gpu = args.n_per_gpu or 12_500_000
@@ -78,8 +80,7 @@ def main():
         sync()
         dt = time.perf_counter() - t0
         # slowest rank defines the step
-        dt = comm.allreduce(dt, ht.MPI.MAX) if comm.size > 1 else dt
-        ms = dt / args.steps * 1e3
+        ms = rank_times(comm, dt, args.steps, extra)
         flops = 2.0 * n * k * f
         value = flops / (ms * 1e-3) / 1e9
         metric = "kmeans_iter_gflops"
@@ -90,9 +91,26 @@ def main():
                "n_per_gpu": args.n_per_gpu}
         extra["iter_ms"] = ms
         extra["precision"] = ("fp32 data and centroids; distance GEMM as a 3-term fp16 split with fp32 "
-                              "accumulation (fp32-GEMM accuracy)" if args.precision == "fast"
+                              "accumulation (fp32-GEMM accuracy, per-row power-of-two scales for points "
+                              "AND centroids); value is an fp32-EQUIVALENT rate (2*n*k*f per iteration), "
+                              "not an fp32-MFMA rate" if args.precision == "fast"
                               else "fp32-input MFMA (exact fp32 products)")
         extra["tflops_per_gpu"] = value / n_gpus / 1e3
+        if args.precision == "fast" and args.exact_steps > 0:
+            # the exact fp32-MFMA path on the same data, for an honest side-by-side
+            km_exact = ht.cluster.KMeans(n_clusters=k, init="random", max_iter=1, tol=None, random_state=42)
+            km_exact.precision = "exact"
+            for _ in range(2):
+                km_exact.step(x)
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(args.exact_steps):
+                km_exact.step(x)
+            sync()
+            dte = time.perf_counter() - t0
+            dte = comm.allreduce(dte, ht.MPI.MAX) if comm.size > 1 else dte
+            extra["exact_ms_per_step"] = dte / args.exact_steps * 1e3
+            extra["exact_gflops_fp32"] = flops / (extra["exact_ms_per_step"] * 1e-3) / 1e9
         if args.with_reference:
             extra["reference_impl_ms"] = reference_iteration(x, km, k)
             extra["speedup_vs_reference_impl"] = extra["reference_impl_ms"] / ms
@@ -120,8 +138,7 @@ def main():
             one()
         sync()
         dt = time.perf_counter() - t0
-        dt = comm.allreduce(dt, ht.MPI.MAX) if comm.size > 1 else dt
-        ms = dt / args.steps * 1e3
+        ms = rank_times(comm, dt, args.steps, extra)
         value = 2.0 * n * n * f / (ms * 1e-3) / 1e9
         metric, unit = "cdist_gflops", "GFLOP/s"
         cfg = {"model": "cdist euclidean n={} f={} float32 split=0 (streamed tiles)".format(n, f),
@@ -142,18 +159,39 @@ def main():
             v = ht.var(x)
         sync()
         dt = time.perf_counter() - t0
-        dt = comm.allreduce(dt, ht.MPI.MAX) if comm.size > 1 else dt
-        ms = dt / args.steps * 1e3
+        ms = rank_times(comm, dt, args.steps, extra)
         value = 2 * n * 4 / (ms * 1e-3) / 1e9
         metric, unit = "moments_GB_per_s", "GB/s"
         cfg = {"model": "mean+var float32 split=0", "global_batch": n, "seq_len": 1,
                "parallelism": "dp{}".format(n_gpus)}
+    if args.workload == "kmeans" and args.precision == "fast":
+        unit = "GFLOP/s (fp32-equivalent)"
     if comm.rank == 0:
         out = {"metric": metric, "value": value, "unit": unit, "n_gpus": n_gpus, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": scaling,
                "vs_baseline": None, "dtype": "fp32", "data": "synthetic (device Threefry normal samples)",
                "config": cfg, "extra": extra}
         print(json.dumps(out), flush=True)
+
+
+def rccl_world_size(comm) -> int:
+    """Number of ranks a DEVICE all-reduce actually reaches (RCCL on a GPU job, gloo on CPU)."""
+    import torch.distributed as dist
+
+    if comm.size == 1 or not dist.is_initialized():
+        return 1
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    one = torch.ones(1, dtype=torch.int32, device=dev)
+    dist.all_reduce(one)
+    return int(one.item())
+
+
+def rank_times(comm, dt: float, steps: int, extra: dict) -> float:
+    """ms per step of the SLOWEST rank (the job's step time); per-rank spread into ``extra``."""
+    per_rank = comm.allgather(dt) if comm.size > 1 else [dt]
+    extra["rank_ms_per_step_min"] = min(per_rank) / steps * 1e3
+    extra["rank_ms_per_step_max"] = max(per_rank) / steps * 1e3
+    return max(per_rank) / steps * 1e3
 
 
 def reference_iteration(x, km, k):

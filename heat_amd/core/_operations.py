@@ -96,8 +96,14 @@ def binary_op(operation: Callable, t1, t2, out: Optional[DNDarray] = None, where
         if s1 is not None and s2 is not None and s1 != s2:
             from .manipulations import resplit
 
-            t2 = resplit(t2, s1 - (nd - t2.ndim))
-            s2 = s1
+            if s1 - (nd - t2.ndim) >= 0:
+                t2 = resplit(t2, s1 - (nd - t2.ndim))
+                s2 = s1
+            else:
+                # t1's split axis is a broadcast (leading) axis of t2: replicate t2 (it is
+                # smaller than the result), the s1 path below slices it where needed
+                t2 = resplit(t2, None)
+                s2 = None
         a, b = t1.larray, t2.larray
         split = s1 if s1 is not None else s2
         balanced = True
@@ -208,8 +214,12 @@ def reduce_op(x: DNDarray, partial_op: Callable, reduction_op: Op, axis=None, ou
         axis = axis[0]
     split = x.split
     t = x.larray
-    if split is not None and t.shape[split] == 0 and x.is_distributed():
-        # empty local block: substitute neutral elements so the all-reduce is correct
+    red_axes = None if axis is None else ((axis,) if isinstance(axis, int) else tuple(axis))
+    if (split is not None and t.shape[split] == 0 and x.is_distributed()
+            and (red_axes is None or split in red_axes)):
+        # empty local block whose split axis is reduced: substitute neutral elements so the
+        # all-reduce is correct (ref _operations.py:401 guards on `split in axis` the same way;
+        # a reduction along another axis keeps the empty block and its (.., 0, ..) shape)
         shp = list(t.shape)
         shp[split] = 1
         fill = neutral if neutral is not None else 0

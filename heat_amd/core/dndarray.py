@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import math
 import warnings
-from typing import Any, List, Optional, Sequence, Tuple, Union
+from typing import Any, Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -603,6 +603,18 @@ class DNDarray:
             out = out[:i] + [slice(None)] * (self.ndim - consumed) + out[i + 1:]
         else:
             out = out + [slice(None)] * (self.ndim - consumed)
+        # a k-dim boolean mask inside a key is k integer index arrays (NumPy semantics): expand it
+        # so every key entry addresses exactly one array dimension
+        exp = []
+        for k in out:
+            if isinstance(k, torch.Tensor) and k.dtype == torch.bool and k.dim() != 1:
+                if k.dim() == 0:
+                    exp.append(k)
+                else:
+                    exp.extend(torch.nonzero(k, as_tuple=True))
+            else:
+                exp.append(k)
+        out = exp
         # torch has no negative slice steps: express them as index arrays
         dim = 0
         for i, k in enumerate(out):
@@ -622,7 +634,10 @@ class DNDarray:
                 if self.is_distributed() and key.split != self.split:
                     _, _, sl = self.comm.chunk(self.gshape, self.split)
                     mask = mask[sl]
-                res = self.__array[mask.to(self.__array.device)]
+                mask = mask.to(self.__array.device)
+                if self.is_distributed() and self.split != 0:
+                    return self._masked_select_c_order(mask)
+                res = self.__array[mask]
                 if not self.is_distributed():
                     return DNDarray(res, tuple(res.shape), self.dtype, None if self.split is None else 0,
                                     self.device, self.comm, True)
@@ -717,15 +732,81 @@ class DNDarray:
             new_split = self._out_split(key, adv, gout)
             return DNDarray(res, gout, self.dtype, new_split, self.device, self.comm, None)
 
-        # general advanced indexing (several index arrays / boolean masks): gather, index, re-chunk
-        full = self._gathered()
-        dkey = tuple(k.to(full.device) if isinstance(k, torch.Tensor) else k for k in key)
-        res = full[dkey].reshape(gout)
-        new_split = 0 if len(gout) > 0 else None
-        if new_split is not None:
-            _, _, sl = self.comm.chunk(gout, new_split)
-            res = res[sl]
-        return DNDarray(res, gout, self.dtype, new_split, self.device, self.comm, True)
+        # general advanced indexing (several index arrays / boolean masks): owner-computes. Every
+        # rank derives the global source coordinates of ITS chunk of the result (split 0) from
+        # zero-stride coordinate proxies indexed with the key, then fetches exactly those elements
+        # from their owners in one request/reply round trip - the input is never gathered.
+        ckey = tuple(k.cpu() if isinstance(k, torch.Tensor) else k for k in key)
+        if len(gout) == 0:
+            coords = []
+            for d in range(self.ndim):
+                shp = [1] * self.ndim
+                shp[d] = -1
+                coords.append(torch.arange(self.gshape[d]).view(shp).expand(self.gshape)[ckey].reshape(1))
+            val = self._fetch_elements(coords) if rank == 0 else self._fetch_elements(
+                [c[:0] for c in coords])
+            res = val.reshape(()) if rank == 0 else torch.empty((), dtype=self.__array.dtype, device=self.__array.device)
+            self.comm.Bcast(res, root=0)
+            return DNDarray(res, gout, self.dtype, None, self.device, self.comm, True)
+        _, lout, sl = self.comm.chunk(gout, 0)
+        coords = []
+        for d in range(self.ndim):
+            shp = [1] * self.ndim
+            shp[d] = -1
+            cd = torch.arange(self.gshape[d]).view(shp).expand(self.gshape)[ckey].reshape(gout)
+            coords.append(cd[sl[0]])
+        res = self._fetch_elements(coords).reshape(lout)
+        return DNDarray(res, gout, self.dtype, 0, self.device, self.comm, True)
+
+    def _mask_positions(self, mask: torch.Tensor):
+        """Global C-order positions of the local True entries of a same-distribution ``mask``
+        (ascending along the local selection) and the global number of True entries."""
+        s, rank = self.split, self.comm.rank
+        dev = mask.device
+        outer = int(np.prod(self.gshape[:s])) if s > 0 else 1
+        m2 = mask.reshape(outer, -1)
+        cnt = m2.sum(dim=1, dtype=torch.int64)
+        allc = self.comm.allgather_tensor(cnt.reshape(1, -1), axis=0)  # [p, O]
+        total_o = allc.sum(dim=0)
+        base_o = torch.cumsum(total_o, 0) - total_o + allc[:rank].sum(dim=0)  # first slot of (o, rank)
+        local_start = torch.cumsum(cnt, 0) - cnt
+        o_idx = torch.repeat_interleave(torch.arange(outer, device=dev), cnt)
+        pos = base_o[o_idx] + torch.arange(o_idx.numel(), device=dev) - local_start[o_idx]
+        return pos, int(total_o.sum())
+
+    def _masked_select_c_order(self, mask: torch.Tensor) -> "DNDarray":
+        """``self[mask]`` for a split > 0 array: the selected elements in global C order, balanced
+        along split 0.
+
+        Every local selection is already in C order within the rank, and the global position of
+        an element only depends on its outer index o (the dims before the split) and on how many
+        elements lower ranks select for the same o. So one all-gather of the per-o counts (O =
+        prod(gshape[:split]) integers per rank) gives every element its global position, and one
+        personalised exchange moves the values to their balanced owner - no array gather."""
+        pos, n = self._mask_positions(mask)
+        out = self._place_by_position(self.__array[mask], pos, n)
+        return DNDarray(out, (n,), self.dtype, 0, self.device, self.comm, True)
+
+    def _place_by_position(self, vals: torch.Tensor, pos: torch.Tensor, n: int) -> torch.Tensor:
+        """Rows ``vals`` with ascending global positions ``pos`` (out of ``n``) moved to the
+        balanced split-0 block that owns each position; returns this rank's block."""
+        p, rank = self.comm.size, self.comm.rank
+        dev = vals.device
+        out_counts = _chunk_counts(n, p)
+        bnds = _partition_bounds(out_counts)
+        bounds = torch.tensor([hi for _, hi in bnds], dtype=torch.int64, device=dev)
+        owner = torch.bucketize(pos, bounds, right=True)
+        send_n = torch.bincount(owner, minlength=p)
+        # positions increase along the local selection, so each destination gets one contiguous run
+        splits = send_n.tolist()
+        recv_n = self.comm.allgather_tensor(send_n.reshape(1, -1), axis=0)[:, rank].tolist()
+        rest = tuple(vals.shape[1:])
+        rv = self.comm.exchange(list(torch.split(vals, splits)), [(c,) + rest for c in recv_n])
+        rp = self.comm.exchange(list(torch.split(pos, splits)), [(c,) for c in recv_n])
+        out = torch.empty((out_counts[rank],) + rest, dtype=vals.dtype, device=dev)
+        if out.shape[0]:
+            out[torch.cat(rp) - bnds[rank][0]] = torch.cat(rv)
+        return out
 
     def _out_split(self, key, adv, gout) -> Optional[int]:
         """Split axis of the result of basic/advanced indexing."""
@@ -751,46 +832,79 @@ class DNDarray:
         return None
 
     def _take_split(self, idx: torch.Tensor) -> torch.Tensor:
-        """Rows ``idx`` (global indices along the split axis, any order) block-distributed in the
-        order of ``idx``: one personalised exchange (owner -> consumer)."""
-        s = self.split
+        """Rows ``idx`` (global indices along the split axis, the same on every rank, any order)
+        block-distributed in the order of ``idx``: every rank fetches its chunk of the key."""
+        lo, hi = _partition_bounds(_chunk_counts(idx.numel(), self.comm.size))[self.comm.rank]
+        return self._fetch_rows(idx[lo:hi])
+
+    def _serve(self, owner: torch.Tensor, req: torch.Tensor, serve: Callable, item_shape: Tuple[int, ...],
+               dtype: torch.dtype) -> torch.Tensor:
+        """Owner-computes request/reply: rank-local requests ``req`` (int64, any order, different on
+        every rank) go to ``owner``; the owner answers with ``serve(requests) -> [n, *item_shape]``.
+        Returns the answers in request order. Two personalised exchanges plus one p x p count
+        all-gather; nothing is gathered whole."""
         p, rank = self.comm.size, self.comm.rank
-        counts, displs = self.counts_displs()
-        m = idx.numel()
-        out_counts = _chunk_counts(m, p)
-        out_bounds = _partition_bounds(out_counts)
-        bounds = torch.tensor([d + c for d, c in zip(displs, counts)], dtype=torch.int64)
-        idx_cpu = idx.cpu()
-        owner = torch.bucketize(idx_cpu, bounds, right=True)
         dev = self.__array.device
-        blocks, shapes = [], []
-        base = list(self.__array.shape)
-        for q in range(p):
-            lo, hi = out_bounds[q]
-            sel = idx_cpu[lo:hi]
-            mine = sel[owner[lo:hi] == rank] - displs[rank]
-            blocks.append(self.__array.index_select(s, mine.to(dev)))
-        my_lo, my_hi = out_bounds[rank]
-        my_owner = owner[my_lo:my_hi]
-        for r in range(p):
-            sh = list(base)
-            sh[s] = int((my_owner == r).sum())
-            shapes.append(tuple(sh))
-        parts = self.comm.exchange(blocks, shapes)
-        sh = list(base)
-        sh[s] = my_hi - my_lo
-        out = torch.empty(sh, dtype=self.__array.dtype, device=dev)
-        for r in range(p):
-            pos = torch.nonzero(my_owner == r).reshape(-1).to(dev)
-            if pos.numel():
-                out.index_copy_(s, pos, parts[r])
+        owner = owner.to(dev)
+        req = req.to(dev)
+        order = torch.argsort(owner, stable=True)
+        send_n = torch.bincount(owner, minlength=p)
+        nmat = self.comm.allgather_tensor(send_n.reshape(1, -1), axis=0)
+        recv_n = nmat[:, rank].tolist()
+        send_l = send_n.tolist()
+        incoming = self.comm.exchange(list(torch.split(req[order], send_l)), [(c,) for c in recv_n])
+        replies = [serve(t).to(dtype) for t in incoming]
+        back = self.comm.exchange(replies, [(c,) + tuple(item_shape) for c in send_l])
+        vals = torch.cat(back, dim=0) if back else torch.empty((0,) + tuple(item_shape), dtype=dtype, device=dev)
+        out = torch.empty_like(vals)
+        out[order] = vals
         return out
 
-    def __setitem__(self, key, value):
-        from . import factories
+    def _owners(self, gidx: torch.Tensor) -> torch.Tensor:
+        counts, displs = self.counts_displs()
+        bounds = torch.tensor([d + c for d, c in zip(displs, counts)], dtype=torch.int64, device=gidx.device)
+        return torch.bucketize(gidx, bounds, right=True)
 
+    def _fetch_rows(self, gidx: torch.Tensor) -> torch.Tensor:
+        """Slices ``gidx`` (global indices along the split axis, rank-local request, any order)
+        stacked along the split axis in request order (owner-computes, one round trip)."""
+        s = self.split
+        a = self.__array
+        gidx = gidx.reshape(-1).to(torch.int64).to(a.device)
+        _, displs = self.counts_displs()
+        d0 = displs[self.comm.rank]
+        item = tuple(sz for i, sz in enumerate(a.shape) if i != s)
+        rows = self._serve(self._owners(gidx), gidx, lambda t: a.index_select(s, t - d0).movedim(s, 0), item, a.dtype)
+        return rows.movedim(0, s)
+
+    def _fetch_elements(self, coords: Sequence[torch.Tensor]) -> torch.Tensor:
+        """Elements at global coordinates ``coords`` (one int64 tensor per dim, rank-local
+        requests) in request order (owner-computes, one round trip)."""
+        s = self.split
+        a = self.__array
+        dev = a.device
+        coords = [c.reshape(-1).to(torch.int64).to(dev) for c in coords]
+        counts, displs = self.counts_displs()
+        owner = self._owners(coords[s])
+        # linear offset inside the owner's local block (its split extent is counts[owner])
+        lin = torch.zeros_like(coords[s])
+        cnt_t = torch.tensor(counts, dtype=torch.int64, device=dev)[owner]
+        dsp_t = torch.tensor(displs, dtype=torch.int64, device=dev)[owner]
+        for d in range(self.ndim):
+            ext = cnt_t if d == s else self.gshape[d]
+            c = coords[d] - dsp_t if d == s else coords[d]
+            lin = lin * ext + c
+        flat = a.reshape(-1)
+        return self._serve(owner, lin, lambda t: flat[t], (), a.dtype)
+
+    def __setitem__(self, key, value):
+        """Global setter. A distributed ``value`` is never gathered whole when it has the shape of
+        the selection: each rank fetches exactly the part it writes (owner-computes request/reply),
+        after at most one all-to-all resplit of the value (reference dndarray.py:1334-1549
+        redistributes the value with point-to-point chains instead)."""
+        value_d = value if isinstance(value, DNDarray) and value.is_distributed() else None
         if isinstance(value, DNDarray):
-            vt = value._gathered() if value.is_distributed() else value.larray
+            vt = None if value_d is not None else value.larray
         elif isinstance(value, torch.Tensor):
             vt = value
         elif isinstance(value, np.ndarray):
@@ -799,8 +913,17 @@ class DNDarray:
             vt = torch.tensor(value)
         else:
             vt = value
+        dev, ldt = self.__array.device, self.__array.dtype
         if isinstance(vt, torch.Tensor):
-            vt = vt.to(device=self.__array.device, dtype=self.__array.dtype)
+            vt = vt.to(device=dev, dtype=ldt)
+
+        def gathered_value():
+            return value_d._gathered().to(device=dev, dtype=ldt)
+
+        def value_rows(axis: int, gidx: torch.Tensor) -> torch.Tensor:
+            """Slices ``gidx`` of the distributed value along ``axis`` (resplit to ``axis`` first)."""
+            v = value_d if value_d.split == axis else value_d.__resplit_copy(axis)
+            return v._fetch_rows(gidx).to(device=dev, dtype=ldt)
 
         # boolean mask with the same shape
         if isinstance(key, DNDarray) and key.dtype is types.bool and key.gshape == self.gshape:
@@ -808,23 +931,29 @@ class DNDarray:
             if self.is_distributed() and key.split != self.split:
                 _, _, sl = self.comm.chunk(self.gshape, self.split)
                 mask = mask[sl]
-            mask = mask.to(self.__array.device)
+            mask = mask.to(dev)
+            if not self.is_distributed():
+                self.__array[mask] = gathered_value() if value_d is not None else vt
+                return
+            if value_d is not None and value_d.ndim == 1:
+                pos, n = self._mask_positions(mask)
+                if value_d.gshape[0] == n:
+                    self.__array[mask] = value_rows(0, pos)
+                    return
+                vt = gathered_value()
+            elif value_d is not None:
+                vt = gathered_value()
             if isinstance(vt, torch.Tensor) and vt.numel() > 1:
-                if self.is_distributed():
-                    # values are given for the global sequence of True positions
-                    n_loc = int(mask.sum())
-                    sizes = self.comm.allgather_sizes(n_loc)
-                    off = sum(sizes[: self.comm.rank])
-                    vt = vt.reshape(-1)[off: off + n_loc]
-                self.__array[mask] = vt
-            else:
-                self.__array[mask] = vt if isinstance(vt, torch.Tensor) else vt
+                # values are given for the global C-order sequence of True positions
+                pos, _ = self._mask_positions(mask)
+                vt = vt.reshape(-1)[pos]
+            self.__array[mask] = vt
             return
 
         key, adv = self._normalize_key(key)
         if not self.is_distributed():
-            dkey = tuple(k.to(self.__array.device) if isinstance(k, torch.Tensor) else k for k in key)
-            self.__array[dkey] = vt
+            dkey = tuple(k.to(dev) if isinstance(k, torch.Tensor) else k for k in key)
+            self.__array[dkey] = gathered_value() if value_d is not None else vt
             return
 
         s = self.split
@@ -835,13 +964,16 @@ class DNDarray:
         proxy = self.__torch_proxy__()
         pkey = tuple(k.cpu() if isinstance(k, torch.Tensor) else k for k in key)
         gsel = tuple(proxy[pkey].shape)
+        shaped_value = value_d is not None and tuple(value_d.gshape) == gsel
 
         if isinstance(ks, int):
             idx = ks + self.gshape[s] if ks < 0 else ks
+            if value_d is not None:
+                vt = gathered_value()  # one slice of the split axis: the owner needs all of it
             if c0 <= idx < c1:
                 lkey = list(key)
                 lkey[s] = idx - c0
-                dkey = tuple(k.to(self.__array.device) if isinstance(k, torch.Tensor) else k for k in lkey)
+                dkey = tuple(k.to(dev) if isinstance(k, torch.Tensor) else k for k in lkey)
                 self.__array[dkey] = vt
             return
 
@@ -852,51 +984,84 @@ class DNDarray:
                 return self.__setitem__(key[:s] + (idx,) + key[s + 1:], value)
             g0 = start if c0 <= start else start + ((c0 - start + step - 1) // step) * step
             g1 = min(stop, c1)
-            if g0 >= g1:
+            cnt = len(range(g0, g1, step)) if g0 < g1 else 0
+            first = (g0 - start) // step if cnt else 0
+            # position of the split dim inside the selection
+            pos = sum(1 for k in key[:s] if not isinstance(k, int))
+            if shaped_value:
+                vt_l = value_rows(pos, torch.arange(first, first + cnt, dtype=torch.int64))
+            else:
+                if value_d is not None:
+                    vt = gathered_value()
+                if cnt == 0:
+                    return
+                if isinstance(vt, torch.Tensor) and vt.dim() > 0:
+                    vfull = vt.expand(gsel) if vt.shape != gsel else vt
+                    vt_l = vfull.narrow(pos, first, cnt)
+                else:
+                    vt_l = vt
+            if cnt == 0:
                 return
             lkey = list(key)
             lkey[s] = slice(g0 - c0, g1 - c0, step)
-            if isinstance(vt, torch.Tensor) and vt.dim() > 0:
-                vfull = vt.expand(gsel) if vt.shape != gsel else vt
-                # position of the split dim inside the selection
-                pos = sum(1 for k in key[:s] if not isinstance(k, int))
-                first = (g0 - start) // step
-                cnt = len(range(g0, g1, step))
-                vt_l = vfull.narrow(pos, first, cnt)
-            else:
-                vt_l = vt
             self.__array[tuple(lkey)] = vt_l
             return
 
-        # advanced indexing along / around the split axis
-        if isinstance(ks, torch.Tensor) and ks.dtype != torch.bool:
+        n_adv = sum(1 for k in key if isinstance(k, torch.Tensor))
+        # one integer index array along the split axis (the other keys basic)
+        if isinstance(ks, torch.Tensor) and ks.dtype != torch.bool and n_adv == 1 and ks.dim() == 1:
             idx = ks.to(torch.int64).reshape(-1)
             idx = torch.where(idx < 0, idx + self.gshape[s], idx)
             mine = ((idx >= c0) & (idx < c1)).nonzero().reshape(-1)
+            pos = sum(1 for k in key[:s] if not isinstance(k, int))
+            if shaped_value:
+                vt_l = value_rows(pos, mine)
+            elif value_d is not None:
+                vt = gathered_value()
             if mine.numel() == 0:
                 return
             lkey = list(key)
-            lkey[s] = (idx[mine] - c0).to(self.__array.device)
-            n_adv = sum(1 for k in key if isinstance(k, torch.Tensor))
-            for i, k in enumerate(key):
-                if i != s and isinstance(k, torch.Tensor):
-                    kk = k.reshape(-1)
-                    lkey[i] = kk[mine].to(self.__array.device) if kk.numel() == idx.numel() else kk.to(self.__array.device)
-            if isinstance(vt, torch.Tensor) and vt.dim() > 0:
-                vfull = vt.expand(gsel) if vt.shape != gsel else vt
-                adv_pos = min(i for i, k in enumerate(key) if isinstance(k, torch.Tensor))
-                pos = sum(1 for k in key[:adv_pos] if not isinstance(k, int)) if n_adv == 1 else 0
-                vt_l = vfull.index_select(pos, mine.to(vfull.device))
-            else:
-                vt_l = vt
+            lkey[s] = (idx[mine] - c0).to(dev)
+            if not shaped_value:
+                if isinstance(vt, torch.Tensor) and vt.dim() > 0:
+                    vfull = vt.expand(gsel) if vt.shape != gsel else vt
+                    vt_l = vfull.index_select(pos, mine.to(vfull.device))
+                else:
+                    vt_l = vt
             self.__array[tuple(lkey)] = vt_l
             return
 
-        # fallback: gather, assign, re-chunk
-        full = self._gathered().clone()
-        dkey = tuple(k.to(full.device) if isinstance(k, torch.Tensor) else k for k in key)
-        full[dkey] = vt
-        self.__array = full.narrow(s, c0, c1 - c0).clone()
+        # general case (several index arrays, masks): owner-computes over the selection. Each
+        # rank finds the selected elements that live in its block and writes them; values come
+        # from the (broadcast) local value or are fetched from the distributed value.
+        ckey = tuple(k.cpu() if isinstance(k, torch.Tensor) else k for k in key)
+        coords = []
+        for d in range(self.ndim):
+            shp = [1] * self.ndim
+            shp[d] = -1
+            coords.append(torch.arange(self.gshape[d]).view(shp).expand(self.gshape)[ckey].reshape(-1))
+        sel_lin = torch.arange(coords[0].numel() if coords else 1, dtype=torch.int64)
+        mine = (coords[s] >= c0) & (coords[s] < c1)
+        lin_mine = sel_lin[mine]
+        if shaped_value:
+            vcoords = list(torch.unravel_index(lin_mine, gsel)) if len(gsel) else []
+            vals = value_d._fetch_elements(vcoords).to(device=dev, dtype=ldt)
+        else:
+            if value_d is not None:
+                vt = gathered_value()
+            if isinstance(vt, torch.Tensor) and vt.dim() > 0:
+                vals = vt.expand(gsel).reshape(-1)[lin_mine.to(dev)]
+            else:
+                vals = vt
+        if lin_mine.numel() == 0:
+            return
+        lidx = tuple((coords[d][mine] - (c0 if d == s else 0)).to(dev) for d in range(self.ndim))
+        self.__array[lidx] = vals
+
+    def __resplit_copy(self, axis: int) -> "DNDarray":
+        from .manipulations import resplit
+
+        return resplit(self, axis)
 
     # ------------------------------------------------------------------ in-place arithmetic helpers
     def __iadd__(self, other):

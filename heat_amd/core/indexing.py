@@ -19,10 +19,19 @@ def nonzero(x: DNDarray) -> DNDarray:
         raise TypeError("Input must be a DNDarray, is {}".format(type(x)))
     t = x.larray
     nz = torch.nonzero(t, as_tuple=False)
+    balanced = None
     if x.is_distributed():
         counts, displs = x.counts_displs()
         nz[:, x.split] += displs[x.comm.rank]
-        total = x.comm.allreduce(int(nz.shape[0]), MPI.SUM)
+        if x.split == 0:
+            # rank blocks are already in C order: keep the local rows (unbalanced, no traffic)
+            total = x.comm.allreduce(int(nz.shape[0]), MPI.SUM)
+        else:
+            # split > 0: rank order is not C order - place every row at its global C position
+            # (per-outer-index counts + one exchange; the reference returns rank order here)
+            pos, total = x._mask_positions(t != 0)
+            nz = x._place_by_position(nz, pos, total)
+            balanced = True
         split = 0
     else:
         total = int(nz.shape[0])
@@ -32,7 +41,8 @@ def nonzero(x: DNDarray) -> DNDarray:
         gshape = (total,)
     else:
         gshape = (total, x.ndim)
-    return DNDarray(nz, gshape, types.int64, split, x.device, x.comm, None if split is not None else True)
+    return DNDarray(nz, gshape, types.int64, split, x.device, x.comm,
+                    balanced if split is not None else True)
 
 
 def where(cond: DNDarray, x=None, y=None) -> DNDarray:

@@ -1,0 +1,248 @@
+"""
+Edge-case checks run at every world size of ``tests/test_distributed.py`` (1..8 ranks):
+
+* empty ranks - arrays whose split extent is smaller than the world size (``p > gshape[split]``),
+  so some ranks hold a (.., 0, ..) block. Reductions along other axes must keep the empty block,
+  reductions along the split must not see phantom rows (ref ``_operations.py:401``);
+* C-order of boolean-mask selection / ``nonzero`` on split > 0 arrays with data whose order
+  would expose rank-block concatenation;
+* owner-computes advanced indexing and ``__setitem__`` with distributed values (no gathers).
+
+Every check compares against NumPy on the same global data.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import heat_amd as ht
+
+from .dist_checks import assert_array_equal, for_splits
+
+
+def _small_shapes():
+    # split extents 1..3: at p >= 4 some ranks are empty for every split axis
+    return [(3, 5), (5, 2), (2, 3, 4), (1, 6), (4, 1, 3)]
+
+
+def check_empty_rank_reductions():
+    rng = np.random.default_rng(11)
+    for shp in _small_shapes():
+        a = rng.standard_normal(shp)
+        for s in for_splits(a):
+            A = ht.array(a, split=s)
+            assert_array_equal(ht.sum(A), a.sum())
+            assert_array_equal(ht.max(A), a.max())
+            assert_array_equal(ht.min(A), a.min())
+            assert_array_equal(ht.prod(A), a.prod())
+            for ax in range(a.ndim):
+                assert_array_equal(ht.sum(A, axis=ax), a.sum(axis=ax))
+                assert_array_equal(ht.max(A, axis=ax), a.max(axis=ax))
+                assert_array_equal(ht.min(A, axis=ax), a.min(axis=ax))
+                assert_array_equal(ht.prod(A, axis=ax), a.prod(axis=ax))
+                assert_array_equal(ht.sum(A, axis=ax, keepdim=True), a.sum(axis=ax, keepdims=True))
+                assert_array_equal(ht.argmax(A, axis=ax), a.argmax(axis=ax))
+                assert_array_equal(ht.argmin(A, axis=ax), a.argmin(axis=ax))
+                assert_array_equal(ht.cumsum(A, axis=ax), a.cumsum(axis=ax))
+                assert_array_equal(ht.cumprod(A, axis=ax), a.cumprod(axis=ax))
+                assert_array_equal(ht.all(A > -10, axis=ax), (a > -10).all(axis=ax))
+                assert_array_equal(ht.any(A > 1, axis=ax), (a > 1).any(axis=ax))
+            assert ht.argmax(A).item() == a.argmax()
+            assert ht.argmin(A).item() == a.argmin()
+            # chained: a reduction along a non-split axis followed by one along the split
+            if a.ndim == 2:
+                assert_array_equal(ht.sum(ht.max(A, axis=1)), a.max(axis=1).sum())
+                assert_array_equal(ht.min(ht.sum(A, axis=0)), a.sum(axis=0).min())
+
+
+def check_empty_rank_moments():
+    rng = np.random.default_rng(12)
+    for shp in _small_shapes():
+        a = rng.standard_normal(shp)
+        for s in for_splits(a):
+            A = ht.array(a, split=s)
+            assert_array_equal(ht.mean(A), a.mean())
+            assert_array_equal(ht.var(A), a.var())
+            assert_array_equal(ht.std(A, ddof=1), a.std(ddof=1) if a.size > 1 else np.nan)
+            for ax in range(a.ndim):
+                assert_array_equal(ht.mean(A, axis=ax), a.mean(axis=ax))
+                assert_array_equal(ht.var(A, axis=ax), a.var(axis=ax))
+                if a.shape[ax] > 1:
+                    assert_array_equal(ht.std(A, axis=ax, ddof=1), a.std(axis=ax, ddof=1))
+            if a.ndim == 2:
+                assert_array_equal(ht.median(A, axis=0), np.median(a, axis=0))
+                assert_array_equal(ht.median(A), np.median(a))
+                assert_array_equal(ht.percentile(A, 30.0), np.percentile(a, 30.0), rtol=1e-6)
+
+
+def check_empty_rank_manipulations():
+    rng = np.random.default_rng(13)
+    for shp in _small_shapes():
+        a = rng.standard_normal(shp)
+        ai = rng.integers(0, 3, size=shp)
+        for s in for_splits(a):
+            A = ht.array(a, split=s)
+            for ax in range(a.ndim):
+                v, _ = ht.sort(A, axis=ax)
+                assert_array_equal(v, np.sort(a, axis=ax))
+            u = ht.unique(ht.array(ai, split=s), sorted=True)
+            assert_array_equal(u, np.unique(ai))
+            assert_array_equal(ht.resplit(A, None), a)
+            for t in range(a.ndim):
+                assert_array_equal(ht.resplit(A, t), a)
+            assert_array_equal(ht.flip(A, 0), np.flip(a, 0))
+            assert_array_equal(ht.roll(A, 1, axis=0), np.roll(a, 1, axis=0))
+            assert_array_equal(ht.reshape(A, (-1,), new_split=0), a.reshape(-1))
+            assert_array_equal(ht.concatenate([A, A], axis=0), np.concatenate([a, a], axis=0))
+            assert_array_equal(A.T if a.ndim == 2 else ht.transpose(A), a.T)
+            B = A.copy()
+            B.balance_()
+            assert_array_equal(B, a)
+
+
+def check_empty_rank_indexing():
+    rng = np.random.default_rng(14)
+    for shp in _small_shapes():
+        a = rng.standard_normal(shp)
+        for s in for_splits(a):
+            A = ht.array(a, split=s)
+            assert_array_equal(A[0], a[0])
+            assert_array_equal(A[-1], a[-1])
+            assert_array_equal(A[1:], a[1:], check_split_chunks=False)
+            assert_array_equal(A[A > 0], a[a > 0], check_split_chunks=False)
+            assert_array_equal(ht.nonzero(A > 0), np.argwhere(a > 0), check_split_chunks=False)
+            B = ht.array(a, split=s)
+            B[B > 0] = 0.0
+            b = a.copy()
+            b[b > 0] = 0.0
+            assert_array_equal(B, b)
+            B[0] = 7.0
+            b[0] = 7.0
+            assert_array_equal(B, b)
+            B[..., -1] = -3.0
+            b[..., -1] = -3.0
+            assert_array_equal(B, b)
+
+
+def check_empty_rank_linalg():
+    rng = np.random.default_rng(15)
+    for m, k, n in [(3, 2, 5), (2, 6, 3), (1, 3, 1), (5, 1, 2)]:
+        a = rng.standard_normal((m, k))
+        b = rng.standard_normal((k, n))
+        for sa in (None, 0, 1):
+            for sb in (None, 0, 1):
+                C = ht.matmul(ht.array(a, split=sa), ht.array(b, split=sb))
+                assert_array_equal(C, a @ b, rtol=1e-5, atol=1e-8, check_split_chunks=False)
+        for s in (None, 0, 1):
+            A = ht.array(a, split=s)
+            for ordv in (None, "fro", 1, -1, np.inf, -np.inf):
+                got = ht.linalg.matrix_norm(A, ord=ordv) if ordv is not None else ht.linalg.norm(A)
+                exp = np.linalg.norm(a, ord=ordv)
+                assert abs(float(got.item()) - exp) < 1e-8 * max(1.0, abs(exp)), (ordv, s, got, exp)
+            v = rng.standard_normal(k)
+            assert_array_equal(ht.matmul(A, ht.array(v, split=0)), a @ v, check_split_chunks=False)
+            assert abs(float(ht.linalg.trace(A)) - np.trace(a)) < 1e-10
+            x = rng.standard_normal(m)
+            X = ht.array(x, split=0)
+            assert abs(ht.dot(X, X).item() - x @ x) < 1e-10
+            assert abs(ht.linalg.vector_norm(X).item() - np.linalg.norm(x)) < 1e-10
+
+
+# ---------------------------------------------------------------------------------------------
+def check_mask_order_split_gt0():
+    """Data whose values equal their C-order position: any rank-order concatenation shows."""
+    for shp in [(3, 4), (2, 5, 3), (6, 7), (1, 9)]:
+        a = np.arange(int(np.prod(shp))).reshape(shp)
+        for s in for_splits(a):
+            A = ht.array(a, split=s)
+            for t in (2, 5, 11):
+                assert_array_equal(A[A > t], a[a > t], check_split_chunks=False)
+                assert_array_equal(A[(A % 3) == 0], a[(a % 3) == 0], check_split_chunks=False)
+                assert_array_equal(ht.nonzero(A > t), np.argwhere(a > t), check_split_chunks=False)
+            # masked assignment with an array value in C order of the True positions
+            B = ht.array(a, split=s)
+            msk = a % 2 == 1
+            vals = -np.arange(int(msk.sum()))
+            B[B % 2 == 1] = ht.array(vals, split=0)
+            b = a.copy()
+            b[msk] = vals
+            assert_array_equal(B, b)
+            B = ht.array(a, split=s)
+            B[B % 2 == 1] = ht.array(vals)  # replicated value
+            assert_array_equal(B, b)
+
+
+def check_advanced_indexing_owner_computes():
+    rng = np.random.default_rng(16)
+    a = rng.standard_normal((7, 6, 5))
+    idx0 = np.array([6, 0, 3, 3, 1])
+    idx1 = np.array([5, 2, 0, 1, 4])
+    for s in for_splits(a):
+        A = ht.array(a, split=s)
+        assert_array_equal(A[idx0, idx1], a[idx0, idx1], check_split_chunks=False)
+        assert_array_equal(A[idx0, :, idx1[:5] % 5], a[idx0, :, idx1[:5] % 5], check_split_chunks=False)
+        assert_array_equal(A[:, idx1, 2], a[:, idx1, 2], check_split_chunks=False)
+        assert_array_equal(A[idx0[:, None], idx1[None, :3]], a[idx0[:, None], idx1[None, :3]],
+                           check_split_chunks=False)
+        m2 = a[:, :, 0] > 0
+        assert_array_equal(A[m2], a[m2], check_split_chunks=False)
+        assert_array_equal(A[2, idx1], a[2, idx1], check_split_chunks=False)
+
+
+def check_setitem_distributed_value():
+    rng = np.random.default_rng(17)
+    a = rng.standard_normal((9, 6))
+    for s in for_splits(a):
+        for vs in (None, 0, 1):
+            # slice along the split axis with a distributed value of the selection's shape
+            A = ht.array(a, split=s)
+            v = rng.standard_normal((5, 6))
+            A[2:7] = ht.array(v, split=vs)
+            b = a.copy()
+            b[2:7] = v
+            assert_array_equal(A, b)
+            A = ht.array(a, split=s)
+            w = rng.standard_normal((9, 3))
+            A[:, 1:4] = ht.array(w, split=vs)
+            b = a.copy()
+            b[:, 1:4] = w
+            assert_array_equal(A, b)
+            A = ht.array(a, split=s)
+            A[::2, ::3] = ht.array(rng.standard_normal((5, 2)), split=vs) * 0 + 1.5
+            b = a.copy()
+            b[::2, ::3] = 1.5
+            assert_array_equal(A, b)
+            # integer index arrays
+            A = ht.array(a, split=s)
+            idx = np.array([8, 1, 4])
+            u = rng.standard_normal((3, 6))
+            A[idx] = ht.array(u, split=vs)
+            b = a.copy()
+            b[idx] = u
+            assert_array_equal(A, b)
+            A = ht.array(a, split=s)
+            A[idx, np.array([0, 5, 2])] = ht.array(np.array([1.0, 2.0, 3.0]), split=None if vs == 1 else vs)
+            b = a.copy()
+            b[idx, np.array([0, 5, 2])] = [1.0, 2.0, 3.0]
+            assert_array_equal(A, b)
+        # broadcast value (local), the general path
+        A = ht.array(a, split=s)
+        A[np.array([0, 3]), np.array([1, 2])] = 9.0
+        b = a.copy()
+        b[np.array([0, 3]), np.array([1, 2])] = 9.0
+        assert_array_equal(A, b)
+
+
+def check_different_split_binary_ops():
+    """Intentional extension: operands split along different axes are aligned with one
+    all-to-all (the reference raises NotImplementedError, ``_operations.py:104-107``)."""
+    rng = np.random.default_rng(18)
+    a = rng.standard_normal((6, 5, 4))
+    b = rng.standard_normal((6, 5, 4))
+    for sa in range(3):
+        for sb in range(3):
+            C = ht.array(a, split=sa) * ht.array(b, split=sb)
+            assert C.split == sa
+            assert_array_equal(C, a * b)
+    # broadcast operand of lower rank with a different split
+    c = rng.standard_normal((5, 4))
+    assert_array_equal(ht.array(a, split=0) + ht.array(c, split=1), a + c)

@@ -1,11 +1,12 @@
 """Every distributed check also runs in a world of one (in-process, CPU)."""
 import pytest
 
-from . import dist_checks
+from . import dist_checks, dist_checks_edge
 
-CHECKS = [n for n in dir(dist_checks) if n.startswith("check_")]
+CASES = [(mod, n) for mod in (dist_checks, dist_checks_edge) for n in dir(mod)
+         if n.startswith("check_") and getattr(mod, n).__module__ == mod.__name__]
 
 
-@pytest.mark.parametrize("name", CHECKS)
-def test_local(name):
-    getattr(dist_checks, name)()
+@pytest.mark.parametrize("mod,name", CASES, ids=[n for _, n in CASES])
+def test_local(mod, name):
+    getattr(mod, name)()

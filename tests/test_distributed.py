@@ -1,26 +1,31 @@
-"""The same checks in 2 and 3 gloo ranks (the reference runs its suite under mpirun -n 1..8).
+"""The same checks in 2, 3, 4, 5 and 8 gloo ranks (the reference runs its whole suite under
+``mpirun -n 1..8``, Jenkinsfile:19-26; the world of one runs in ``test_core_local.py``).
 
-All checks of one world size run in ONE multi-rank job (interpreter start-up dominated the
-per-check runs); a failing check is re-run alone in a fresh job to report a clean traceback."""
+All checks of one (module, world size) run in ONE multi-rank job (interpreter start-up dominated
+the per-check runs); a failing check is re-run alone in a fresh job to report a clean traceback."""
 import pytest
 
-from . import dist_checks
+from . import dist_checks, dist_checks_edge
 from ._dist import run_distributed, run_distributed_batch
 
-CHECKS = [n for n in dir(dist_checks) if n.startswith("check_")]
+MODULES = {"tests.dist_checks": dist_checks, "tests.dist_checks_edge": dist_checks_edge}
+CASES = [(m, n) for m, mod in MODULES.items() for n in dir(mod) if n.startswith("check_")
+         and getattr(getattr(mod, n), "__module__", m) == m]
 _BATCH = {}
 
 
-def _batch(nprocs):
-    if nprocs not in _BATCH:
-        _BATCH[nprocs] = run_distributed_batch("tests.dist_checks", CHECKS, nprocs)
-    return _BATCH[nprocs]
+def _batch(module, nprocs):
+    key = (module, nprocs)
+    if key not in _BATCH:
+        names = [n for m, n in CASES if m == module]
+        _BATCH[key] = run_distributed_batch(module, names, nprocs)
+    return _BATCH[key]
 
 
-@pytest.mark.parametrize("nprocs", [2, 3])
-@pytest.mark.parametrize("name", CHECKS)
-def test_distributed(name, nprocs):
-    ok, err = _batch(nprocs)[name]
+@pytest.mark.parametrize("nprocs", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("module,name", CASES)
+def test_distributed(module, name, nprocs):
+    ok, err = _batch(module, nprocs)[name]
     if not ok:
-        run_distributed("tests.dist_checks:" + name, nprocs)  # raises with the full per-rank log
+        run_distributed(module + ":" + name, nprocs)  # raises with the full per-rank log
         pytest.fail("check {} failed in the batched job but passed alone:\n{}".format(name, err))
