@@ -19,6 +19,7 @@ import torch
 
 from . import factories, types
 from . import _sample_sort
+from .. import ops
 from .communication import MPI
 from .dndarray import DNDarray, _chunk_counts, _partition_bounds
 from .stride_tricks import broadcast_shape, sanitize_axis, sanitize_shape
@@ -903,7 +904,9 @@ def topk(a: DNDarray, k: int, dim: int = -1, largest: bool = True, sorted: bool 
     (replaces the reference's custom MPI_TOPK reduction, manipulations.py:3997)."""
     dim = sanitize_axis(a.gshape, dim)
     if not a.is_distributed() or dim != a.split:
-        vals, idx = torch.topk(a.larray, k, dim=dim, largest=largest, sorted=sorted)
+        native = ops.topk_rows(a.larray, k, dim, largest)   # one wave per row (csrc/select.hip)
+        vals, idx = native if native is not None else torch.topk(a.larray, k, dim=dim, largest=largest,
+                                                                 sorted=sorted)
         gshape = list(a.gshape)
         gshape[dim] = k
         v = DNDarray(vals, tuple(gshape), a.dtype, a.split, a.device, a.comm, a.balanced)
@@ -912,8 +915,12 @@ def topk(a: DNDarray, k: int, dim: int = -1, largest: bool = True, sorted: bool 
         counts, displs = a.counts_displs()
         me = a.comm.rank
         kl = min(k, counts[me])
-        vals, idx = torch.topk(a.larray, kl, dim=dim, largest=largest, sorted=True)
-        idx = idx + displs[me]
+        native = ops.topk_rows(a.larray, kl, dim, largest, displs[me]) if kl > 0 else None
+        if native is not None:
+            vals, idx = native
+        else:
+            vals, idx = torch.topk(a.larray, kl, dim=dim, largest=largest, sorted=True)
+            idx = idx + displs[me]
         # pad to k with sentinel values so every rank contributes k candidates
         if kl < k:
             sh = list(vals.shape)

@@ -235,7 +235,9 @@ def _argext(x: DNDarray, axis, out, largest: bool, keepdim: bool = False):
     axis = sanitize_axis(x.gshape, axis)
     t = x.larray
     fn = torch.argmax if largest else torch.argmin
-    if axis is None:
+    if t.is_cuda and x.gnumel and ops.argreduce_supported(t, x.gnumel if axis is None else x.gshape[axis]):
+        r = _argext_native(x, axis, largest, keepdim)
+    elif axis is None:
         if x.is_distributed():
             counts, displs = x.counts_displs()
             me = x.comm.rank
@@ -302,6 +304,37 @@ def _argext(x: DNDarray, axis, out, largest: bool, keepdim: bool = False):
         out.larray = r.larray.to(out.larray.dtype)
         return out
     return r
+
+
+def _argext_native(x: DNDarray, axis, largest: bool, keepdim: bool) -> DNDarray:
+    """Device arg-reduction through packed (value, first index) int64 keys (``csrc/select.hip``):
+    one local kernel, and along the split axis ONE int64 MAX all-reduce of the keys (the
+    reference all-reduces a pickled custom op, statistics.py:1139-1207)."""
+    t = x.larray
+    dist_split = x.is_distributed()
+    displ = x.counts_displs()[1][x.comm.rank] if dist_split else 0
+    if axis is None:
+        keys = ops.argreduce_keys(t, None, not largest, displ, x.gshape[x.split] if dist_split else None,
+                                   x.split if dist_split else None)
+        if dist_split:
+            x.comm.Allreduce(MPI.IN_PLACE, keys, MPI.MAX)
+        gshape = (1,) * x.ndim if keepdim else ()
+        res = ops.argreduce_decode(keys).reshape(gshape)
+        return DNDarray(res, gshape, types.int64, None, x.device, x.comm, True)
+    along_split = dist_split and axis == x.split
+    keys = ops.argreduce_keys(t, axis, not largest, displ if along_split else 0)
+    if along_split:
+        x.comm.Allreduce(MPI.IN_PLACE, keys, MPI.MAX)
+    res = ops.argreduce_decode(keys)
+    if keepdim:
+        res = res.unsqueeze(axis)
+        gshape = tuple(1 if i == axis else s for i, s in enumerate(x.gshape))
+    else:
+        gshape = tuple(s for i, s in enumerate(x.gshape) if i != axis)
+    if along_split or x.split is None:
+        return DNDarray(res, gshape, types.int64, None, x.device, x.comm, True)
+    split = x.split if (keepdim or x.split < axis) else x.split - 1
+    return DNDarray(res, gshape, types.int64, split, x.device, x.comm, x.balanced)
 
 
 def argmax(x: DNDarray, axis: Optional[int] = None, out: Optional[DNDarray] = None, **kwargs) -> DNDarray:

@@ -13,11 +13,16 @@
 // slots: a rank writes a slot again two calls later, after a barrier for which every peer's block b
 // already finished reading it (kernels of one stream are ordered). Epochs only grow, and waits use
 // ">=", so a fast peer announcing the next epoch cannot starve a slow waiter.
-// Spins are bounded: on timeout the block records an error word in its own signal buffer and
-// continues (wrong sums, no hang); callers check it.
+// Spins are bounded: on timeout the block records an error word in its own signal buffer, fills
+// its output slice with NaN (floating types; the stale sum is never returned silently) and exits
+// (no hang). ha_ipc_error_async copies the word into pinned host memory behind every call; the
+// host raises at the next call (or at an explicit check) and the communicator is poisoned, since
+// the two-slot reuse argument no longer holds after a missed barrier.
 #include "common.h"
 
 #include <cstring>
+#include <limits>
+#include <type_traits>
 
 namespace {
 
@@ -30,10 +35,19 @@ struct PeerPtrs {
   unsigned* sig[IPC_MAX_RANKS];
 };
 
+template <typename T>
+__device__ __forceinline__ T poison() {
+  if constexpr (std::is_integral<T>::value) return std::numeric_limits<T>::min();  // an implausible sum
+  else return std::numeric_limits<T>::quiet_NaN();
+}
+
 template <typename T, int W>
 __global__ __launch_bounds__(256) void ipc_allreduce(PeerPtrs pp, int rank, T* __restrict__ buf, int64_t n,
                                                      int64_t chunk, int64_t slot_off, unsigned epoch,
                                                      int64_t max_spins) {
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  __syncthreads();
   const int b = blockIdx.x;
   const int64_t lo = (int64_t)b * chunk;
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
@@ -50,6 +64,7 @@ __global__ __launch_bounds__(256) void ipc_allreduce(PeerPtrs pp, int rank, T* _
     while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (++spins > max_spins) {
         __hip_atomic_store(pp.sig[rank] + IPC_ERR_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -57,6 +72,11 @@ __global__ __launch_bounds__(256) void ipc_allreduce(PeerPtrs pp, int rank, T* _
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
+  if (timed_out) {
+    // a peer never arrived: poison this block's output instead of summing stale slots
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) buf[i] = poison<T>();
+    return;
+  }
   const T* src[W];
 #pragma unroll
   for (int r = 0; r < W; ++r) src[r] = reinterpret_cast<const T*>(pp.data[r]) + slot_off;
@@ -141,6 +161,13 @@ HA_EXPORT int ha_ipc_allreduce(void* const* data, void* const* sig, int world, i
     case 2: return launch<int64_t>(pp, world, rank, (int64_t*)buf, n, slot_off, epoch, blocks, max_spins, s);
     default: return HA_UNSUPPORTED;
   }
+}
+
+// Stream-ordered copy of the error word into host memory (pinned, or any host pointer the runtime
+// can DMA to) behind the calls already on ``stream``.
+HA_EXPORT int ha_ipc_error_async(void* sig, void* host, void* stream) {
+  unsigned* w = reinterpret_cast<unsigned*>(sig) + IPC_ERR_WORD;
+  return hipMemcpyAsync(host, w, 4, hipMemcpyDeviceToHost, (hipStream_t)stream) == hipSuccess ? HA_OK : HA_LAUNCH;
 }
 
 // Error word of this rank's signal buffer (1 after a barrier timed out); reset with clear != 0.

@@ -4,13 +4,17 @@
 //
 // Points are scaled per row by a power of two s_x (max |x_i| in [0.5, 1)) and split once per fit
 // into fp16 hi = fp16(x s_x), lo = fp16(x s_x - hi) ("planes", cached across Lloyd iterations by
-// the caller).  Centroids use ONE power-of-two scale s_C for all of them and are packed per
-// iteration into the MFMA A-fragment image.  Per (point, centroid):
+// the caller).  Centroids get their OWN power-of-two scale s_c (max |c_i| s_c in [0.5, 1)) and are
+// packed per iteration into the MFMA A-fragment image. Per (point, centroid):
 //     D = hi_c.hi_x + hi_c.lo_x + lo_c.hi_x           (three MFMAs, fp32 accumulation)
-//       = s_x s_C x.c  up to ~3 * 2^-22 relative per product term
-//   argmin_c |c|^2 - 2 x.c  =  argmax_c  D - s_x * u_c,   u_c = s_C |c|^2 / 2
-// so the epilogue is one (packed) FMA per pair, a 16-way max per 32-centroid tile and a select
-// that keeps the best tile's 16 values; the index is searched once per point at the end.
+//       = s_x s_c x.c  up to ~3 * 2^-22 relative per product term
+//   argmin_c |c|^2 - 2 x.c  =  argmax_c  D r_c - s_x u_c,   r_c = 1 / s_c,  u_c = |c|^2 / 2
+// (r_c is a power of two, so D r_c is exact). The per-centroid scale keeps every centroid's hi/lo
+// split at full fp16 precision however different the centroid norms are: with one shared scale a
+// centroid 2^-e smaller than the largest one had its lo term pushed into (or below) fp16's
+// subnormal range, losing up to e bits of its own products. The epilogue is one packed multiply
+// + one packed FMA per pair, a 16-way max per 32-centroid tile and a select that keeps the best
+// tile's 16 values; the index is searched once per point at the end.
 //
 // Layout and orientation follow km_assign (kmeans.hip): centroids = A (rows), points = B
 // (columns), the K dimension is permuted so lane half h owns features [h*F2, h*F2 + F2) of its
@@ -72,66 +76,82 @@ __global__ __launch_bounds__(256) void h3_pack_points(const float* __restrict__ 
   if (grp == 0) sx[row] = s;
 }
 
-// Centroid packing in two short launches (a single-workgroup version took 90 us at k=1024):
-// h3_cmax: max |c| over all centroids -> meta[1] (float bits, atomicMax on a zeroed word; valid
-// for non-negative floats); h3_pack_centroids: s_C = 2^-e from it, the packed image
+// Centroid packing in two short launches. h3_cscale: per centroid (FPAD/8 lanes, 8 features each)
+// max |c_i| and |c|^2 -> ur[chunk][0:CB) = u_c = |c|^2 / 2 (+inf for padding rows) and
+// ur[chunk][CB:2CB) = r_c = 2^e (max |c_i| 2^-e in [0.5, 1); 1 for zero / padding rows), plus
+// meta[1] = max_c max_i |c_i| and meta[2] = max_c u_c (float bits, atomicMax on zeroed words: valid
+// for non-negative floats; used by the certified filter's error bound). u and r of one chunk are
+// adjacent so ONE LDS-DMA instruction stages both. h3_pack_centroids: the packed image
 //   image[chunk][cb][ks][hl][lane][8] (lane = h*32 + j, centroid chunk*CB + cb*32 + j,
-//   features h*F2 + 8 ks .. +8), u[c] = s_C |c|^2 / 2 (+inf for padding) and meta[0] = s_C.
-__global__ __launch_bounds__(256) void h3_cmax(const float* __restrict__ C, int k, int f, int64_t ldc,
-                                               float* __restrict__ meta) {
-  float mx = 0.f;
-  const int64_t total = (int64_t)k * f;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256)
-    mx = fmaxf(mx, fabsf(C[(e / f) * ldc + e % f]));
+//   features h*F2 + 8 ks .. +8) of c * s_c split into fp16 hi / lo.
+template <int FPAD>
+__global__ __launch_bounds__(256) void h3_cscale(const float* __restrict__ C, int k, int f, int64_t ldc, int kpad,
+                                                 float* __restrict__ ur, float* __restrict__ meta) {
+  constexpr int G8 = FPAD / 8;  // lanes per centroid (divides 64)
+  constexpr int CB = H3Cfg<FPAD>::CB;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = (int)(t / G8), g8 = (int)(t % G8);
+  const bool live = c < k;
+  float mx = 0.f, sq = 0.f;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  if ((threadIdx.x & 63) == 0 && mx > 0.f && mx < __builtin_huge_valf())
+  for (int i = 0; i < 8; ++i) {
+    const int fe = g8 * 8 + i;
+    const float x = (live && fe < f) ? C[(int64_t)c * ldc + fe] : 0.f;
+    mx = fmaxf(mx, fabsf(x));
+    sq = fmaf(x, x, sq);
+  }
+#pragma unroll
+  for (int o = 1; o < G8; o <<= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    sq += __shfl_xor(sq, o, 64);
+  }
+  if (g8 != 0 || c >= kpad) return;
+  float* urc = ur + (int64_t)(c / CB) * 2 * CB + c % CB;
+  if (!live) {
+    urc[0] = __builtin_huge_valf();
+    urc[CB] = 1.f;
+    return;
+  }
+  int e = 0;
+  if (mx > 0.f && mx < __builtin_huge_valf()) frexpf(mx, &e);
+  urc[0] = 0.5f * sq;
+  urc[CB] = ldexpf(1.f, e);
+  if (mx > 0.f && mx < __builtin_huge_valf())
     atomicMax(reinterpret_cast<unsigned int*>(meta + 1), __float_as_uint(mx));
+  if (sq > 0.f && sq < __builtin_huge_valf())
+    atomicMax(reinterpret_cast<unsigned int*>(meta + 2), __float_as_uint(0.5f * sq));
 }
 
 template <int FPAD>
 __global__ __launch_bounds__(256) void h3_pack_centroids(const float* __restrict__ C, int k, int f, int64_t ldc,
                                                          int kpad, _Float16* __restrict__ image,
-                                                         float* __restrict__ u, float* __restrict__ meta) {
+                                                         const float* __restrict__ ur) {
   using K = H3Cfg<FPAD>;
   constexpr int G8 = FPAD / 8;
-  const float mxc = meta[1];
-  int ex = 0;
-  if (mxc > 0.f) frexpf(mxc, &ex);
-  const float s = ldexpf(1.f, -ex);
   const int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (it == 0) meta[0] = s;
-  if (it < (int64_t)kpad * G8) {
-    const int c = (int)(it / G8), g8 = (int)(it % G8);
-    const int fe = g8 * 8;
-    halfx8 hi, lo;
+  if (it >= (int64_t)kpad * G8) return;
+  const int c = (int)(it / G8), g8 = (int)(it % G8);
+  const int fe = g8 * 8;
+  const float s = 1.f / ur[(int64_t)(c / K::CB) * 2 * K::CB + K::CB + c % K::CB];  // exact: a power of two
+  halfx8 hi, lo;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float x = (c < k && fe + i < f) ? C[(int64_t)c * ldc + fe + i] * s : 0.f;
-      const _Float16 h = (_Float16)x;
-      hi[i] = h;
-      lo[i] = (_Float16)(x - (float)h);
-    }
-    const int h = fe / K::F2, ks = (fe % K::F2) / 8;
-    const int chunk = c / K::CB, cb = (c % K::CB) / 32, j = c % 32;
-    const int lane = h * 32 + j;
-    const int64_t base = ((((int64_t)chunk * (K::CB / 32) + cb) * K::KS + ks) * 2) * 64 * 8;
-    *reinterpret_cast<halfx8*>(image + base + (int64_t)lane * 8) = hi;
-    *reinterpret_cast<halfx8*>(image + base + 64 * 8 + (int64_t)lane * 8) = lo;
-  } else if (it < (int64_t)kpad * (G8 + 1)) {
-    const int c = (int)(it - (int64_t)kpad * G8);
-    if (c < k) {
-      float acc = 0.f;
-      for (int i = 0; i < f; ++i) {
-        const float x = C[(int64_t)c * ldc + i];
-        acc = fmaf(x, x, acc);
-      }
-      u[c] = 0.5f * s * acc;
-      atomicMax(reinterpret_cast<unsigned int*>(meta + 2), __float_as_uint(0.5f * s * acc));  // u_max (>= 0)
-    } else {
-      u[c] = __builtin_huge_valf();
-    }
+  for (int i = 0; i < 8; ++i) {
+    const float x = (c < k && fe + i < f) ? C[(int64_t)c * ldc + fe + i] * s : 0.f;
+    const _Float16 h = (_Float16)x;
+    hi[i] = h;
+    lo[i] = (_Float16)(x - (float)h);
   }
+  const int h = fe / K::F2, ks = (fe % K::F2) / 8;
+  const int chunk = c / K::CB, cb = (c % K::CB) / 32, j = c % 32;
+  const int lane = h * 32 + j;
+  const int64_t base = ((((int64_t)chunk * (K::CB / 32) + cb) * K::KS + ks) * 2) * 64 * 8;
+  *reinterpret_cast<halfx8*>(image + base + (int64_t)lane * 8) = hi;
+  *reinterpret_cast<halfx8*>(image + base + 64 * 8 + (int64_t)lane * 8) = lo;
+}
+
+// the per-pair score of 2 adjacent accumulator values: s_x (x.c - |c|^2/2) = D r_c - s_x u_c
+__device__ __forceinline__ floatx2 h3_score2(floatx2 acc, floatx2 r, floatx2 u, floatx2 nsx) {
+  return __builtin_elementwise_fma(acc, r, nsx * u);
 }
 
 // Assignment kernel. A wave keeps NPB 32-point blocks (hi/lo fragments) in registers; the packed
@@ -202,10 +222,20 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
   }
 
   constexpr int PIECES = CHUNK_H * 2 / 1024;  // 1 KB (64 lanes x 16 B) per DMA instruction
+  // two chunk buffers: the epilogue of a chunk's last tile runs during the next chunk's first
+  // tile and still reads its u/r from the previous buffer
+  constexpr int BUF = CHUNK_H * 2 + CB * 8;
   floatx16 acc[2][NPB];
-  floatx4 cnr[2][4];
+  const float* pu = nullptr;  // LDS u/r of the tile whose epilogue is pending
   int ptile = -1;
-  auto epilogue = [&](const floatx16 (&ac)[NPB], const floatx4 (&cn)[4], int tile) {
+  auto epilogue = [&](const floatx16 (&ac)[NPB], const float* pu_, int tile) {
+    // u and r of the tile straight from LDS (the chunk buffer is still live: see the loop)
+    floatx4 cn[4], cr[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      cn[g] = *reinterpret_cast<const floatx4*>(pu_ + 8 * g + 4 * h);
+      cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
+    }
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb) {
       const floatx2 sx2 = {nsx[pb], nsx[pb]};
@@ -213,8 +243,9 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+        const floatx2 rc2 = {cr[q >> 1][(2 * q) & 3], cr[q >> 1][(2 * q + 1) & 3]};
         const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
-        const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+        const floatx2 r2 = h3_score2(a2, rc2, c2, sx2);
         w[2 * q] = r2[0];
         w[2 * q + 1] = r2[1];
       }
@@ -231,17 +262,18 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
   for (int ch = 0; ch < nchunks; ++ch) {
     {
       const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+      unsigned char* dst = smem + (ch & 1) * BUF;
 #pragma unroll
       for (int pc = wave; pc < PIECES; pc += 4)
         __builtin_amdgcn_global_load_lds(src + pc * 1024,
-                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
-      if (wave == 0 && lane < CB / 4)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H * 2), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 2)  // u and r of the chunk (adjacent)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H * 2), 16, 0, 0);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
-    const unsigned char* buf = smem;
+    const unsigned char* buf = smem + (ch & 1) * BUF;
     const _Float16* img = reinterpret_cast<const _Float16*>(buf);
     const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
 #pragma unroll
@@ -261,11 +293,10 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
           acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
         }
       }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) cnr[cur][g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
       // epilogue of the previous tile (independent of the MFMAs above)
-      if (ptile >= 0) epilogue(acc[cur ^ 1], cnr[cur ^ 1], ptile);
+      if (ptile >= 0) epilogue(acc[cur ^ 1], pu, ptile);
       ptile = ch * (CB / 32) + cb;
+      pu = ub + cb * 32;
 #pragma unroll
       for (int i = 0; i < 3 * KS * NPB; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
@@ -274,9 +305,8 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
     }
     __syncthreads();  // every wave is done with the buffer before the next chunk's DMA
   }
-  if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], cnr[((CB / 32) - 1) & 1], ptile);
+  if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], pu, ptile);
 
-  const float sC = meta[0];
   int bidx[NPB];
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
@@ -298,9 +328,9 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
     if (h == 0 && row >= 0) {
       labels[row] = bidx[pb];
       if (mind) {
-        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) + 2 best / (s_x s_C)
+        // |x|^2 + |c|^2 - 2 x.c = (xs_scaled / s_x^2) - 2 best / s_x
         const float isx = 1.f / sx[pb];
-        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
+        mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx, 0.f);
       }
     }
   }
@@ -368,10 +398,18 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
 
   // only the hi half of every (cb, ks) fragment pair is staged: piece 2q of the chunk -> LDS q
   constexpr int PIECES = CHUNK_H * 2 / 1024 / 2;
+  constexpr int BUF = CHUNK_H + CB * 8;  // two buffers, as in h3_assign_p
   floatx16 acc[2][NPB];
-  floatx4 cnr[2][4];
+  const float* pu = nullptr;  // LDS u/r of the tile whose epilogue is pending
   int ptile = -1;
-  auto epilogue = [&](const floatx16 (&ac)[NPB], const floatx4 (&cn)[4], int tile) {
+  auto epilogue = [&](const floatx16 (&ac)[NPB], const float* pu_, int tile) {
+    // u and r of the tile straight from LDS (the chunk buffer is still live: see the loop)
+    floatx4 cn[4], cr[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      cn[g] = *reinterpret_cast<const floatx4*>(pu_ + 8 * g + 4 * h);
+      cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
+    }
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb) {
       const floatx2 sx2 = {nsx[pb], nsx[pb]};
@@ -379,8 +417,9 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+        const floatx2 rc2 = {cr[q >> 1][(2 * q) & 3], cr[q >> 1][(2 * q + 1) & 3]};
         const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
-        const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+        const floatx2 r2 = h3_score2(a2, rc2, c2, sx2);
         w[2 * q] = r2[0];
         w[2 * q + 1] = r2[1];
       }
@@ -398,18 +437,19 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
   for (int ch = 0; ch < nchunks; ++ch) {
     {
       const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+      unsigned char* dst = smem + (ch & 1) * BUF;
 #pragma unroll
       for (int pc = wave; pc < PIECES; pc += 4)
         __builtin_amdgcn_global_load_lds(src + 2 * pc * 1024,
-                                         (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
-      if (wave == 0 && lane < CB / 4)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(smem + CHUNK_H), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 2)  // u and r of the chunk (adjacent)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H), 16, 0, 0);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
-    const _Float16* img = reinterpret_cast<const _Float16*>(smem);
-    const float* ub = reinterpret_cast<const float*>(smem + CHUNK_H);
+    const _Float16* img = reinterpret_cast<const _Float16*>(smem + (ch & 1) * BUF);
+    const float* ub = reinterpret_cast<const float*>(smem + (ch & 1) * BUF + CHUNK_H);
 #pragma unroll
     for (int cb = 0; cb < CB / 32; ++cb) {
       const int cur = cb & 1;
@@ -422,10 +462,9 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
         for (int pb = 0; pb < NPB; ++pb)
           acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
       }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) cnr[cur][g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
-      if (ptile >= 0) epilogue(acc[cur ^ 1], cnr[cur ^ 1], ptile);
+      if (ptile >= 0) epilogue(acc[cur ^ 1], pu, ptile);
       ptile = ch * (CB / 32) + cb;
+      pu = ub + cb * 32;
 #pragma unroll
       for (int i = 0; i < KS * NPB; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
@@ -434,10 +473,10 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
     }
     __syncthreads();
   }
-  if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], cnr[((CB / 32) - 1) & 1], ptile);
+  if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], pu, ptile);
 
-  const float sC = meta[0], umax = meta[2];
-  const float cmax = sqrtf(2.f * sC * umax);
+  const float umax = meta[2];
+  const float cmax = sqrtf(2.f * umax);  // max_c |c|_2 (unscaled: scores are s_x (x.c - |c|^2/2))
   int* const cnt = amb_count;
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
@@ -463,7 +502,7 @@ __global__ __launch_bounds__(256, MINB) void h1_filter(const _Float16* __restric
       bidx = oi;
     }
     const float xc = xn * cmax;
-    const float E = 1.01f * 0x1p-10f * xc + 0x1p-16f * (xc - nsx[pb] * umax) + 0x1p-16f;
+    const float E = 1.01f * 0x1p-10f * xc + 0x1p-16f * (xc - nsx[pb] * umax) + 0x1p-15f * cmax;
     const int64_t row = pbase + pb * 32 + j;
     const bool live = h == 0 && row < n;
     const bool amb = live && !(b - s2 > 2.f * E);
@@ -553,8 +592,8 @@ __global__ __launch_bounds__(256, 2) void h3_topk(const _Float16* __restrict__ p
       for (int pc = wave; pc < PIECES; pc += 4)
         __builtin_amdgcn_global_load_lds(src + pc * 1024,
                                          (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
-      if (wave == 0 && lane < CB / 4)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * CB) + lane * 16,
+      if (wave == 0 && lane < CB / 2)  // u and r of the chunk (adjacent)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
                                          (__attribute__((address_space(3))) void*)(smem + CHUNK_H * 2), 16, 0, 0);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
@@ -578,9 +617,10 @@ __global__ __launch_bounds__(256, 2) void h3_topk(const _Float16* __restrict__ p
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const floatx4 cn = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
+        const floatx4 cr = *reinterpret_cast<const floatx4*>(ub + CB + cb * 32 + 8 * g + 4 * h);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          w[4 * g + i] = fmaf(nsx, cn[i], acc[4 * g + i]);
+          w[4 * g + i] = fmaf(acc[4 * g + i], cr[i], nsx * cn[i]);
           m = fmaxf(m, w[4 * g + i]);
         }
       }
@@ -602,12 +642,12 @@ __global__ __launch_bounds__(256, 2) void h3_topk(const _Float16* __restrict__ p
   }
   const float xs = q + __shfl_xor(q, 32, 64);  // all lanes: a shuffle from an inactive lane is undefined
   if (h == 0 && p < n) {
-    const float isx = 1.f / sx, sC = meta[0];
+    const float isx = 1.f / sx;
 #pragma unroll
     for (int s = 0; s < KN; ++s)
       if (s < kout) {
         const bool ok = ti[s] >= 0;
-        dist[p * kout + s] = ok ? fmaxf(xs * isx * isx - 2.f * tv[s] * isx / sC, 0.f) : __builtin_huge_valf();
+        dist[p * kout + s] = ok ? fmaxf(xs * isx * isx - 2.f * tv[s] * isx, 0.f) : __builtin_huge_valf();
         idx[p * kout + s] = ti[s];
       }
   }
@@ -650,12 +690,11 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
       __builtin_amdgcn_global_load_lds(src + (int64_t)pc * 1024,
                                        (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
     float* us = reinterpret_cast<float*>(smem + (size_t)nch * CHUNK_H * 2);
-    for (int e = tid; e < nch * CB; e += NW * 64) us[e] = u[ch0 * CB + e];
+    for (int e = tid; e < nch * 2 * CB; e += NW * 64) us[e] = u[(int64_t)ch0 * 2 * CB + e];
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
   const float* ubase = reinterpret_cast<const float*>(smem + (size_t)nch * CHUNK_H * 2);
-  const float sC = meta[0];
 
   for (int64_t blk = (int64_t)blockIdx.x * NW + wave; blk * (NPB * 32) < n; blk += (int64_t)gridDim.x * NW) {
     const int64_t pbase = blk * (NPB * 32);
@@ -696,9 +735,16 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
       for (int r = 0; r < 16; ++r) sv[pb][r] = -__builtin_huge_valf();
 
     floatx16 acc[2][NPB];
-    floatx4 cnr[2][4];
+    const float* pu = nullptr;  // LDS u/r of the tile whose epilogue is pending
     int ptile = -1;
-    auto epilogue = [&](const floatx16 (&ac)[NPB], const floatx4 (&cn)[4], int tile) {
+    auto epilogue = [&](const floatx16 (&ac)[NPB], const float* pu_, int tile) {
+    // u and r of the tile straight from LDS (the chunk buffer is still live: see the loop)
+    floatx4 cn[4], cr[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      cn[g] = *reinterpret_cast<const floatx4*>(pu_ + 8 * g + 4 * h);
+      cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
+    }
 #pragma unroll
       for (int pb = 0; pb < NPB; ++pb) {
         const floatx2 sx2 = {nsx[pb], nsx[pb]};
@@ -706,8 +752,9 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
+          const floatx2 rc2 = {cr[q >> 1][(2 * q) & 3], cr[q >> 1][(2 * q + 1) & 3]};
           const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
-          const floatx2 r2 = __builtin_elementwise_fma(sx2, c2, a2);
+          const floatx2 r2 = h3_score2(a2, rc2, c2, sx2);
           w[2 * q] = r2[0];
           w[2 * q + 1] = r2[1];
         }
@@ -723,7 +770,7 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
     };
     for (int ch = 0; ch < nch; ++ch) {
       const _Float16* img = reinterpret_cast<const _Float16*>(smem + (size_t)ch * CHUNK_H * 2);
-      const float* ub = ubase + ch * CB;
+      const float* ub = ubase + ch * 2 * CB;
 #pragma unroll
       for (int cb = 0; cb < CB / 32; ++cb) {
         const int cur = cb & 1;
@@ -741,10 +788,9 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
             acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
           }
         }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) cnr[cur][g] = *reinterpret_cast<const floatx4*>(ub + cb * 32 + 8 * g + 4 * h);
-        if (ptile >= 0) epilogue(acc[cur ^ 1], cnr[cur ^ 1], ptile);
+        if (ptile >= 0) epilogue(acc[cur ^ 1], pu, ptile);
         ptile = (ch0 + ch) * (CB / 32) + cb;
+        pu = ub + cb * 32;
         if constexpr (SGV > 0) {
 #pragma unroll
           for (int i = 0; i < 3 * KS * NPB; ++i) {
@@ -754,7 +800,7 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
         }
       }
     }
-    if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], cnr[((CB / 32) - 1) & 1], ptile);
+    if (ptile >= 0) epilogue(acc[((CB / 32) - 1) & 1], pu, ptile);
 
     int bidx[NPB];
 #pragma unroll
@@ -779,7 +825,7 @@ __global__ __launch_bounds__(NW * 64, 1) void h3_assign_r(const _Float16* __rest
           labels[row] = bidx[pb];
           if (mind) {
             const float isx = 1.f / sx[pb];
-            mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx / sC, 0.f);
+            mind[row] = fmaxf(xs * isx * isx - 2.f * best[pb] * isx, 0.f);
           }
         } else {
           pbest[row] = best[pb];
@@ -822,7 +868,7 @@ HA_EXPORT int64_t ha_h3_workspace_bytes(int k, int f) {
   if (fpad < 0 || k <= 0) return -1;
   const int cb = fpad >= 128 ? 64 : 128;
   const int64_t kpad = (int64_t)(k + cb - 1) / cb * cb;
-  return kpad * fpad * 2 * 2 + kpad * 4 + 16;  // image + u + meta {s_C, max|c|_inf, u_max, -}
+  return kpad * fpad * 2 * 2 + kpad * 8 + 16;  // image + (u, r) per chunk + meta {-, max|c|_inf, u_max, -}
 }
 
 HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f, const float* C, int k, int64_t ldc,
@@ -835,19 +881,21 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
   const int kpad = (k + cb - 1) / cb * cb;
   _Float16* image = (_Float16*)workspace;
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
-  float* meta = u + kpad;
+  float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
   // FPAD 128 keeps one 32-point block per wave (two spill: 4.62 -> 4.20 ms at f=100, k=1024, n=6.25M)
 #define HA_H3(FP)                                                                                           \
   case FP: {                                                                                                \
-    constexpr int NPB = FP >= 128 ? 1 : 2, MINB = FP >= 128 ? 3 : 2;                                        \
+    constexpr int NPB = FP >= 128 ? 1 : 2, MINB = 2;  /* 2 chunk buffers (~66 KB) per WG: 2 WGs/CU */                                        \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
-    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
-                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
-    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta);                              \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
+                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
+    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8);                                          \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                         \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h3_assign_p<FP, NPB, true, MINB>),                    \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                              \
     hipLaunchKernelGGL((h3_assign_p<FP, NPB, true, MINB>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, \
                        meta, kpad / KC::CB, labels, mind);                                                 \
     break;                                                                                                  \
@@ -886,26 +934,30 @@ HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_
   const int kpad = (k + cb - 1) / cb * cb;
   _Float16* image = (_Float16*)workspace;
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
-  float* meta = u + kpad;
+  float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
   hipMemsetAsync(amb_count, 0, sizeof(int), s);
 #define HA_H1(FP)                                                                                           \
   case FP: {                                                                                                \
-    constexpr int NPB = FP >= 128 ? 1 : 2, MINB = FP >= 128 ? 3 : 2;                                        \
+    constexpr int NPB = FP >= 128 ? 1 : 2, MINB = 2;  /* 2 chunk buffers (~66 KB) per WG: 2 WGs/CU */                                        \
     constexpr int NPB1 = FP >= 128 ? 1 : 2, MINB1 = 2;                                                      \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     using K1 = H3Cfg<FP, NPB1>;                                                                             \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
-    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
-                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
-    const size_t lds1 = (size_t)K1::CHUNK_H + K1::CB * 4;                                                   \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta);                              \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
+                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
+    const size_t lds1 = 2 * ((size_t)K1::CHUNK_H + K1::CB * 8);                                                   \
     const unsigned blocks1 = (unsigned)((n + K1::PTS_PER_WG - 1) / K1::PTS_PER_WG);                        \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_filter<FP, NPB1, MINB1>),                          \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);                             \
     hipLaunchKernelGGL((h1_filter<FP, NPB1, MINB1>), dim3(blocks1), dim3(256), lds1, s, p, sx, n, image, u, meta, \
                        kpad / K1::CB, labels, amb_rows, amb_count);                                        \
-    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                \
+    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8);                                          \
     const int64_t maxb = (n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG;                                        \
     const unsigned blocks = (unsigned)(maxb < (int64_t)ncu * MINB ? maxb : (int64_t)ncu * MINB);            \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h3_assign_p<FP, NPB, true, MINB, true>),              \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                              \
     hipLaunchKernelGGL((h3_assign_p<FP, NPB, true, MINB, true>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, \
                        meta, kpad / KC::CB, labels, (float*)nullptr, (const int*)amb_rows, (const int*)amb_count); \
     break;                                                                                                  \
@@ -945,7 +997,7 @@ HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, 
   const int kpad = (m + cb - 1) / cb * cb;
   _Float16* image = (_Float16*)workspace;
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
-  float* meta = u + kpad;
+  float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
 #define HA_TK_LAUNCH(FP, KN)                                                                                 \
   hipLaunchKernelGGL((h3_topk<FP, KN>), dim3(blocks, splits), dim3(256), lds, s, p, sx, n, image, u, meta,      \
@@ -954,10 +1006,10 @@ HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, 
   case FP: {                                                                                                 \
     using KC = H3Cfg<FP, 1>;                                                                                 \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                           \
-    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, m, f, ldc, meta);                               \
-    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),   \
-                       dim3(256), 0, s, C, m, f, ldc, kpad, image, u, meta);                                \
-    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 4;                                                 \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, m, f, ldc, kpad, u, meta);                               \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),   \
+                       dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                \
+    const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 8;                                                 \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                          \
     if (kout <= 4)                                                                                           \
       HA_TK_LAUNCH(FP, 4);                                                                                   \
@@ -1009,7 +1061,7 @@ HA_EXPORT int ha_h3_assign_r(const void* planes, const float* sx, int64_t n, int
   if (phases > 1 && !scratch) return HA_BAD_ARG;
   _Float16* image = (_Float16*)workspace;
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
-  float* meta = u + kpad;
+  float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
   float* pb = (float*)scratch;
   int* pi = scratch ? (int*)((char*)scratch + n * sizeof(float)) : nullptr;
@@ -1020,12 +1072,12 @@ HA_EXPORT int ha_h3_assign_r(const void* planes, const float* sx, int64_t n, int
     constexpr int NPB = FP >= 128 ? 1 : 2;                                                                  \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cmax, dim3(64), dim3(256), 0, s, C, k, f, ldc, meta);                              \
-    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8 + 1) + 255) / 256)),  \
-                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u, meta);                               \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta);                              \
+    hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
+                       dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
     for (int ph = 0; ph < phases; ++ph) {                                                                   \
       const int c0 = ph * rc, nc = nchunks - c0 < rc ? nchunks - c0 : rc;                                   \
-      const size_t lds = (size_t)nc * KC::CHUNK_H * 2 + (size_t)nc * KC::CB * 4;                            \
+      const size_t lds = (size_t)nc * KC::CHUNK_H * 2 + (size_t)nc * KC::CB * 8;                            \
       hipFuncSetAttribute(reinterpret_cast<const void*>(h3_assign_r<FP, NPB, H3R_NW>),                      \
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
       hipLaunchKernelGGL((h3_assign_r<FP, NPB, H3R_NW>), dim3(grid), dim3(H3R_NW * 64), lds, s, p, sx, n, image, \

@@ -8,13 +8,15 @@ import ctypes
 import os
 from typing import NamedTuple, Optional, Tuple
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd"]
+           "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
+           "argreduce_decode", "argreduce_supported", "topk_rows"]
 
 _NUM_CUS = {}
 
@@ -785,3 +787,74 @@ def gemm_f16x3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = N
     check(lib().ha_split_unscale(_ptr(C), M, N, C.stride(0), _ptr(ea), _ptr(eb),
                                  ctypes.c_void_p(stream_ptr(a.device))), "ha_split_unscale")
     return C
+
+
+# --------------------------------------------------------------------------------------------- selection
+_SEL_DTYPES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.int32: 3, torch.int16: 4,
+               torch.int8: 5, torch.uint8: 6, torch.bool: 6}
+_KEY_IDENTITY = -(1 << 63)
+
+
+def argreduce_supported(t: torch.Tensor, max_index: int) -> bool:
+    """Whether the packed-key kernels handle ``t`` (device, <= 32-bit dtype, indices < 2^32 - 1)."""
+    return t.is_cuda and t.dtype in _SEL_DTYPES and max_index < 0xFFFFFFFF and use_native(t)
+
+
+def argreduce_keys(t: torch.Tensor, axis: Optional[int], smallest: bool, displ: int = 0,
+                   gextent: Optional[int] = None, split: Optional[int] = None) -> torch.Tensor:
+    """Packed (value, first index) keys of an arg-reduction of the device tensor ``t``
+    (``csrc/select.hip``): int64, the larger key is the winner, so combining partial results -
+    across ranks too - is an integer MAX (one RCCL all-reduce).
+
+    axis None: one key over all elements; the index is the GLOBAL flat index when ``t`` is the
+    local block of an array split along ``split`` whose extent is ``gextent`` and this block starts
+    at ``displ``. axis given: keys of shape ``t.shape`` without ``axis``, indices along ``axis``
+    offset by ``displ``."""
+    t = t.contiguous()
+    if t.dtype == torch.bool:
+        t = t.view(torch.uint8)
+    shp = list(t.shape)
+    L = lib()
+    if axis is None:
+        s = 0 if split is None else split
+        O = int(np.prod(shp[:s])) if shp else 1
+        Lx = shp[s] if shp else 1
+        I = int(np.prod(shp[s + 1:])) if shp else 1
+        gL = gextent if gextent is not None else Lx
+        out = torch.full((1,), _KEY_IDENTITY, dtype=torch.int64, device=t.device)
+        mode = 0
+    else:
+        O = int(np.prod(shp[:axis]))
+        Lx = shp[axis]
+        I = int(np.prod(shp[axis + 1:]))
+        gL = Lx
+        out = torch.full(shp[:axis] + shp[axis + 1:], _KEY_IDENTITY, dtype=torch.int64, device=t.device)
+        mode = 1
+    check(L.ha_argreduce(_ptr(t), _SEL_DTYPES[t.dtype], O, Lx, I, gL, displ, mode, int(smallest), _ptr(out),
+                         ctypes.c_void_p(stream_ptr(t.device))), "ha_argreduce")
+    return out
+
+
+def argreduce_decode(keys: torch.Tensor) -> torch.Tensor:
+    """Indices of packed arg-reduction keys (-1 where no element contributed)."""
+    idx = 0xFFFFFFFF - (keys & 0xFFFFFFFF)
+    return torch.where(keys == _KEY_IDENTITY, torch.full_like(idx, -1), idx)
+
+
+def topk_rows(t: torch.Tensor, k: int, dim: int, largest: bool, displ: int = 0):
+    """Top-k (k <= 32) along ``dim`` of a device tensor with one wave per row (``csrc/select.hip``):
+    values sorted best first, int64 indices (+ ``displ``); ties resolve to the smaller index; NaN
+    ranks like torch.topk (largest). None where the kernel does not apply."""
+    if not (t.is_cuda and t.dtype in _SEL_DTYPES and t.dtype != torch.bool and 0 < k <= 32
+            and t.shape[dim] >= k and t.shape[dim] < 0xFFFFFFFF and use_native(t)):
+        return None
+    x = t.movedim(dim, -1).contiguous()
+    lead = tuple(x.shape[:-1])
+    O = int(np.prod(lead)) if lead else 1
+    Lr = x.shape[-1]
+    vals = torch.empty(lead + (k,), dtype=x.dtype, device=x.device)
+    idx = torch.empty(lead + (k,), dtype=torch.int64, device=x.device)
+    if O:
+        check(lib().ha_topk_rows(_ptr(x), _SEL_DTYPES[x.dtype], O, Lr, displ, k, int(not largest), _ptr(vals),
+                                 _ptr(idx), ctypes.c_void_p(stream_ptr(x.device))), "ha_topk_rows")
+    return vals.movedim(-1, dim), idx.movedim(-1, dim)

@@ -40,10 +40,16 @@ def _lib():
             ("ha_ipc_close", c_int, [c_void_p]),
             ("ha_ipc_allreduce", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p,
                                          c_int64, c_int, c_int64, c_uint, c_int, c_int64, c_void_p]),
-            ("ha_ipc_error", c_int, [c_void_p, c_int])):
+            ("ha_ipc_error", c_int, [c_void_p, c_int]),
+            ("ha_ipc_error_async", c_int, [c_void_p, c_void_p, c_void_p])):
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
     return L
+
+
+class IpcTimeoutError(RuntimeError):
+    """A peer missed an IPC barrier: the affected output was poisoned (NaN) and the communicator
+    cannot be used again (slot reuse is only safe while every barrier completes)."""
 
 
 def _check(rc: int, what: str):
@@ -94,16 +100,45 @@ class IpcAllreduce:
         self._data = arr(*data)
         self._sig = arr(*sig)
         self._L = L
+        # error word of every call, copied behind it on the stream into pinned host memory; the
+        # next call (or check()) reads it once the copy's event has completed
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._err_event = None
+        self._poisoned = False
         comm.Barrier()
 
     def supports(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype in _DTYPES and t.is_contiguous()
                 and t.numel() * t.element_size() <= self.capacity)
 
+    def _poll(self, wait: bool = False):
+        """Raise if an earlier call of this rank timed out (reads the pinned copy of the error
+        word once the copy behind that call has landed; ``wait`` blocks for it)."""
+        if self._poisoned:
+            raise IpcTimeoutError("IPC all-reduce disabled after an earlier barrier timeout")
+        ev = self._err_event
+        if ev is None:
+            return
+        if wait:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        if int(self._err_host[0]) != 0:
+            self._poisoned = True
+            raise IpcTimeoutError("an IPC all-reduce barrier timed out on rank {}: its result was "
+                                  "poisoned with NaN".format(self.rank))
+
+    def check(self):
+        """Block until every issued call has finished and raise if any of them timed out."""
+        self._poll(wait=True)
+
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place SUM of ``t`` over the ranks, ordered on the current stream."""
+        """In-place SUM of ``t`` over the ranks, ordered on the current stream. Raises
+        :class:`IpcTimeoutError` when an EARLIER call timed out (this rank's view); a timed-out
+        call's own output is NaN-poisoned, so a silent wrong sum is impossible either way."""
         if not self.supports(t):
             raise ValueError("tensor not supported by the IPC all-reduce")
+        self._poll()
         self.epoch += 1
         es = t.element_size()
         rc = self._L.ha_ipc_allreduce(self._data, self._sig, self.world, self.rank, ctypes.c_void_p(t.data_ptr()),
@@ -111,6 +146,12 @@ class IpcAllreduce:
                                       self.blocks, self.spins,
                                       ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream))
         _check(rc, "launch")
+        stream = torch.cuda.current_stream(t.device)
+        _check(self._L.ha_ipc_error_async(ctypes.c_void_p(self._own[1]), ctypes.c_void_p(self._err_host.data_ptr()),
+                                          ctypes.c_void_p(stream.cuda_stream)), "error copy")
+        if self._err_event is None:
+            self._err_event = torch.cuda.Event()
+        self._err_event.record(stream)
         return t
 
     def error(self, clear: bool = False) -> int:

@@ -103,14 +103,30 @@ class Lasso(RegressionMixin, BaseEstimator):
             X = X.float()
         tt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
         X = X.to(tt)
-        yl = y.larray.reshape(-1).to(tt)
-        if y.split is None and x.is_distributed():
-            counts, displs = x.counts_displs()
-            r0 = displs[x.comm.rank]
-            yl = yl[r0: r0 + counts[x.comm.rank]]
+        if y.gnumel != m:
+            raise ValueError("y must hold one target per row of x: {} != {}".format(y.gnumel, m))
+        # y's local rows must be exactly x's local rows (the native kernels index both by row)
+        if y.ndim != 1:
+            # (m, 1) / (1, m) targets of any split -> 1-D (split 0 if distributed, C order)
+            y = ht.reshape(y, (m,), new_split=0 if y.split is not None else None)
+        if x.is_distributed():
+            if y.split is None:
+                counts, displs = x.counts_displs()
+                r0 = displs[x.comm.rank]
+                yl = y.larray.reshape(-1)[r0: r0 + counts[x.comm.rank]]
+            else:
+                yl = y.larray if y.split_counts() == x.split_counts() else \
+                    y._exchange_rows(y.split_counts(), x.split_counts())
+                yl = yl.reshape(-1)
+        else:
+            yl = (ht.resplit(y, None) if y.is_distributed() else y).larray.reshape(-1)
+        yl = yl.to(device=X.device, dtype=tt)
+        if yl.numel() != X.shape[0]:
+            raise ValueError("local rows of x ({}) and y ({}) differ".format(X.shape[0], yl.numel()))
         dist = x.is_distributed()
         solver = os.environ.get("HEAT_LASSO_SOLVER", "auto")
-        if solver == "gram" or (solver == "auto" and _prefer_gram(m // x.comm.size, n, self.max_iter, X.is_cuda)):
+        # the cost model sees the rows this rank really processes (all m when x is replicated)
+        if solver == "gram" or (solver == "auto" and _prefer_gram(X.shape[0], n, self.max_iter, X.is_cuda)):
             G = ops.lasso_gram(X, yl)                         # [n+1, n+1] fp64, local rows
             if dist:
                 x.comm.Allreduce(MPI.IN_PLACE, G, MPI.SUM)

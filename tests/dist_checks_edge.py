@@ -246,3 +246,46 @@ def check_different_split_binary_ops():
     # broadcast operand of lower rank with a different split
     c = rng.standard_normal((5, 4))
     assert_array_equal(ht.array(a, split=0) + ht.array(c, split=1), a + c)
+
+
+def check_lasso_mismatched_y_layouts():
+    """y distributed differently from x (split None vs 0, (m,1) split 1, unbalanced
+    split 0) must give the same fit, never an out-of-bounds read of y in the native kernels."""
+    import os
+
+    rng = np.random.default_rng(19)
+    m, n = 97, 5
+    X = rng.normal(size=(m, n)).astype(np.float32)
+    X /= np.sqrt((X ** 2).mean(0))
+    w = np.array([0.5, 2.0, 0.0, -1.5, 0.7], np.float32)
+    y = (X @ w + 0.01 * rng.normal(size=m)).astype(np.float32)
+    prev = os.environ.get("HEAT_LASSO_SOLVER")
+    ref = None
+    try:
+        for solver in ("sweep", "gram"):
+            os.environ["HEAT_LASSO_SOLVER"] = solver
+            for xs, ys, yshape in ((0, None, (m, 1)), (None, 0, (m,)), (0, 1, (1, m)), (0, 1, (m, 1)),
+                                   (None, 1, (1, m)), (0, "unbal", (m,))):
+                yv = y.reshape(yshape)
+                if ys == "unbal":
+                    Y = ht.array(yv, split=0)[3:]
+                    Y = ht.concatenate([ht.array(yv[:3]), Y])  # unbalanced distribution of the same y
+                else:
+                    Y = ht.array(yv, split=ys if not (ys == 1 and yshape[1] == 1) else 1)
+                est = ht.regression.Lasso(lam=0.01, max_iter=100, tol=1e-8)
+                est.fit(ht.array(X, split=xs), Y)
+                th = est.theta.numpy().ravel()
+                if ref is None:
+                    ref = th
+                assert np.allclose(th, ref, atol=1e-4), (solver, xs, ys, yshape, th, ref)
+        bad = ht.array(y[:-1], split=0)
+        try:
+            ht.regression.Lasso(max_iter=2).fit(ht.array(X, split=0), bad)
+            raise AssertionError("a y of the wrong length must raise")
+        except ValueError:
+            pass
+    finally:
+        if prev is None:
+            os.environ.pop("HEAT_LASSO_SOLVER", None)
+        else:
+            os.environ["HEAT_LASSO_SOLVER"] = prev

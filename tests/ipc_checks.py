@@ -71,3 +71,40 @@ def check_ipc_through_communication():
     assert x.larray.is_cuda
     assert ht.sum(x).item() == 4000 * 3999 / 2
     assert comm._ipc.error() == 0
+
+
+def check_ipc_timeout_is_loud():
+    """A rank that never joins: the waiting rank's output is NaN-poisoned and the NEXT call (or
+    check()) raises IpcTimeoutError - never a silently wrong sum."""
+    import time
+
+    from heat_amd.parallel.ipc import IpcTimeoutError
+
+    comm = ht.MPI_WORLD
+    r = comm.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ar = IpcAllreduce(comm, capacity_bytes=1 << 16, blocks=4, timeout_spins=2_000_000)
+    t = torch.ones(1000, device=dev)
+    ar.allreduce_(t)                                   # a good call first
+    ar.check()
+    assert torch.equal(t.cpu(), torch.full((1000,), float(comm.size)))
+    comm.Barrier()
+    if r == 0:
+        ar.spins = 2000                                # a short bound for the call nobody joins
+        t = torch.ones(1000, device=dev)
+        ar.allreduce_(t)                               # the peers sit out this call
+        torch.cuda.synchronize()
+        assert torch.isnan(t).all(), "a timed-out call must not return a sum"
+        try:
+            ar.check()
+            raise AssertionError("check() must raise after a timeout")
+        except IpcTimeoutError:
+            pass
+        try:
+            ar.allreduce_(torch.ones(10, device=dev))
+            raise AssertionError("a poisoned communicator must refuse further calls")
+        except IpcTimeoutError:
+            pass
+    else:
+        time.sleep(0.5)
+    comm.Barrier()

@@ -15,3 +15,7 @@ def test_ipc_allreduce(gpu, nprocs):
 def test_ipc_through_communication(gpu):
     run_distributed("tests.ipc_checks:check_ipc_through_communication", 2, timeout=110, keep_gpu=True,
                     env_extra={"HEAT_IPC_ALLREDUCE": "1"})
+
+
+def test_ipc_timeout_is_loud(gpu):
+    run_distributed("tests.ipc_checks:check_ipc_timeout_is_loud", 2, timeout=110, keep_gpu=True)

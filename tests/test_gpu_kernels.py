@@ -58,6 +58,69 @@ def test_kmeans_assign_f16x3(n, k, f, scale):
     assert torch.allclose(mind.double(), ref_min, rtol=1e-4, atol=1e-4 * scale * scale * f)
 
 
+def _hetero(n, k, f, seed, span=(-4.0, 4.0)):
+    """Centroid norms log-uniform over 10^span (1e-4 .. 1e4) within ONE call; every point sits
+    near a random centroid (noise 20% of that centroid's norm), so points near the tiny centroids
+    need the tiny centroids' products at full relative precision."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lo, hi = span
+    norms = 10.0 ** (lo + (hi - lo) * torch.rand(k, generator=g, dtype=torch.float64))
+    C = torch.randn(k, f, generator=g, dtype=torch.float64)
+    C = C / C.norm(dim=1, keepdim=True) * norms[:, None]
+    owner = torch.randint(0, k, (n,), generator=g)
+    X = C[owner] + 0.2 * norms[owner, None] * torch.randn(n, f, generator=g, dtype=torch.float64) / f ** 0.5
+    return X.float(), C.float()
+
+
+def _local_minimality(X, C, lab):
+    """chosen - best <= tol_i with tol_i LOCAL to point i: it scales with |x_i|^2 and the norms of
+    the two contenders only (not with the largest centroid), i.e. fp32-GEMM relative accuracy per
+    centroid."""
+    Xd, Cd = X.double(), C.double()
+    d = torch.cdist(Xd, Cd) ** 2
+    ref_min, ref_lab = d.min(1)
+    chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+    cn = (Cd * Cd).sum(1)
+    tol = 4e-6 * ((Xd * Xd).sum(1) + cn[lab.long()] + cn[ref_lab])
+    bad = chosen - ref_min > tol
+    return bad, d, ref_min, ref_lab
+
+
+@pytest.mark.parametrize("mode", ["resident_all", "chunked", "certified"])
+@pytest.mark.parametrize("n,k,f", [(20000, 1024, 64), (5000, 300, 32), (3333, 200, 100), (9000, 500, 16)])
+def test_kmeans_assign_f16x3_heterogeneous_centroids(n, k, f, mode, monkeypatch):
+    """Centroid norms spanning 1e-4..1e4 in one call: per-centroid scales keep every centroid at
+    fp32-GEMM relative accuracy (a shared scale lost up to 27 bits on the smallest ones)."""
+    from heat_amd import ops
+
+    dev = _dev()
+    monkeypatch.setattr(ops.kernels, "_H3_RESIDENT", mode == "resident_all")
+    monkeypatch.setattr(ops.kernels, "_H3_RESIDENT_ALL", mode == "resident_all")
+    X, C = _hetero(n, k, f, seed=n + k + f)
+    X, C = X.to(dev), C.to(dev)
+    packed = ops.kmeans_pack_points(X)
+    lab, mind = ops.kmeans_assign(X, C, want_mind=mode != "certified", packed=packed,
+                                  certified=mode == "certified")
+    bad, d, ref_min, ref_lab = _local_minimality(X, C, lab)
+    assert not bad.any(), int(bad.sum())
+    assert (lab.long() == ref_lab).float().mean() > 0.999
+    if mind is not None:
+        assert torch.all((mind.double() - ref_min).abs() <= 1e-4 * ref_min + 4e-6 * (X.double() ** 2).sum(1))
+
+
+def test_knn_topk_heterogeneous(gpu):
+    from heat_amd import ops
+
+    X, C = _hetero(3000, 4000, 32, seed=5)
+    X, C = X.cuda(), C.cuda()
+    dist, idx = ops.knn_topk(X, C, 4)
+    d = torch.cdist(X.double(), C.double()) ** 2
+    ref, _ = d.topk(4, dim=1, largest=False)
+    got = d.gather(1, idx.long())
+    tol = 4e-6 * ((X.double() ** 2).sum(1, keepdim=True) + (C.double() ** 2).sum(1)[idx.long()])
+    assert torch.all(got - ref <= tol)
+
+
 @pytest.mark.parametrize("mode", ["resident_all", "chunked"])
 @pytest.mark.parametrize("n,k,f", [(5000, 300, 32), (70000, 1500, 64), (3333, 700, 100), (9000, 2100, 16)])
 def test_kmeans_assign_f16x3_kernels(n, k, f, mode, monkeypatch):
