@@ -595,10 +595,14 @@ class MPICommunication(Communication):
                 shapes.append(tuple(s_))
         else:
             shapes = [tuple(send.narrow(axis, 0, 0).shape)] * self.size
-        out = self.exchange(blocks, shapes)
-        if self.rank == root and recv is not None:
-            recv.copy_(torch.cat(out, dim=axis).to(recv.dtype).reshape(recv.shape))
-        return MPIRequest()
+        work, fin = self._exchange_async(blocks, shapes)
+
+        def done():
+            out = fin()
+            if self.rank == root and recv is not None:
+                recv.copy_(torch.cat(out, dim=axis).to(recv.dtype).reshape(recv.shape))
+
+        return MPIRequest(work, done)
 
     def Gatherv(self, sendbuf, recvbuf, root: int = 0, axis: int = 0, recv_axis: int = None):
         self.Igatherv(sendbuf, recvbuf, root, axis, recv_axis).Wait()
@@ -626,9 +630,12 @@ class MPICommunication(Communication):
         else:
             blocks = [recv.new_empty((0,)) for _ in range(self.size)]
         recv_shapes = [tuple(recv.shape) if r == root else (0,) for r in range(self.size)]
-        out = self.exchange(blocks, recv_shapes)
-        recv.copy_(out[root].reshape(recv.shape))
-        return MPIRequest()
+        work, fin = self._exchange_async(blocks, recv_shapes)
+
+        def done():
+            recv.copy_(fin()[root].reshape(recv.shape))
+
+        return MPIRequest(work, done)
 
     def Scatterv(self, sendbuf, recvbuf, root: int = 0, axis: int = 0):
         self.Iscatterv(sendbuf, recvbuf, root, axis).Wait()
@@ -640,8 +647,16 @@ class MPICommunication(Communication):
     def exchange(self, send_blocks: List[torch.Tensor], recv_shapes: List[Tuple[int, ...]]) -> List[torch.Tensor]:
         """Personalised exchange: ``send_blocks[r]`` goes to rank r, the block from rank r has
         shape ``recv_shapes[r]``. One packed ``all_to_all_single`` (RCCL grouped p2p over xGMI)."""
+        work, fin = self._exchange_async(send_blocks, recv_shapes)
+        if work is not None:
+            work.wait()
+        return fin()
+
+    def _exchange_async(self, send_blocks, recv_shapes):
+        """Start :meth:`exchange`; returns (work or None, finalize -> list of received blocks)."""
         if self.size == 1:
-            return [send_blocks[0].reshape(recv_shapes[0])]
+            blk = send_blocks[0].reshape(recv_shapes[0])
+            return None, lambda: [blk]
         ref = next((b for b in send_blocks if b is not None), None)
         dtype, device = ref.dtype, ref.device
         wire = torch.uint8 if dtype == torch.bool else dtype
@@ -652,14 +667,19 @@ class MPICommunication(Communication):
         flat_out = torch.empty(sum(out_sizes), dtype=wire, device=device)
         if flat_in.is_complex():
             fi, fo = torch.view_as_real(flat_in).reshape(-1), torch.view_as_real(flat_out).reshape(-1)
-            dist.all_to_all_single(fo, fi, [2 * s for s in out_sizes], [2 * s for s in in_sizes], group=self.group)
+            work = dist.all_to_all_single(fo, fi, [2 * s for s in out_sizes], [2 * s for s in in_sizes],
+                                          group=self.group, async_op=True)
         else:
-            dist.all_to_all_single(flat_out, flat_in, out_sizes, in_sizes, group=self.group)
-        res, off = [], 0
-        for s, n in zip(recv_shapes, out_sizes):
-            res.append(flat_out[off: off + n].reshape(s).to(dtype))
-            off += n
-        return res
+            work = dist.all_to_all_single(flat_out, flat_in, out_sizes, in_sizes, group=self.group, async_op=True)
+
+        def fin():
+            res, off = [], 0
+            for s, n in zip(recv_shapes, out_sizes):
+                res.append(flat_out[off: off + n].reshape(s).to(dtype))
+                off += n
+            return res
+
+        return work, fin
 
     def _alltoall_impl(self, sendbuf, recvbuf, send_axis, recv_axis) -> MPIRequest:
         send, scounts, _ = self._unpack_v(sendbuf)
@@ -682,9 +702,12 @@ class MPICommunication(Communication):
             s[recv_axis] = rcounts[r]
             shapes.append(tuple(s))
         self._trace("Alltoallv", send)
-        out = self.exchange(blocks, shapes)
-        recv.copy_(torch.cat(out, dim=recv_axis))
-        return MPIRequest()
+        work, fin = self._exchange_async(blocks, shapes)
+
+        def done():
+            recv.copy_(torch.cat(fin(), dim=recv_axis))
+
+        return MPIRequest(work, done)
 
     def Ialltoallv(self, sendbuf, recvbuf, send_axis: int = 0, recv_axis: int = None) -> MPIRequest:
         return self._alltoall_impl(sendbuf, recvbuf, send_axis, recv_axis)

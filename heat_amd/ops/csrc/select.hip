@@ -33,7 +33,8 @@ __device__ __forceinline__ int32_t ar_hi(T v) {
   } else {
     const float f = ar_tof<T>(v);
     if (f != f) return (NAN_WINS || !SMALL) ? INT32_MAX : INT32_MIN;
-    const unsigned b = __float_as_uint(f);
+    unsigned b = __float_as_uint(f);
+    if ((b << 1) == 0u) b = 0u;  // -0.0 == +0.0 (a tie, resolved by the index like NumPy)
     const unsigned o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
     const int32_t k = (int32_t)(o ^ 0x80000000u);
     // ~k of a non-NaN never equals INT32_MAX (that would need k = INT32_MIN = -NaN pattern)

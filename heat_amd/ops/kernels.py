@@ -16,7 +16,7 @@ from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
-           "argreduce_decode", "argreduce_supported", "topk_rows"]
+           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3"]
 
 _NUM_CUS = {}
 
@@ -858,3 +858,91 @@ def topk_rows(t: torch.Tensor, k: int, dim: int, largest: bool, displ: int = 0):
         check(lib().ha_topk_rows(_ptr(x), _SEL_DTYPES[x.dtype], O, Lr, displ, k, int(not largest), _ptr(vals),
                                  _ptr(idx), ctypes.c_void_p(stream_ptr(x.device))), "ha_topk_rows")
     return vals.movedim(-1, dim), idx.movedim(-1, dim)
+
+
+# --------------------------------------------------------------------------------------------- exact fp32 GEMM
+def _gemm_operand(t: torch.Tensor, contig_dim: int):
+    """(tensor, ld, alt_major) for a 2-D fp32 operand: alt_major False when dim ``contig_dim`` is
+    contiguous, True when the other dim is; otherwise a contiguous copy."""
+    if t.stride(contig_dim) == 1 and t.stride(1 - contig_dim) >= max(1, t.shape[contig_dim]):
+        return t, t.stride(1 - contig_dim), False
+    if t.stride(1 - contig_dim) == 1 and t.stride(contig_dim) >= max(1, t.shape[1 - contig_dim]):
+        return t, t.stride(contig_dim), True
+    t = t.contiguous()
+    return t, t.stride(0) if contig_dim == 1 else t.stride(1), contig_dim == 0
+
+
+_GEMM_BK = int(os.environ.get("HEAT_GEMM_VARIANT", "4"))  # exact GEMM block: 2 = 128x128, 4 = 128x256
+
+
+def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+             accumulate: bool = False) -> torch.Tensor:
+    """Exact fp32 ``a @ b`` on the f32-input matrix cores (``csrc/gemm_mfma.hip``): fp32 products
+    and accumulation in k order like any fp32 GEMM, every operand layout (row-/column-major views
+    such as ``x.T @ x``) without a copy, 64-bit offsets (no 4 GB operand limit). ``out``: a
+    row-major fp32 [M, N] view (e.g. a row block of a larger result); ``accumulate`` adds into it."""
+    if not (a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32 \
+            or a.dim() != 2 or b.dim() != 2:
+        if out is None:
+            return a @ b
+        return out.add_(a @ b) if accumulate else torch.mm(a, b, out=out)
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K:
+        raise ValueError("gemm_f32: inner dimensions differ: {} vs {}".format(K, b.shape[0]))
+    if out is None:
+        out = torch.zeros((M, N), dtype=torch.float32, device=a.device) if accumulate else \
+            torch.empty((M, N), dtype=torch.float32, device=a.device)
+    elif out.shape != (M, N) or out.dtype != torch.float32 or (N > 1 and out.stride(1) != 1):
+        raise ValueError("gemm_f32: out must be a row-major float32 [M, N] tensor")
+    if M == 0 or N == 0:
+        return out
+    if K == 0:
+        return out if accumulate else out.zero_()
+    A, lda, a_km = _gemm_operand(a, 1)      # row-major: k contiguous; k-major: m contiguous
+    B, ldb, b_nm = _gemm_operand(b, 1)      # k-major: n contiguous; n-major: k contiguous
+    check(lib().ha_gemm_f32(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, out.stride(0) if M > 1 else N,
+                            int(a_km), int(b_nm), int(accumulate), _GEMM_BK, ctypes.c_void_p(stream_ptr(a.device))),
+          "ha_gemm_f32")
+    return out
+
+
+def _h3_rows(X: torch.Tensor, Kp: int):
+    """fp16 hi/lo planes [R, Kp] (zero tail) + int32 row exponents of a row-major fp32 matrix X
+    [R, K], and the device non-finite flag."""
+    R, K = X.shape
+    if K % 4 != 0 or X.stride(1) != 1 or X.stride(0) % 4 != 0 or X.data_ptr() % 16 != 0:
+        X = F.pad(X.contiguous(), (0, Kp - K)) if K % 4 else X.contiguous()
+        K = X.shape[1]
+    hi = torch.empty((R, Kp), dtype=torch.float16, device=X.device)
+    lo = torch.empty((R, Kp), dtype=torch.float16, device=X.device)
+    if Kp > K:
+        hi[:, K:].zero_()
+        lo[:, K:].zero_()
+    ex = torch.empty(R, dtype=torch.int32, device=X.device)
+    flag = torch.zeros(1, dtype=torch.int32, device=X.device)
+    check(lib().ha_split3_rows(_ptr(X), R, K, X.stride(0), _ptr(hi), _ptr(None), _ptr(lo), Kp, _ptr(ex), _ptr(flag),
+                               ctypes.c_void_p(stream_ptr(X.device))), "ha_split3_rows")
+    return hi, lo, ex, flag
+
+
+def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """fp32 ``a @ b`` by the FUSED fp16x3 MFMA kernel (``csrc/gemm_mfma.hip: gemm_h3``): row
+    scaled hi/lo planes of ``a`` and of ``b^T``, one kernel forming hi.hi + hi.lo + lo.hi with fp32
+    accumulation and the exact power-of-two unscale in its epilogue. Accuracy of an fp32 GEMM
+    (see :func:`gemm_f16x3`). Returns None for non-finite operands (the caller falls back; the
+    check is one host sync)."""
+    M, K = a.shape
+    N = b.shape[1]
+    Kp = (K + 31) // 32 * 32
+    A = a if a.stride(-1) == 1 else a.contiguous()
+    BT = b.t() if b.stride(0) == 1 else b.t().contiguous()
+    ahi, alo, ea, fa = _h3_rows(A, Kp)
+    bhi, blo, eb, fb = _h3_rows(BT, Kp)
+    if int((fa + fb).item()) != 0:
+        return None
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    check(lib().ha_gemm_h3(_ptr(ahi), _ptr(alo), _ptr(bhi), _ptr(blo), _ptr(ea), _ptr(eb), _ptr(out), M, N, Kp,
+                           out.stride(0) if M > 1 else N, ctypes.c_void_p(stream_ptr(a.device))), "ha_gemm_h3")
+    return out

@@ -289,3 +289,38 @@ def check_lasso_mismatched_y_layouts():
             os.environ.pop("HEAT_LASSO_SOLVER", None)
         else:
             os.environ["HEAT_LASSO_SOLVER"] = prev
+
+
+def check_nonblocking_v_collectives():
+    """Ialltoallv / Igatherv / Iscatterv return a pending request: several can be in flight at once
+    and complete in any Wait order (round 1 completed them synchronously)."""
+    import torch
+
+    comm = ht.MPI_WORLD
+    p, r = comm.size, comm.rank
+    # all-to-all of rank-dependent blocks, two requests in flight
+    send1 = torch.arange(p * 3, dtype=torch.float64).reshape(p * 3, 1) + 100 * r
+    recv1 = torch.empty(p * 3, 1, dtype=torch.float64)
+    send2 = torch.full((p * 2, 4), float(r), dtype=torch.float32)
+    recv2 = torch.empty(p * 2, 4, dtype=torch.float32)
+    q1 = comm.Ialltoallv(send1, recv1)
+    q2 = comm.Ialltoallv(send2, recv2)
+    q2.Wait()
+    q1.Wait()
+    for src in range(p):
+        assert torch.equal(recv1[3 * src: 3 * src + 3, 0], torch.arange(3 * r, 3 * r + 3, dtype=torch.float64) + 100 * src)
+        assert torch.all(recv2[2 * src: 2 * src + 2] == src)
+    # gather of unequal blocks to root 0 and a scatter back, overlapped
+    blk = torch.full((r + 1, 2), float(r))
+    tot = sum(range(1, p + 1))
+    g = torch.empty(tot, 2) if r == 0 else None
+    qg = comm.Igatherv(blk, g, root=0)
+    sc_recv = torch.empty(2, 3)
+    sc_send = torch.arange(p * 6, dtype=torch.float32).reshape(p * 2, 3) if r == 0 else None
+    qs = comm.Iscatterv(sc_send, sc_recv, root=0)
+    qs.Wait()
+    qg.Wait()
+    assert torch.equal(sc_recv, torch.arange(6 * r, 6 * r + 6, dtype=torch.float32).reshape(2, 3))
+    if r == 0:
+        exp = torch.cat([torch.full((q + 1, 2), float(q)) for q in range(p)])
+        assert torch.equal(g, exp)

@@ -1,0 +1,97 @@
+"""Exact fp32 MFMA GEMM (``ops/csrc/gemm_mfma.hip``) against an fp64 torch reference: every
+operand layout, edge sizes (not multiples of the 128 x 128 x 16 tile), accumulate, row blocks."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from heat_amd import ops
+
+    assert ops.available(), "native library must load on a GPU box"
+    return torch.device("cuda", 0)
+
+
+def _bound(a, b):
+    # fp32 GEMM error bound class: ~K * 2^-24 * |a||b| elementwise (k-ordered fma chain)
+    K = a.shape[1]
+    return 4 * K * 2.0 ** -24 * (a.abs().double() @ b.abs().double()) + 1e-30
+
+
+@pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 512, 768), (4099, 130, 65), (64, 4096, 64), (1, 7, 1),
+                                   (129, 1, 131), (2000, 33, 3)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+def test_gemm_f32_layouts(m, k, n, layout):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m * 7 + k * 3 + n)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    c = ops.gemm_f32(A, B)
+    ref = a.double() @ b.double()
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
+
+
+def test_gemm_f32_accumulate_rowblock_and_gram():
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3001, 70, generator=g).to(dev)
+    gram = ops.gemm_f32(x.t(), x)                      # X^T X without a copy (k-major A)
+    ref = x.double().t() @ x.double()
+    assert torch.all((gram.double() - ref).abs() <= _bound(x.t(), x))
+    out = torch.ones(500, 70, device=dev)
+    big = torch.zeros(1000, 70, device=dev)
+    ops.gemm_f32(x[:500], gram, out=out, accumulate=True)
+    assert torch.allclose(out.double(), 1 + x[:500].double() @ gram.double(), rtol=1e-5, atol=1e-3)
+    ops.gemm_f32(x[:300], gram, out=big[200:500])       # a row block of a larger result
+    assert torch.allclose(big[200:500].double(), x[:300].double() @ gram.double(), rtol=1e-5, atol=1e-3)
+    assert torch.all(big[:200] == 0) and torch.all(big[500:] == 0)
+
+
+def test_gemm_f32_exact_products():
+    """Integer-valued operands: every product and partial sum is exact in fp32, so the result must
+    equal the integer matmul bit for bit (catches a transposed fragment map at once)."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(9)
+    a = torch.randint(-8, 9, (257, 300), generator=g).float().to(dev)
+    b = torch.randint(-8, 9, (300, 191), generator=g).float().to(dev)
+    assert torch.equal(ops.gemm_f32(a, b), (a.double() @ b.double()).float())
+
+
+@pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 512, 768), (4099, 130, 65), (64, 4096, 64), (1, 7, 1),
+                                   (129, 1, 131), (2000, 33, 3), (517, 1000, 300)])
+@pytest.mark.parametrize("scale", ["unit", "rows", "tiny", "huge"])
+def test_gemm_h3_fused(m, k, n, scale):
+    """Fused fp16x3 kernel: fp32-GEMM accuracy against fp64 (same bound family as the split GEMM
+    tests), for heterogeneous row / column scales too."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + 3 * k + 7 * n)
+    a = torch.randn(m, k, generator=g)
+    b = torch.randn(k, n, generator=g)
+    if scale == "rows":
+        a = a * torch.logspace(-6, 6, m).unsqueeze(1)
+        b = b * torch.logspace(4, -4, n).unsqueeze(0)
+    elif scale == "tiny":
+        a, b = a * 1e-20, b * 1e-15
+    elif scale == "huge":
+        a, b = a * 1e18, b * 1e15
+    a, b = a.to(dev), b.to(dev)
+    c = ops.gemm_h3(a, b)
+    ref = a.double() @ b.double()
+    bound = 8 * k * 2.0 ** -24 * (a.abs().double() @ b.abs().double()) + 1e-300
+    assert torch.all((c.double() - ref).abs() <= bound), ((c.double() - ref).abs() / bound).max()
+    # layouts: a column-major view and a k-contiguous b
+    c2 = ops.gemm_h3(a.t().contiguous().t(), b.t().contiguous().t())
+    assert torch.equal(c, c2)

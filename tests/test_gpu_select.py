@@ -88,6 +88,8 @@ def test_topk_rows(dtype, shape, dim, k, largest):
     from heat_amd import ops
 
     dev = _dev()
+    if shape[dim] < k:
+        pytest.skip("k larger than the row")
     x = _data(shape, dtype, seed=k + sum(shape), ties=dtype in (torch.int8,)).to(dev)
     res = ops.topk_rows(x, k, dim, largest)
     assert res is not None
