@@ -4,10 +4,13 @@ split 1 panel broadcast 849-1018).
 
 MI355X design: tall-skinny input (every rank holds >= 2n rows) uses CholeskyQR2 / shifted
 CholeskyQR3 on the matrix cores (``_cholqr``: Gram GEMM + one n x n all-reduce + fp64 Cholesky per
-pass). Otherwise split-0 input uses TSQR - one local Householder QR per rank
-(rocSOLVER geqrf on the rank's block), ONE all-gather of the p small R factors, a redundant QR
-of the stacked R on every rank (no tree latency: p <= 8 per node) and one local GEMM
-``Q_r @ Q2_r`` to form Q. The reference's binary merge tree with per-tile sends and string tags
+pass). When the Cholesky breaks down (cond(A) beyond ~6e7) the rows stay where they are and a
+distributed blocked Householder QR runs instead (``ops.householder_qr``, csrc/householder.hip:
+one kernel per panel column with an fp64 2-vector all-reduce, compact-WY trailing updates as
+GEMMs with one all-reduce of V^T C per panel) - backward stable for any conditioning. Other
+split-0 input uses TSQR - one local QR per rank, ONE all-gather of the p small R factors, a
+redundant QR of the stacked R on every rank (no tree latency: p <= 8 per node) and one local
+GEMM ``Q_r @ Q2_r`` to form Q. The reference's binary merge tree with per-tile sends and string tags
 (``qr.py:477-846``) disappears.
 
 Q mode: the reference returns a complete m x m Q. That is kept for matrices whose complete Q
@@ -63,6 +66,10 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
         res = _cholqr(t, a.comm, calc_q, False) if mode == "reduced" and t.shape[0] >= 2 * n else None
         if res is not None:
             q, r = res
+        elif mode == "reduced" and t.is_cuda:
+            from ... import ops
+
+            q, r = ops.householder_qr(t, 0, t.shape[0], calc_q)  # csrc/householder.hip
         elif mode == "reduced":
             q, r = _local_qr(t, calc_q)
         else:
@@ -147,9 +154,18 @@ def _cholqr_attempt(local: torch.Tensor, comm, calc_q: bool, distributed: bool, 
             comm.Allreduce(MPI.IN_PLACE, g, MPI.SUM)
         return g
 
-    def chol(g: torch.Tensor):
+    # CholeskyQR2 is stable while cond(A) <~ u^{-1/2} of the Gram precision: a Cholesky that
+    # "succeeds" beyond that returns an R whose Q has lost orthogonality (no breakdown to catch).
+    # max/min |diag R| is a cheap lower bound of cond(A); past the limit the caller goes on to the
+    # precise pass, then to Householder.
+    cond_limit = 1e7 if wide == torch.float64 else 1e3
+
+    def chol(g: torch.Tensor, first: bool = False):
         r, info = torch.linalg.cholesky_ex(g.double(), upper=True)
         ok = int(info) == 0 and bool(torch.isfinite(r).all())
+        if ok and first:
+            dg = torch.diagonal(r).abs()
+            ok = bool(dg.min() > 0) and float(dg.max() / dg.min()) <= cond_limit
         if distributed:
             ok = comm.allreduce(int(ok)) == comm.size
         return r if ok else None
@@ -167,7 +183,7 @@ def _cholqr_attempt(local: torch.Tensor, comm, calc_q: bool, distributed: bool, 
     for _, blk in blocks(local):
         bw = blk.to(wide)
         g += _mm(bw.T, bw)
-    r1 = chol(allreduce(g))
+    r1 = chol(allreduce(g), first=True)
     if r1 is None:
         return None
     rinv = tri_inv(r1, wide)
@@ -236,6 +252,22 @@ def _tsqr(local: torch.Tensor, comm, n: int, calc_q: bool):
         res = _cholqr(local, comm, calc_q, True)
         if res is not None:
             return res
+    if local.is_floating_point():
+        # cond(A) beyond CholeskyQR's reach: distributed blocked Householder (one fp64 vector
+        # all-reduce per column, two per panel; csrc/householder.hip) - backward stable for any
+        # conditioning, Q orthogonal to working precision
+        from ... import ops
+        from ..communication import MPI
+
+        counts = comm.allgather_sizes(m_r)
+        g0 = sum(counts[: comm.rank])
+
+        def red(t):
+            comm.Allreduce(MPI.IN_PLACE, t, MPI.SUM)
+            return t
+
+        q, r = ops.householder_qr(local, g0, sum(counts), calc_q, red)
+        return q, r
     if m_r > 0:
         q1, r1 = _local_qr(local, calc_q)  # q1: m_r x min(m_r,n), r1: min(m_r,n) x n
     else:

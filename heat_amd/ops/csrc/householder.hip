@@ -1,0 +1,325 @@
+// Blocked Householder QR building blocks (SURVEY K8 geqrf panel / K9 larfb trailing update) for
+// tall row-distributed matrices: the panel is factorised column by column with ONE kernel per
+// column, the trailing matrix is updated by GEMMs (compact WY: C -= V (T^T (V^T C))).
+//
+// Panel column j (global column k0 + j, diagonal row d = k0 + j) needs, over all rows >= d,
+//   S[c] = sum_{g >= d} A[g][j] A[g][c]   (c >= j)   and   rowd[c] = A[d][c]
+// - one small vector (2 NB doubles) that is summed over the row blocks of all ranks (an RCCL
+// all-reduce between the column kernels when the rows are distributed; every rank's contribution
+// to rowd is zero except the owner's). From it EVERY block computes the reflector redundantly:
+//   alpha = rowd[j], |x| = sqrt(S[j]), beta = -sign(alpha) |x|, tau = (beta - alpha) / beta,
+//   v = x / (alpha - beta) (v_d = 1), w_c = v^T A[:, c] = rowd[c] + (S[c] - alpha rowd[c]) / (alpha - beta)
+// and applies A[g][c] -= tau v_g w_c to its rows g > d, stores v_g in A[g][j] and (owner of d) the
+// R row (beta, rowd[c] - tau w_c) in row d. The same kernel then accumulates the S / rowd vector of
+// column j + 1 from the rows it has just updated - so a panel of NB columns is NB launches, each one
+// pass over the panel's rows, with fp64 accumulation of every dot product.
+//
+// Layout: A row-major (lda), rows of this rank = global rows [g0, g0 + m). 8 lanes own one row (4
+// consecutive panel columns each: 16- or 32-byte accesses, a row segment per 8 lanes), 32 rows per
+// 256-thread block, grid-stride over the rows; block partial sums go through LDS and one atomicAdd
+// per column per block.
+#include "common.h"
+
+namespace {
+
+constexpr int HH_NB = 32;  // panel width (8 lanes x 4 columns)
+
+template <typename T>
+struct Vec4 {
+  T v[4];
+};
+
+template <typename T>
+__device__ __forceinline__ Vec4<T> hh_load4(const T* p, int ncols_here) {
+  Vec4<T> r;
+  if (ncols_here >= 4 && ((uintptr_t)p % (4 * sizeof(T))) == 0) {
+    if constexpr (sizeof(T) == 4) {
+      const floatx4 q = *reinterpret_cast<const floatx4*>(p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r.v[i] = q[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r.v[i] = p[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = i < ncols_here ? p[i] : T(0);
+  }
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ void hh_store4(T* p, const Vec4<T>& r, int ncols_here) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < ncols_here) p[i] = r.v[i];
+}
+
+// Block-reduce the per-lane partials acc[4] (columns 4 q .. 4 q + 3, q = lane % 8) over the 32
+// row groups of the block, then one atomicAdd per column into out[0 .. NB).
+__device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __restrict__ out, double* red) {
+  const int tid = threadIdx.x, q = tid & 7, grp = tid >> 3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[grp * HH_NB + 4 * q + i] = acc[i];
+  __syncthreads();
+  if (tid < HH_NB) {
+    double s = 0.0;
+    for (int g = 0; g < 32; ++g) s += red[g * HH_NB + tid];
+    if (s != 0.0) atomicAdd(out + tid, s);
+  }
+  __syncthreads();
+}
+
+// S / rowd of the first column of a panel: S[c] = sum_{g >= d} A[g][0] A[g][c], rowd = row d.
+template <typename T>
+__global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64_t m, int64_t lda, int64_t g0,
+                                                  int64_t k0, int ncols, int64_t d, double* __restrict__ S) {
+  __shared__ double red[32 * HH_NB];
+  const int q = threadIdx.x & 7;
+  const int nh = ncols - 4 * q < 4 ? (ncols - 4 * q > 0 ? ncols - 4 * q : 0) : 4;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3); i < m; i += (int64_t)gridDim.x * 32) {
+    const int64_t g = g0 + i;
+    if (g < d) continue;
+    const Vec4<T> a = hh_load4(A + i * lda + k0 + 4 * q, nh);
+    const double x0 = (double)__shfl(a.v[0], threadIdx.x & ~7, 64);  // column 0 lives on lane 0 of the group
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] += x0 * (double)a.v[c];
+    if (g == d) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < nh) atomicAdd(S + HH_NB + 4 * q + c, (double)a.v[c]);
+    }
+  }
+  hh_block_sum(acc, S, red);
+}
+
+// One panel column: apply reflector j (from Sin) to this rank's rows, store v / R, accumulate the
+// next column's S / rowd into Sout (nullptr for the panel's last column).
+template <typename T>
+__global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int64_t lda, int64_t g0, int64_t k0,
+                                               int ncols, int j, const double* __restrict__ Sin,
+                                               double* __restrict__ Sout, T* __restrict__ tau) {
+  __shared__ double red[32 * HH_NB];
+  const int64_t d = k0 + j;
+  const int q = threadIdx.x & 7;
+  const int nh = ncols - 4 * q < 4 ? (ncols - 4 * q > 0 ? ncols - 4 * q : 0) : 4;
+  // reflector scalars (identical in every thread of every block)
+  const double alpha = Sin[HH_NB + j];
+  const double nrm2 = Sin[j];
+  const double sig = nrm2 - alpha * alpha;  // sum of squares strictly below the diagonal
+  double beta = alpha, tauv = 0.0, scale = 0.0;
+  if (sig > 0.0 && nrm2 > 0.0) {
+    const double nx = sqrt(nrm2);
+    beta = alpha >= 0.0 ? -nx : nx;
+    tauv = (beta - alpha) / beta;
+    scale = 1.0 / (alpha - beta);
+  }
+  double w[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int col = 4 * q + c;
+    const double rd = Sin[HH_NB + col];
+    w[c] = (col > j && col < ncols) ? rd + scale * (Sin[col] - alpha * rd) : 0.0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) tau[j] = (T)tauv;
+  const int jl = j & 3, jq = j >> 2;              // lane group slot holding column j
+  const int j1 = j + 1, j1l = j1 & 3, j1q = j1 >> 2;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3); i < m; i += (int64_t)gridDim.x * 32) {
+    const int64_t g = g0 + i;
+    if (g < d) continue;  // rows above the diagonal: untouched (the group is uniform in g)
+    T* row = A + i * lda + k0 + 4 * q;
+    Vec4<T> a = hh_load4(row, nh);
+    if (g == d) {
+      // the owner writes the R row: beta on the diagonal, rowd[c] - tau w_c right of it
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = 4 * q + c;
+        if (col == j) a.v[c] = (T)beta;
+        else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * w[c]);
+      }
+      hh_store4(row, a, nh);
+      continue;
+    }
+    // g > d: v_g = x_g / (alpha - beta), A[g][c] -= tau v_g w_c
+    const T xj = __shfl(a.v[jl], (threadIdx.x & ~7) + jq, 64);
+    const double v = (double)xj * scale;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = 4 * q + c;
+      if (col == j) a.v[c] = (T)v;
+      else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * v * w[c]);
+    }
+    hh_store4(row, a, nh);
+    if (Sout) {
+      // next column's sums over rows g >= d + 1 (all rows handled here), row d + 1's values
+      const double x1 = (double)__shfl(a.v[j1l], (threadIdx.x & ~7) + j1q, 64);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] += x1 * (double)a.v[c];
+      if (g == d + 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < nh) atomicAdd(Sout + HH_NB + 4 * q + c, (double)a.v[c]);
+      }
+    }
+  }
+  if (Sout) hh_block_sum(acc, Sout, red);
+}
+
+// larft: T (nb x nb, upper triangular, row-major, ldt = nb) of the compact WY form
+// H_0 ... H_{nb-1} = I - V T V^T from tau and Y = V^T V (fp64, summed over all rows):
+// T[j][j] = tau_j, T[0:j, j] = -tau_j T[0:j, 0:j] Y[0:j, j]. One workgroup; column by column.
+template <typename T>
+__global__ __launch_bounds__(64) void hh_larft(const double* __restrict__ Y, const T* __restrict__ tau, int nb,
+                                               T* __restrict__ Tm) {
+  __shared__ double t[HH_NB * HH_NB];
+  __shared__ double z[HH_NB];
+  const int i = threadIdx.x;
+  for (int e = i; e < HH_NB * HH_NB; e += 64) t[e] = 0.0;
+  __syncthreads();
+  for (int j = 0; j < nb; ++j) {
+    const double tj = (double)tau[j];
+    if (i < j) {
+      double s = 0.0;
+      for (int k = i; k < j; ++k) s += t[i * HH_NB + k] * Y[k * nb + j];
+      z[i] = -tj * s;
+    }
+    __syncthreads();
+    if (i < j) t[i * HH_NB + j] = z[i];
+    if (i == 0) t[j * HH_NB + j] = tj;
+    __syncthreads();
+  }
+  for (int e = i; e < nb * nb; e += 64) Tm[e] = (T)t[(e / nb) * HH_NB + e % nb];
+}
+
+// W[c][j] += sum_i V[i][c] C[i][j] (c < nc <= 32, j < N) over rows [0, m) with FP64 accumulation:
+// the V^T C products of the trailing update / Q accumulation reduce over ALL rows of the matrix
+// (1e6+), where an fp32 GEMM's accumulation error (~sqrt(m) u) would cost orthogonality. Memory /
+// fp64-FMA bound: each C element is read once and feeds 32 fp64 FMAs. Block = 64 columns of C x
+// a row slice (split-K over blockIdx.y); thread (j = t % 64, c-group = t / 64) owns 8 rows of W;
+// V rows are staged through LDS 64 at a time (broadcast reads), partials land by fp64 atomicAdd.
+template <typename T>
+__global__ __launch_bounds__(256) void hh_vtc(const T* __restrict__ V, int64_t ldv, const T* __restrict__ C,
+                                              int64_t ldc, int64_t m, int64_t N, int nc, int64_t rows_per_split,
+                                              double* __restrict__ W, int64_t ldw) {
+  __shared__ T vs[64 * HH_NB];
+  const int t = threadIdx.x, jl = t & 63, cg = t >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + jl;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t r1 = r0 + rows_per_split < m ? r0 + rows_per_split : m;
+  double acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
+  for (int64_t rb = r0; rb < r1; rb += 64) {
+    const int nr = r1 - rb < 64 ? (int)(r1 - rb) : 64;
+    __syncthreads();
+    for (int e = t; e < 64 * HH_NB; e += 256) {
+      const int rr = e / HH_NB, cc = e % HH_NB;
+      vs[e] = (rr < nr && cc < nc) ? V[(rb + rr) * ldv + cc] : T(0);
+    }
+    __syncthreads();
+    if (j < N) {
+      for (int rr = 0; rr < nr; ++rr) {
+        const double x = (double)C[(rb + rr) * ldc + j];
+        const T* vr = vs + rr * HH_NB + 8 * cg;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] = fma((double)vr[c], x, acc[c]);
+      }
+    }
+  }
+  if (j < N) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (8 * cg + c < nc && acc[c] != 0.0) atomicAdd(W + (int64_t)(8 * cg + c) * ldw + j, acc[c]);
+  }
+}
+
+int hh_grid(int64_t m) {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int64_t need = (m + 31) / 32;
+  const int64_t cap = 2LL * ncu;  // the per-column atomics stay few
+  return (int)(need < cap ? (need > 0 ? need : 1) : cap);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------ C ABI
+HA_EXPORT int ha_hh_nb() { return HH_NB; }
+
+// S (2 NB doubles, zeroed by the caller) += column-0 sums of the panel at column k0 (ncols <= NB
+// columns) over this rank's rows g >= d, and row d's values if this rank owns it.
+HA_EXPORT int ha_hh_colsums(const void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols,
+                            int64_t d, double* S, void* stream) {
+  if (ncols <= 0 || ncols > HH_NB || m < 0) return HA_BAD_ARG;
+  if (m == 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 0)
+    hipLaunchKernelGGL(hh_colsums<float>, dim3(hh_grid(m)), dim3(256), 0, s, (const float*)A, m, lda, g0, k0, ncols,
+                       d, S);
+  else
+    hipLaunchKernelGGL(hh_colsums<double>, dim3(hh_grid(m)), dim3(256), 0, s, (const double*)A, m, lda, g0, k0, ncols,
+                       d, S);
+  return ha_launch_status();
+}
+
+// Reflector j of the panel (see the header); Sout (zeroed, 2 NB doubles) receives column j + 1's
+// partial sums unless it is null.
+HA_EXPORT int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols, int j,
+                         const double* Sin, double* Sout, void* tau, void* stream) {
+  if (ncols <= 0 || ncols > HH_NB || j < 0 || j >= ncols || m < 0) return HA_BAD_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = hh_grid(m);
+  if (dtype == 0)
+    hipLaunchKernelGGL(hh_step<float>, dim3(grid), dim3(256), 0, s, (float*)A, m, lda, g0, k0, ncols, j, Sin, Sout,
+                       (float*)tau);
+  else
+    hipLaunchKernelGGL(hh_step<double>, dim3(grid), dim3(256), 0, s, (double*)A, m, lda, g0, k0, ncols, j, Sin, Sout,
+                       (double*)tau);
+  return ha_launch_status();
+}
+
+HA_EXPORT int ha_hh_larft(const double* Y, const void* tau, int nb, int dtype, void* Tm, void* stream) {
+  if (nb <= 0 || nb > HH_NB) return HA_BAD_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 0)
+    hipLaunchKernelGGL(hh_larft<float>, dim3(1), dim3(64), 0, s, Y, (const float*)tau, nb, (float*)Tm);
+  else
+    hipLaunchKernelGGL(hh_larft<double>, dim3(1), dim3(64), 0, s, Y, (const double*)tau, nb, (double*)Tm);
+  return ha_launch_status();
+}
+
+// W (fp64 [nc][ldw], zeroed by the caller) += V[:, :nc]^T C[:, :N] over m rows, fp64 accumulation.
+HA_EXPORT int ha_hh_vtc(const void* V, int64_t ldv, const void* C, int64_t ldc, int dtype, int64_t m, int64_t N,
+                        int nc, double* W, int64_t ldw, void* stream) {
+  if (nc <= 0 || nc > HH_NB || m < 0 || N < 0) return HA_BAD_ARG;
+  if (m == 0 || N == 0) return HA_OK;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int64_t bx = (N + 63) / 64;
+  int64_t splits = (4LL * ncu + bx - 1) / bx;               // ~4 blocks per CU overall
+  const int64_t maxs = (m + 255) / 256;                     // >= 256 rows per split
+  splits = splits < maxs ? splits : maxs;
+  splits = splits < 1 ? 1 : splits > 65535 ? 65535 : splits;
+  const int64_t rps = ((m + splits - 1) / splits + 63) / 64 * 64;
+  splits = (m + rps - 1) / rps;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 0)
+    hipLaunchKernelGGL(hh_vtc<float>, dim3((unsigned)bx, (unsigned)splits), dim3(256), 0, s, (const float*)V, ldv,
+                       (const float*)C, ldc, m, N, nc, rps, W, ldw);
+  else
+    hipLaunchKernelGGL(hh_vtc<double>, dim3((unsigned)bx, (unsigned)splits), dim3(256), 0, s, (const double*)V, ldv,
+                       (const double*)C, ldc, m, N, nc, rps, W, ldw);
+  return ha_launch_status();
+}

@@ -16,7 +16,7 @@ from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
-           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3"]
+           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr"]
 
 _NUM_CUS = {}
 
@@ -946,3 +946,160 @@ def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     check(lib().ha_gemm_h3(_ptr(ahi), _ptr(alo), _ptr(bhi), _ptr(blo), _ptr(ea), _ptr(eb), _ptr(out), M, N, Kp,
                            out.stride(0) if M > 1 else N, ctypes.c_void_p(stream_ptr(a.device))), "ha_gemm_h3")
     return out
+
+
+# --------------------------------------------------------------------------------------------- Householder QR
+def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = True, allreduce=None):
+    """Blocked Householder QR of a row block (rows [g0, g0 + m_r) of an m_total x n matrix whose
+    other rows live on other ranks) - ``csrc/householder.hip``: one kernel per panel column
+    (geqrf panel, fp64 dot products), compact-WY T by ``hh_larft`` and the trailing update
+    C -= V (T^T (V^T C)) as two GEMMs. ``allreduce(t)`` sums a device tensor over the ranks in
+    place (None: a single block holds all rows). Backward stable for any conditioning.
+
+    Returns (this rank's rows of the reduced Q or None, R [min(m, n), n] replicated), with
+    diag(R) >= 0."""
+    native = local.is_cuda and use_native(local)
+    L = lib() if native else None
+    nb = L.ha_hh_nb() if native else 32
+    dev = local.device
+    dt = local.dtype
+    code = 0 if dt == torch.float32 else 1
+    m_r, n = local.shape
+    kmax = min(m_total, n)
+    A = local.contiguous().clone()
+    st = ctypes.c_void_p(stream_ptr(dev)) if native else None
+    red = allreduce or (lambda t: t)
+    rows = torch.arange(g0, g0 + m_r, device=dev).unsqueeze(1)
+    panels = []
+    for k0 in range(0, kmax, nb):
+        nc = min(nb, kmax - k0)
+        S = torch.zeros((nc + 1, 2 * nb), dtype=torch.float64, device=dev)
+        tau = torch.empty(nc, dtype=dt, device=dev)
+        if native:
+            check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), st), "ha_hh_colsums")
+        else:
+            _hh_colsums_host(A, rows, k0, nc, S[0])
+        red(S[0])
+        for j in range(nc):
+            last = j + 1 == nc
+            if native:
+                check(L.ha_hh_step(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, j, _ptr(S[j]),
+                                   _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), st), "ha_hh_step")
+            else:
+                _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau)
+            if not last:
+                red(S[j + 1])
+        V = _hh_v(A, rows, k0, nc)
+        Y = V.double().T @ V.double()
+        red(Y)
+        Tm = torch.empty((nc, nc), dtype=dt, device=dev)
+        if native:
+            check(L.ha_hh_larft(_ptr(Y.contiguous()), _ptr(tau), nc, code, _ptr(Tm), st), "ha_hh_larft")
+        else:
+            Tm.copy_(_hh_larft_host(Y, tau))
+        panels.append((k0, nc, Tm))
+        if k0 + nc < n:
+            C = A[:, k0 + nc:]
+            W = _vtc(V, C, native, st)   # fp64 reduction over all rows
+            red(W)
+            C.addmm_(V, (Tm.double().T @ W).to(dt), alpha=-1.0)
+    # R: the upper triangle of global rows [0, kmax), gathered from their owners by the all-reduce
+    R = torch.zeros((kmax, n), dtype=dt, device=dev)
+    lo, hi = max(g0, 0), min(g0 + m_r, kmax)
+    if hi > lo:
+        R[lo:hi] = torch.triu(A[lo - g0: hi - g0], diagonal=lo)
+    red(R)
+    d = torch.sign(torch.diagonal(R))
+    d = torch.where(d == 0, torch.ones_like(d), d)
+    R = d.unsqueeze(1) * R
+    if not calc_q:
+        return None, R
+    Q = torch.zeros((m_r, kmax), dtype=dt, device=dev)
+    if hi > lo:
+        Q[lo - g0: hi - g0, lo:hi] = torch.eye(hi - lo, dtype=dt, device=dev)
+    for k0, nc, Tm in reversed(panels):
+        V = _hh_v(A, rows, k0, nc)
+        Qc = Q[:, k0:]
+        W = _vtc(V, Qc, native, st)
+        red(W)
+        Qc.addmm_(V, (Tm.double() @ W).to(dt), alpha=-1.0)
+    return Q * d.unsqueeze(0), R
+
+
+def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:
+    """V^T C in fp64 accumulation (``hh_vtc``; host: an fp64 GEMM)."""
+    if not native:
+        return V.double().T @ C.double()
+    nc, N = V.shape[1], C.shape[1]
+    W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)
+    if C.stride(1) != 1:
+        C = C.contiguous()
+    check(lib().ha_hh_vtc(_ptr(V), V.stride(0), _ptr(C), C.stride(0), 0 if V.dtype == torch.float32 else 1,
+                          V.shape[0], N, nc, _ptr(W), W.stride(0), st), "ha_hh_vtc")
+    return W
+
+
+def _hh_v(A: torch.Tensor, rows: torch.Tensor, k0: int, nc: int) -> torch.Tensor:
+    """Explicit reflectors of a factorised panel: V[g, c] = A[g, k0 + c] below the diagonal row
+    k0 + c, 1 on it, 0 above."""
+    dcol = torch.arange(k0, k0 + nc, device=A.device).unsqueeze(0)
+    P = A[:, k0: k0 + nc]
+    return torch.where(rows > dcol, P, (rows == dcol).to(A.dtype))
+
+
+# host (CPU) reference of the panel kernels: same math, same buffer conventions (the oracle of the
+# tests and the CPU / gloo multi-rank path)
+def _hh_colsums_host(A, rows, k0, nc, S):
+    below = (rows[:, 0] >= k0)
+    P = A[below, k0: k0 + nc].double()
+    S[:nc] += P[:, 0] @ P
+    own = rows[:, 0] == k0
+    if bool(own.any()):
+        S[32: 32 + nc] += A[own, k0: k0 + nc].double().reshape(-1)
+
+
+def _hh_step_host(A, rows, k0, nc, j, Sin, Sout, tau):
+    d = k0 + j
+    alpha = float(Sin[32 + j])
+    nrm2 = float(Sin[j])
+    sig = nrm2 - alpha * alpha
+    beta, tv, scale = alpha, 0.0, 0.0
+    if sig > 0.0 and nrm2 > 0.0:
+        nx = nrm2 ** 0.5
+        beta = -nx if alpha >= 0 else nx
+        tv = (beta - alpha) / beta
+        scale = 1.0 / (alpha - beta)
+    tau[j] = tv
+    rd = Sin[32: 32 + nc]
+    w = rd + scale * (Sin[:nc] - alpha * rd)
+    w[: j + 1] = 0.0
+    g = rows[:, 0]
+    own = g == d
+    if bool(own.any()):
+        r = A[own, k0: k0 + nc].double()
+        r[:, j + 1:] -= tv * w[j + 1:]
+        r[:, j] = beta
+        A[own, k0: k0 + nc] = r.to(A.dtype)
+    below = g > d
+    P = A[below, k0: k0 + nc].double()
+    v = P[:, j] * scale
+    P -= tv * v.unsqueeze(1) * w.unsqueeze(0)
+    P[:, j] = v
+    A[below, k0: k0 + nc] = P.to(A.dtype)
+    if Sout is not None:
+        P = A[below, k0: k0 + nc].double()
+        Sout[:nc] += P[:, j + 1] @ P
+        nxt = g == d + 1
+        if bool(nxt.any()):
+            Sout[32: 32 + nc] += A[nxt, k0: k0 + nc].double().reshape(-1)
+
+
+def _hh_larft_host(Y, tau):
+    nc = tau.shape[0]
+    T = torch.zeros((nc, nc), dtype=torch.float64, device=Y.device)
+    for j in range(nc):
+        tj = float(tau[j])
+        if j:
+            T[:j, j] = -tj * (T[:j, :j] @ Y[:j, j])
+        T[j, j] = tj
+    return T.to(tau.dtype)

@@ -324,3 +324,19 @@ def check_nonblocking_v_collectives():
     if r == 0:
         exp = torch.cat([torch.full((q + 1, 2), float(q)) for q in range(p)])
         assert torch.equal(g, exp)
+
+
+def check_qr_ill_conditioned_householder():
+    """cond(A) = 1e12 (fp64): CholeskyQR2 breaks down, the distributed Householder path must give
+    an orthogonal Q and A = QR on every split."""
+    rng = np.random.default_rng(20)
+    for m, n in ((120, 17), (64, 40), (300, 33)):
+        u, _ = np.linalg.qr(rng.standard_normal((m, n)))
+        v, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        a = (u * np.logspace(0, -12, n)) @ v.T
+        for s in (None, 0):
+            q, r = ht.linalg.qr(ht.array(a, split=s), mode="reduced")
+            qn, rn = q.numpy(), r.numpy()
+            assert np.abs(qn.T @ qn - np.eye(n)).max() < 1e-12, np.abs(qn.T @ qn - np.eye(n)).max()
+            assert np.abs(qn @ rn - a).max() < 1e-12 * np.abs(a).max() * 10
+            assert np.allclose(rn, np.triu(rn))
