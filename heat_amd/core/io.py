@@ -356,72 +356,301 @@ def load_netcdf(path: str, variable: str, dtype=types.float32, split: Optional[i
     return DNDarray(t, gshape, htype, split, device, comm, True)
 
 
+_NC_TYPES = {1: np.dtype("i1"), 2: np.dtype("S1"), 3: np.dtype(">i2"), 4: np.dtype(">i4"), 5: np.dtype(">f4"),
+             6: np.dtype(">f8")}
+_NC_WRITE_MODES = ("w", "a", "r+")
+
+
+def _nc_classic_layout(path: str, variable: str):
+    """Parse the header of a classic netCDF file (CDF-1 / CDF-2) and return the data layout of
+    ``variable``: (shape with the current record count, big-endian dtype, begin offset, record
+    stride in bytes or None for a fixed-size variable, numrecs offset in the file)."""
+    import struct
+
+    with open(path, "rb") as f:
+        buf = f.read(1 << 16)
+        pos = [0]
+
+        def need(n):
+            nonlocal buf
+            while pos[0] + n > len(buf):
+                more = f.read(1 << 16)
+                if not more:
+                    raise ValueError("truncated netCDF header")
+                buf += more
+
+        def i4():
+            need(4)
+            v = struct.unpack(">i", buf[pos[0]: pos[0] + 4])[0]
+            pos[0] += 4
+            return v
+
+        def i8():
+            need(8)
+            v = struct.unpack(">q", buf[pos[0]: pos[0] + 8])[0]
+            pos[0] += 8
+            return v
+
+        def name():
+            n = i4()
+            need(n + (-n) % 4)
+            v = buf[pos[0]: pos[0] + n].decode("utf-8")
+            pos[0] += n + (-n) % 4
+            return v
+
+        def skip_atts():
+            tag, n = i4(), i4()
+            for _ in range(n if tag else 0):
+                name()
+                t, cnt = i4(), i4()
+                size = cnt * _NC_TYPES[t].itemsize
+                need(size + (-size) % 4)
+                pos[0] += size + (-size) % 4
+
+        need(4)
+        if buf[:3] != b"CDF" or buf[3] not in (1, 2):
+            raise ValueError("{} is not a classic netCDF file".format(path))
+        off64 = buf[3] == 2
+        pos[0] = 4
+        numrecs_at = 4
+        numrecs = i4()
+        tag, nd = i4(), i4()
+        dims = [(name(), i4()) for _ in range(nd if tag else 0)]
+        skip_atts()
+        tag, nv = i4(), i4()
+        vars_ = {}
+        for _ in range(nv if tag else 0):
+            vn = name()
+            ndv = i4()
+            dimids = [i4() for _ in range(ndv)]
+            skip_atts()
+            t, vsize = i4(), i4()
+            begin = i8() if off64 else i4()
+            vars_[vn] = (dimids, t, vsize, begin)
+    if variable not in vars_:
+        raise KeyError(variable)
+    dimids, t, vsize, begin = vars_[variable]
+    is_rec = bool(dimids) and dims[dimids[0]][1] == 0
+    recsize = sum(v[2] for v in vars_.values() if v[0] and dims[v[0][0]][1] == 0)
+    if sum(1 for v in vars_.values() if v[0] and dims[v[0][0]][1] == 0) == 1:
+        recsize = vsize  # a single record variable is not padded per record
+    shape = tuple(numrecs if (k == 0 and is_rec) else dims[d][1] for k, d in enumerate(dimids))
+    return shape, _NC_TYPES[t], begin, (recsize if is_rec else None), numrecs_at
+
+
+def _nc_memmap(path: str, shape, dtype, begin: int, recsize: Optional[int]):
+    """Writable strided view of a classic variable's data (records at ``recsize`` strides)."""
+    if recsize is None:
+        return np.memmap(path, dtype=dtype, mode="r+", offset=begin, shape=shape)
+    nrec = shape[0]
+    inner = int(np.prod(shape[1:])) if len(shape) > 1 else 1
+    if nrec == 0:
+        return np.zeros(shape, dtype=dtype)
+    raw = np.memmap(path, dtype=np.uint8, mode="r+", offset=begin, shape=((nrec - 1) * recsize + inner * dtype.itemsize,))
+    strides = (recsize,) + tuple(int(np.prod(shape[k + 1:])) * dtype.itemsize for k in range(1, len(shape)))
+    return np.ndarray(shape, dtype=dtype, buffer=raw, strides=strides)
+
+
+def _normalize_file_slices(file_slices, ndim: int) -> tuple:
+    if file_slices is None or file_slices is True:
+        return (slice(None),) * ndim
+    key = file_slices if isinstance(file_slices, tuple) else (file_slices,)
+    if any(k is Ellipsis for k in key):
+        i = key.index(Ellipsis)
+        key = key[:i] + (slice(None),) * (ndim - len(key) + 1) + key[i + 1:]
+    return tuple(key) + (slice(None),) * (ndim - len(key))
+
+
 def save_netcdf(data: DNDarray, path: str, variable: str, mode: str = "w", dimension_names=None,
-                **kwargs) -> None:
-    """Write a DNDarray as a netCDF variable. Without netCDF4 a classic (CDF-2) file is written:
-    rank 0 writes the header, every rank writes its slab of the big-endian data block in place."""
+                is_unlimited: bool = False, file_slices=slice(None), **kwargs) -> None:
+    """Write a DNDarray as a netCDF variable (reference io.py:348-650: same modes ``'w', 'a', 'r+'``,
+    ``dimension_names``, ``is_unlimited`` and ``file_slices`` - the keys of the file variable the
+    data is written to, e.g. a record range of an existing unlimited variable).
+
+    With netCDF4: rank 0 defines dimensions / the variable, then the ranks write their slabs in
+    turn. Without it: a classic netCDF (CDF-2) file; rank 0 defines the structure (new file, or an
+    added dimension / variable in an existing file through ``scipy.io.netcdf_file``), grows the
+    record count of an unlimited variable to what ``file_slices`` addresses, and EVERY rank then
+    writes its slab in place through a memory map of the variable's data (record variables as a
+    strided view) - parallel, no gather. Classic files allow one unlimited dimension, the first of a
+    record variable: ``is_unlimited`` makes the variable's first new dimension unlimited. An
+    exception on any rank is raised on every rank."""
     if not isinstance(data, DNDarray):
         raise TypeError("data must be heat tensor, not {}".format(type(data)))
     if not isinstance(path, str):
         raise TypeError("path must be str, not {}".format(type(path)))
     if not isinstance(variable, str):
         raise TypeError("variable must be str, not {}".format(type(variable)))
+    if mode not in _NC_WRITE_MODES:
+        raise ValueError("mode was {}, not in possible modes {}".format(mode, _NC_WRITE_MODES))
     comm = data.comm
     if dimension_names is None:
-        dimension_names = ["dim_{}".format(i) for i in range(data.ndim)]
+        dimension_names = ["{}_dim_{}".format(variable, i) for i in range(data.ndim)]
     elif isinstance(dimension_names, str):
         dimension_names = [dimension_names]
+    elif isinstance(dimension_names, tuple):
+        dimension_names = list(dimension_names)
+    elif not isinstance(dimension_names, list):
+        raise TypeError("dimension_names must be list or tuple or string, not{}".format(type(dimension_names)))
     if len(dimension_names) != data.ndim:
         raise ValueError("{0} names given for {1} dimensions".format(len(dimension_names), data.ndim))
     counts, displs = data.counts_displs() if data.is_distributed() else ((data.gshape[0] if data.ndim else 1,), (0,))
     local = data.larray.cpu().numpy()
-    sl = [slice(None)] * data.ndim
+    lsl = [slice(None)] * data.ndim
     if data.is_distributed():
-        sl[data.split] = slice(displs[comm.rank], displs[comm.rank] + counts[comm.rank])
+        lsl[data.split] = slice(displs[comm.rank], displs[comm.rank] + counts[comm.rank])
+    key = _normalize_file_slices(file_slices, data.ndim)
     exc = None
     if nc is not None:
         if comm.rank == 0:
             try:
                 with nc.Dataset(path, mode) as handle:
-                    for name, size in zip(dimension_names, data.gshape):
-                        if name not in handle.dimensions:
-                            handle.createDimension(name, size)
-                    handle.createVariable(variable, local.dtype, tuple(dimension_names), **kwargs)
+                    if variable not in handle.variables:
+                        for name, size in zip(dimension_names, data.gshape):
+                            if name not in handle.dimensions:
+                                handle.createDimension(name, None if is_unlimited else size)
+                        handle.createVariable(variable, local.dtype, tuple(dimension_names), **kwargs)
             except Exception as e:
                 exc = e
         _exception_barrier(comm, exc)
         for r in range(comm.size):
             if r == comm.rank and (data.is_distributed() or r == 0):
-                with nc.Dataset(path, "r+") as handle:
-                    handle[variable][tuple(sl)] = local
+                try:
+                    with nc.Dataset(path, "r+") as handle:
+                        var = handle[variable]
+                        target = np.empty(0)  # shape probe of the addressed region
+                        full = _file_region(var.shape, key, data.gshape)
+                        var[_sub_region(full, data, lsl)] = local
+                except Exception as e:
+                    exc = e
             comm.Barrier()
+        _exception_barrier(comm, exc)
         return
-    if mode != "w":
-        raise NotImplementedError("without netCDF4 only mode='w' (a new classic file) is supported")
     np_dtype = np.dtype(local.dtype)
     if np_dtype == np.dtype("i8"):
         np_dtype = np.dtype("i4")
     elif np_dtype == np.dtype("bool") or np_dtype == np.dtype("u1"):
         np_dtype = np.dtype("i1")
-    begin = 0
+    elif np_dtype == np.dtype("f2"):
+        np_dtype = np.dtype("f4")
+    layout = None
+    # rank 0 may truncate / restructure the file: every rank must be done with earlier reads of it
+    comm.Barrier()
     if comm.rank == 0:
         try:
-            header, begin = _netcdf3_header(variable, dimension_names, data.gshape, np_dtype)
-            nbytes = int(np.prod(data.gshape)) * np_dtype.itemsize
-            with open(path, "wb") as f:
-                f.write(header)
-                f.truncate(begin + nbytes + ((-nbytes) % 4))
+            layout = _nc_define_classic(path, variable, mode, dimension_names, data.gshape, np_dtype, is_unlimited,
+                                        key)
         except Exception as e:
             exc = e
     _exception_barrier(comm, exc)
-    begin = comm.bcast(begin, root=0)
-    if data.is_distributed() or comm.rank == 0:
-        if local.size:
-            mm = np.memmap(path, dtype=np_dtype.newbyteorder(">"), mode="r+", offset=begin, shape=data.gshape)
-            mm[tuple(sl)] = local.astype(np_dtype)
-            mm.flush()
+    shape, dt, begin, recsize, _ = comm.bcast(layout, root=0)
+    try:
+        if (data.is_distributed() or comm.rank == 0) and local.size:
+            mm = _nc_memmap(path, shape, dt, begin, recsize)
+            full = _file_region(shape, key, data.gshape, recsize is not None)
+            mm[_sub_region(full, data, lsl)] = local.astype(dt)
+            if isinstance(mm, np.memmap):
+                mm.flush()
+            elif hasattr(mm, "base") and isinstance(mm.base, np.memmap):
+                mm.base.flush()
             del mm
+    except Exception as e:
+        exc = e
     comm.Barrier()
+    _exception_barrier(comm, exc)
+
+
+def _file_region(var_shape, key, data_shape, record: bool = False):
+    """The file-variable key as a tuple of slices / int arrays addressing exactly ``data_shape``
+    elements (ints drop a dimension like NumPy). ``record``: dimension 0 is unlimited, where an
+    open-ended slice means "as many records as the data has" (netCDF semantics)."""
+    out = []
+    for i, (k, n) in enumerate(zip(key, var_shape)):
+        if record and i == 0 and isinstance(k, slice) and k.stop is None:
+            start, step = k.start or 0, k.step or 1
+            out.append(range(start, start + step * data_shape[0], step))
+        elif isinstance(k, slice):
+            out.append(range(*k.indices(n)) if k.stop is not None or n else range(k.start or 0, k.stop or 0))
+        elif isinstance(k, (int, np.integer)):
+            out.append(int(k) + n if k < 0 else int(k))
+        else:
+            out.append(np.asarray(k))
+    kept = [len(r) if isinstance(r, range) else (len(r) if isinstance(r, np.ndarray) else None) for r in out]
+    kept = tuple(x for x in kept if x is not None)
+    if kept != tuple(data_shape):
+        raise ValueError("file_slices address shape {} but the data has shape {}".format(kept, tuple(data_shape)))
+    return out
+
+
+def _sub_region(full, data: DNDarray, lsl) -> tuple:
+    """Narrow the file region to this rank's slab of the data (the split dimension)."""
+    key, d = [], 0
+    for r in full:
+        if isinstance(r, int):
+            key.append(r)
+            continue
+        sel = lsl[d]
+        rr = r[sel] if isinstance(sel, slice) else r
+        if isinstance(rr, range):
+            key.append(slice(rr.start, rr.stop, rr.step) if len(rr) else slice(0, 0))
+        else:
+            key.append(rr)
+        d += 1
+    return tuple(key)
+
+
+def _nc_define_classic(path, variable, mode, dims, gshape, np_dtype, is_unlimited, key):
+    """Rank 0: create / extend the classic file so that ``variable`` exists and holds the region
+    ``key`` addresses; returns its data layout."""
+    import os
+
+    exists = os.path.exists(path)
+    if mode == "w" or not exists:
+        if mode == "r+" and not exists:
+            raise FileNotFoundError(path)
+        if not is_unlimited:
+            header, begin = _netcdf3_header(variable, dims, gshape, np_dtype)
+            nbytes = int(np.prod(gshape)) * np_dtype.itemsize
+            with open(path, "wb") as f:
+                f.write(header)
+                f.truncate(begin + nbytes + ((-nbytes) % 4))
+            return _nc_classic_layout(path, variable)
+        if os.path.exists(path):
+            os.unlink(path)
+    from scipy.io import netcdf_file
+
+    with netcdf_file(path, "a" if os.path.exists(path) else "w", version=2, mmap=False) as h:
+        if variable not in h.variables:
+            for i, (name, size) in enumerate(zip(dims, gshape)):
+                if name not in h.dimensions:
+                    h.createDimension(name, None if (is_unlimited and i == 0) else size)
+            v = h.createVariable(variable, np_dtype.newbyteorder("="), tuple(dims))
+            if dims and h.dimensions[dims[0]] is None:
+                # one zero record, so the header carries the record size (scipy writes vsize from data)
+                v[0] = np.zeros(tuple(gshape[1:]), dtype=np_dtype.newbyteorder("="))
+    shape, dt, begin, recsize, nr_at = _nc_classic_layout(path, variable)
+    if recsize is not None:
+        # grow the record count to what the write addresses (zero-filled records)
+        k0 = key[0]
+        need = gshape[0]
+        if isinstance(k0, slice):
+            start = k0.start or 0
+            step = k0.step or 1
+            need = start + step * (gshape[0] - 1) + 1 if gshape[0] else start
+        elif isinstance(k0, (int, np.integer)):
+            need = int(k0) + 1
+        if need > shape[0]:
+            import struct
+
+            with open(path, "r+b") as f:
+                f.seek(nr_at)
+                f.write(struct.pack(">i", int(need)))
+                end = begin + need * recsize
+                f.seek(0, 2)
+                if f.tell() < end:
+                    f.truncate(end + (-end) % 4)
+            shape, dt, begin, recsize, nr_at = _nc_classic_layout(path, variable)
+    return shape, dt, begin, recsize, nr_at
 
 
 DNDarray.save_netcdf = lambda self, path, variable, mode="w", **kwargs: save_netcdf(self, path, variable, mode, **kwargs)

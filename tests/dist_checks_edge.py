@@ -340,3 +340,43 @@ def check_qr_ill_conditioned_householder():
             assert np.abs(qn.T @ qn - np.eye(n)).max() < 1e-12, np.abs(qn.T @ qn - np.eye(n)).max()
             assert np.abs(qn @ rn - a).max() < 1e-12 * np.abs(a).max() * 10
             assert np.allclose(rn, np.triu(rn))
+
+
+def check_netcdf_modes_unlimited_slices():
+    """save_netcdf without netCDF4 (classic CDF-2): mode 'w' / 'a' / 'r+', several variables per
+    file, an unlimited (record) dimension grown by later writes, and file_slices - parity with the
+    reference's netCDF4 path (io.py:348-650), every rank writing its slab in place."""
+    import os
+    import tempfile
+
+    comm = ht.MPI_WORLD
+    d = comm.bcast(tempfile.mkdtemp(prefix="ht_nc_") if comm.rank == 0 else None, root=0)
+    a = np.arange(7 * 5, dtype=np.float32).reshape(7, 5)
+    p = os.path.join(d, "m.nc")
+    for s in (None, 0, 1):
+        ht.save_netcdf(ht.array(a, split=s), p, "x", mode="w")
+        assert np.array_equal(ht.load_netcdf(p, "x").numpy(), a)
+        ht.save_netcdf(ht.array(2 * a, split=s), p, "y", mode="a", dimension_names=["r", "c"])
+        assert np.array_equal(ht.load_netcdf(p, "y", split=0).numpy(), 2 * a)
+        assert np.array_equal(ht.load_netcdf(p, "x").numpy(), a)        # untouched by the append
+        ht.save_netcdf(ht.array(a[:3] + 100, split=s), p, "x", mode="r+", file_slices=slice(2, 5))
+        exp = a.copy()
+        exp[2:5] = a[:3] + 100
+        assert np.array_equal(ht.load_netcdf(p, "x").numpy(), exp)
+        ht.save_netcdf(ht.array(a[:, 1] - 1, split=0 if s is not None else None), p, "x", mode="r+",
+                       file_slices=(slice(None), 1))
+        exp[:, 1] = a[:, 1] - 1
+        assert np.array_equal(ht.load_netcdf(p, "x").numpy(), exp)
+    q = os.path.join(d, "u.nc")
+    ht.save_netcdf(ht.array(a, split=0), q, "z", is_unlimited=True, dimension_names=["t", "c"])
+    ht.save_netcdf(ht.array(a[:4] + 50, split=0), q, "z", mode="a", file_slices=slice(7, 11))
+    z = ht.load_netcdf(q, "z").numpy()
+    assert z.shape == (11, 5) and np.array_equal(z[:7], a) and np.array_equal(z[7:], a[:4] + 50)
+    comm.Barrier()
+    for bad in (lambda: ht.save_netcdf(ht.array(a), p, "x", mode="x"),
+                lambda: ht.save_netcdf(ht.array(a), p, "x", dimension_names=["only_one"])):
+        try:
+            bad()
+            raise AssertionError("must raise")
+        except ValueError:
+            pass
