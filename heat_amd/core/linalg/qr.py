@@ -156,16 +156,15 @@ def _cholqr_attempt(local: torch.Tensor, comm, calc_q: bool, distributed: bool, 
 
     # CholeskyQR2 is stable while cond(A) <~ u^{-1/2} of the Gram precision: a Cholesky that
     # "succeeds" beyond that returns an R whose Q has lost orthogonality (no breakdown to catch).
-    # max/min |diag R| is a cheap lower bound of cond(A); past the limit the caller goes on to the
-    # precise pass, then to Householder.
+    # cond(R) = cond(A) is estimated by power / inverse iteration on R^T R (O(n^2) per step); past
+    # the limit the caller goes on to the precise pass, then to Householder.
     cond_limit = 1e7 if wide == torch.float64 else 1e3
 
     def chol(g: torch.Tensor, first: bool = False):
         r, info = torch.linalg.cholesky_ex(g.double(), upper=True)
         ok = int(info) == 0 and bool(torch.isfinite(r).all())
         if ok and first:
-            dg = torch.diagonal(r).abs()
-            ok = bool(dg.min() > 0) and float(dg.max() / dg.min()) <= cond_limit
+            ok = _cond_estimate(r) <= cond_limit
         if distributed:
             ok = comm.allreduce(int(ok)) == comm.size
         return r if ok else None
@@ -206,6 +205,36 @@ def _cholqr_attempt(local: torch.Tensor, comm, calc_q: bool, distributed: bool, 
     for r0, blk in blocks(q):
         q[r0: r0 + blk.shape[0]] = _mm(blk, rinv2)
     return q, rtot
+
+
+def _cond_estimate(r: torch.Tensor, iters: int = 12) -> float:
+    """2-norm condition number estimate of an upper triangular R: power iteration on R^T R for the
+    largest singular value, inverse iteration (two triangular solves per step) for the smallest.
+    Deterministic start vector (every rank computes the same replicated R and the same answer)."""
+    n = r.shape[0]
+    if n == 0:
+        return 1.0
+    r = r.double()
+    g = torch.Generator(device="cpu").manual_seed(12345)
+    x0 = torch.rand(n, 1, generator=g, dtype=torch.float64).to(r.device) + 0.5
+    x = x0 / x0.norm()
+    smax = 0.0
+    for _ in range(iters):
+        y = r.T @ (r @ x)
+        smax = float(y.norm())
+        if smax == 0.0:
+            return float("inf")
+        x = y / smax
+    x = x0 / x0.norm()
+    inv = 0.0
+    for _ in range(iters):
+        z = torch.linalg.solve_triangular(r.T, x, upper=False)
+        y = torch.linalg.solve_triangular(r, z, upper=True)
+        inv = float(y.norm())
+        if not inv < float("inf"):
+            return float("inf")
+        x = y / inv
+    return (smax * inv) ** 0.5
 
 
 def _local_qr(t: torch.Tensor, calc_q: bool = True):

@@ -22,7 +22,10 @@
 
 namespace {
 
-constexpr int HH_NB = 32;  // panel width (8 lanes x 4 columns)
+constexpr int HH_NB = 32;     // panel width (8 lanes x 4 columns)
+constexpr int HH_COPIES = 32; // replicated S accumulators: block b adds into copy b % 32, so the
+                              // fp64 atomics of the ~2 blocks/CU spread over 32x the addresses
+constexpr int HH_SLEN = 2 * HH_NB;  // one copy: S[NB] | rowd[NB]
 
 template <typename T>
 struct Vec4 {
@@ -65,7 +68,18 @@ __device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __r
   if (tid < HH_NB) {
     double s = 0.0;
     for (int g = 0; g < 32; ++g) s += red[g * HH_NB + tid];
-    if (s != 0.0) atomicAdd(out + tid, s);
+    if (s != 0.0) atomicAdd(out + (blockIdx.x % HH_COPIES) * HH_SLEN + tid, s);
+  }
+  __syncthreads();
+}
+
+// Sum of the HH_COPIES replicated accumulators of one S buffer into LDS (every block).
+__device__ __forceinline__ void hh_gather_s(const double* __restrict__ S, double* __restrict__ out) {
+  for (int e = threadIdx.x; e < HH_SLEN; e += blockDim.x) {
+    double v = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < HH_COPIES; ++c) v += S[c * HH_SLEN + e];
+    out[e] = v;
   }
   __syncthreads();
 }
@@ -101,12 +115,14 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
                                                int ncols, int j, const double* __restrict__ Sin,
                                                double* __restrict__ Sout, T* __restrict__ tau) {
   __shared__ double red[32 * HH_NB];
+  __shared__ double sin_[HH_SLEN];
+  hh_gather_s(Sin, sin_);
   const int64_t d = k0 + j;
   const int q = threadIdx.x & 7;
   const int nh = ncols - 4 * q < 4 ? (ncols - 4 * q > 0 ? ncols - 4 * q : 0) : 4;
   // reflector scalars (identical in every thread of every block)
-  const double alpha = Sin[HH_NB + j];
-  const double nrm2 = Sin[j];
+  const double alpha = sin_[HH_NB + j];
+  const double nrm2 = sin_[j];
   const double sig = nrm2 - alpha * alpha;  // sum of squares strictly below the diagonal
   double beta = alpha, tauv = 0.0, scale = 0.0;
   if (sig > 0.0 && nrm2 > 0.0) {
@@ -119,8 +135,8 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int col = 4 * q + c;
-    const double rd = Sin[HH_NB + col];
-    w[c] = (col > j && col < ncols) ? rd + scale * (Sin[col] - alpha * rd) : 0.0;
+    const double rd = sin_[HH_NB + col];
+    w[c] = (col > j && col < ncols) ? rd + scale * (sin_[col] - alpha * rd) : 0.0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) tau[j] = (T)tauv;
   const int jl = j & 3, jq = j >> 2;              // lane group slot holding column j
@@ -194,23 +210,28 @@ __global__ __launch_bounds__(64) void hh_larft(const double* __restrict__ Y, con
 }
 
 // W[c][j] += sum_i V[i][c] C[i][j] (c < nc <= 32, j < N) over rows [0, m) with FP64 accumulation:
-// the V^T C products of the trailing update / Q accumulation reduce over ALL rows of the matrix
-// (1e6+), where an fp32 GEMM's accumulation error (~sqrt(m) u) would cost orthogonality. Memory /
-// fp64-FMA bound: each C element is read once and feeds 32 fp64 FMAs. Block = 64 columns of C x
-// a row slice (split-K over blockIdx.y); thread (j = t % 64, c-group = t / 64) owns 8 rows of W;
-// V rows are staged through LDS 64 at a time (broadcast reads), partials land by fp64 atomicAdd.
+// the V^T C products of the trailing update / Q accumulation (and V^T V) reduce over ALL rows of
+// the matrix (1e6+), where an fp32 GEMM's accumulation error (~sqrt(m) u) would cost
+// orthogonality - and rocBLAS's fp64 GEMM is slow on these tall-skinny shapes. Block = 256
+// columns of C x a row slice (split-K over blockIdx.y); thread (jl = t % 64, c-group = t / 64)
+// owns W rows 8 cg .. 8 cg + 7 of columns jl + 64 u (u < 4): every V value read from LDS feeds 4
+// fp64 FMAs. V rows are staged through LDS 64 at a time (broadcast reads); partials land by fp64
+// atomicAdd.
 template <typename T>
 __global__ __launch_bounds__(256) void hh_vtc(const T* __restrict__ V, int64_t ldv, const T* __restrict__ C,
                                               int64_t ldc, int64_t m, int64_t N, int nc, int64_t rows_per_split,
                                               double* __restrict__ W, int64_t ldw) {
+  // W here is the partial buffer [splits][nc][ldw]
   __shared__ T vs[64 * HH_NB];
   const int t = threadIdx.x, jl = t & 63, cg = t >> 6;
-  const int64_t j = (int64_t)blockIdx.x * 64 + jl;
+  const int64_t j0 = (int64_t)blockIdx.x * 256 + jl;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
   const int64_t r1 = r0 + rows_per_split < m ? r0 + rows_per_split : m;
-  double acc[8];
+  double acc[8][4];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[c][u] = 0.0;
   for (int64_t rb = r0; rb < r1; rb += 64) {
     const int nr = r1 - rb < 64 ? (int)(r1 - rb) : 64;
     __syncthreads();
@@ -219,19 +240,42 @@ __global__ __launch_bounds__(256) void hh_vtc(const T* __restrict__ V, int64_t l
       vs[e] = (rr < nr && cc < nc) ? V[(rb + rr) * ldv + cc] : T(0);
     }
     __syncthreads();
-    if (j < N) {
-      for (int rr = 0; rr < nr; ++rr) {
-        const double x = (double)C[(rb + rr) * ldc + j];
-        const T* vr = vs + rr * HH_NB + 8 * cg;
+    for (int rr = 0; rr < nr; ++rr) {
+      double x[4];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[c] = fma((double)vr[c], x, acc[c]);
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = j0 + 64 * u;
+        x[u] = j < N ? (double)C[(rb + rr) * ldc + j] : 0.0;
+      }
+      const T* vr = vs + rr * HH_NB + 8 * cg;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const double v = (double)vr[c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[c][u] = fma(v, x[u], acc[c][u]);
       }
     }
   }
-  if (j < N) {
+  // this split's partial block of W (no atomics: a W element would otherwise take one atomic add
+  // per split - millions per call); hh_vtc_sum adds the splits
+  double* P = W + (int64_t)blockIdx.y * nc * ldw;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t j = j0 + 64 * u;
+    if (j >= N) continue;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (8 * cg + c < nc && acc[c] != 0.0) atomicAdd(W + (int64_t)(8 * cg + c) * ldw + j, acc[c]);
+      if (8 * cg + c < nc) P[(int64_t)(8 * cg + c) * ldw + j] = acc[c][u];
+  }
+}
+
+// W[c][j] += sum over splits of P[s][c][j] (coalesced over j)
+__global__ __launch_bounds__(256) void hh_vtc_sum(const double* __restrict__ P, int splits, int64_t plane,
+                                                  double* __restrict__ W, int64_t total) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    double s = 0.0;
+    for (int k = 0; k < splits; ++k) s += P[k * plane + e];
+    W[e] += s;
   }
 }
 
@@ -244,7 +288,7 @@ int hh_grid(int64_t m) {
       ncu = 256;
   }
   const int64_t need = (m + 31) / 32;
-  const int64_t cap = 2LL * ncu;  // the per-column atomics stay few
+  const int64_t cap = 8LL * ncu;  // enough waves in flight; atomics spread over HH_COPIES copies
   return (int)(need < cap ? (need > 0 ? need : 1) : cap);
 }
 
@@ -252,6 +296,8 @@ int hh_grid(int64_t m) {
 
 // ------------------------------------------------------------------------------------------ C ABI
 HA_EXPORT int ha_hh_nb() { return HH_NB; }
+// doubles per S buffer (HH_COPIES replicated accumulators of S[NB] | rowd[NB])
+HA_EXPORT int ha_hh_slen() { return HH_COPIES * HH_SLEN; }
 
 // S (2 NB doubles, zeroed by the caller) += column-0 sums of the panel at column k0 (ncols <= NB
 // columns) over this rank's rows g >= d, and row d's values if this rank owns it.
@@ -295,11 +341,9 @@ HA_EXPORT int ha_hh_larft(const double* Y, const void* tau, int nb, int dtype, v
   return ha_launch_status();
 }
 
-// W (fp64 [nc][ldw], zeroed by the caller) += V[:, :nc]^T C[:, :N] over m rows, fp64 accumulation.
-HA_EXPORT int ha_hh_vtc(const void* V, int64_t ldv, const void* C, int64_t ldc, int dtype, int64_t m, int64_t N,
-                        int nc, double* W, int64_t ldw, void* stream) {
-  if (nc <= 0 || nc > HH_NB || m < 0 || N < 0) return HA_BAD_ARG;
-  if (m == 0 || N == 0) return HA_OK;
+// Number of row splits ha_hh_vtc uses for (m, N) (the caller sizes the partial buffer:
+// splits * nc * N doubles).
+HA_EXPORT int64_t ha_hh_vtc_splits(int64_t m, int64_t N) {
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
@@ -307,19 +351,34 @@ HA_EXPORT int ha_hh_vtc(const void* V, int64_t ldv, const void* C, int64_t ldc, 
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  const int64_t bx = (N + 63) / 64;
-  int64_t splits = (4LL * ncu + bx - 1) / bx;               // ~4 blocks per CU overall
-  const int64_t maxs = (m + 255) / 256;                     // >= 256 rows per split
+  const int64_t bx = (N + 255) / 256;
+  int64_t splits = (4LL * ncu + bx - 1) / bx;  // ~4 blocks per CU overall
+  const int64_t maxs = (m + 255) / 256;        // >= 256 rows per split
   splits = splits < maxs ? splits : maxs;
   splits = splits < 1 ? 1 : splits > 65535 ? 65535 : splits;
   const int64_t rps = ((m + splits - 1) / splits + 63) / 64 * 64;
-  splits = (m + rps - 1) / rps;
+  return (m + rps - 1) / rps;
+}
+
+// W (fp64 [nc][N], contiguous) += V[:, :nc]^T C[:, :N] over m rows, fp64 accumulation.
+// P: scratch of ha_hh_vtc_splits(m, N) * nc * N doubles.
+HA_EXPORT int ha_hh_vtc(const void* V, int64_t ldv, const void* C, int64_t ldc, int dtype, int64_t m, int64_t N,
+                        int nc, double* W, double* P, void* stream) {
+  if (nc <= 0 || nc > HH_NB || m < 0 || N < 0 || !P) return HA_BAD_ARG;
+  if (m == 0 || N == 0) return HA_OK;
+  const int64_t bx = (N + 255) / 256;
+  const int64_t splits = ha_hh_vtc_splits(m, N);
+  const int64_t rps = ((m + splits - 1) / splits + 63) / 64 * 64;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 0)
     hipLaunchKernelGGL(hh_vtc<float>, dim3((unsigned)bx, (unsigned)splits), dim3(256), 0, s, (const float*)V, ldv,
-                       (const float*)C, ldc, m, N, nc, rps, W, ldw);
+                       (const float*)C, ldc, m, N, nc, rps, P, N);
   else
     hipLaunchKernelGGL(hh_vtc<double>, dim3((unsigned)bx, (unsigned)splits), dim3(256), 0, s, (const double*)V, ldv,
-                       (const double*)C, ldc, m, N, nc, rps, W, ldw);
+                       (const double*)C, ldc, m, N, nc, rps, P, N);
+  const int64_t total = (int64_t)nc * N;
+  const int64_t g = (total + 255) / 256;
+  hipLaunchKernelGGL(hh_vtc_sum, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, P, (int)splits, total, W,
+                     total);
   return ha_launch_status();
 }

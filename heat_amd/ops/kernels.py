@@ -961,6 +961,7 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
     native = local.is_cuda and use_native(local)
     L = lib() if native else None
     nb = L.ha_hh_nb() if native else 32
+    slen = L.ha_hh_slen() if native else 2 * nb  # replicated accumulators (the host path: one)
     dev = local.device
     dt = local.dtype
     code = 0 if dt == torch.float32 else 1
@@ -973,7 +974,7 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
     panels = []
     for k0 in range(0, kmax, nb):
         nc = min(nb, kmax - k0)
-        S = torch.zeros((nc + 1, 2 * nb), dtype=torch.float64, device=dev)
+        S = torch.zeros((nc + 1, slen), dtype=torch.float64, device=dev)
         tau = torch.empty(nc, dtype=dt, device=dev)
         if native:
             check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), st), "ha_hh_colsums")
@@ -990,7 +991,7 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
             if not last:
                 red(S[j + 1])
         V = _hh_v(A, rows, k0, nc)
-        Y = V.double().T @ V.double()
+        Y = _vtc(V, V, native, st)   # V^T V, fp64 accumulation (a tall-skinny fp64 BLAS GEMM is slow)
         red(Y)
         Tm = torch.empty((nc, nc), dtype=dt, device=dev)
         if native:
@@ -1034,8 +1035,10 @@ def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:
     W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)
     if C.stride(1) != 1:
         C = C.contiguous()
-    check(lib().ha_hh_vtc(_ptr(V), V.stride(0), _ptr(C), C.stride(0), 0 if V.dtype == torch.float32 else 1,
-                          V.shape[0], N, nc, _ptr(W), W.stride(0), st), "ha_hh_vtc")
+    L = lib()
+    P = torch.empty(max(1, L.ha_hh_vtc_splits(V.shape[0], N) * nc * N), dtype=torch.float64, device=V.device)
+    check(L.ha_hh_vtc(_ptr(V), V.stride(0), _ptr(C), C.stride(0), 0 if V.dtype == torch.float32 else 1,
+                      V.shape[0], N, nc, _ptr(W), _ptr(P), st), "ha_hh_vtc")
     return W
 
 
