@@ -20,7 +20,9 @@ The implementation is MI355X-first rather than an MPI emulation:
 * Scans are an all-gather of one slice per rank plus a local prefix.
 * Strided sub-tensors are packed contiguously on the device (``narrow().contiguous()``) instead of
   MPI derived datatypes.
-* Host staging of device buffers never happens: ``CUDA_AWARE_MPI`` is always True.
+* Device buffers go straight to RCCL. Only a pure gloo group (``HEAT_COMM_BACKEND=gloo``: CPU
+  tests, or several ranks sharing one GPU) stages them through host memory
+  (``parallel/staging.py``, the reference's non-CUDA-aware path); ``CUDA_AWARE_MPI`` says which.
 """
 from __future__ import annotations
 
@@ -33,9 +35,10 @@ import torch
 import torch.distributed as dist
 
 from ..parallel import backend as _backend
+from ..parallel import staging as _SD
 
-# device buffers are always handed straight to RCCL; the flag only keeps the public name
-CUDA_AWARE_MPI = True
+# device buffers are handed straight to RCCL unless the world group is gloo-only (host staging)
+CUDA_AWARE_MPI = os.environ.get("HEAT_COMM_BACKEND", "").lower() != "gloo"
 
 
 # ----------------------------------------------------------------------------------------------
@@ -316,7 +319,7 @@ class MPICommunication(Communication):
             return MPIRequest()
         wire = _wire_dtype(t)
         contig = wire if wire.is_contiguous() and wire is t else wire.contiguous()
-        work = dist.broadcast(contig, src=self._g(root), group=self.group, async_op=True)
+        work = _SD.broadcast(contig, src=self._g(root), group=self.group, async_op=True)
 
         def fin():
             if contig is not t:
@@ -332,7 +335,7 @@ class MPICommunication(Communication):
         """All-gather ``src`` from every rank into a [p, *src.shape] tensor (async)."""
         flat = src.reshape(-1)
         out = torch.empty(self.size * flat.numel(), dtype=src.dtype, device=src.device)
-        work = dist.all_gather_into_tensor(out, flat, group=self.group, async_op=True)
+        work = _SD.all_gather_into_tensor(out, flat, group=self.group, async_op=True)
         return out.view((self.size,) + tuple(src.shape)), work
 
     def _fold_gathered(self, stacked: torch.Tensor, op: Op, upto: Optional[int] = None) -> torch.Tensor:
@@ -365,7 +368,7 @@ class MPICommunication(Communication):
         native = op.torch_op is not None and t.dtype != torch.bool and (not t.is_complex() or op is MPI.SUM)
         if native:
             contig = t if t.is_contiguous() else t.contiguous()
-            work = dist.all_reduce(contig, op=op.torch_op, group=self.group, async_op=True)
+            work = _SD.all_reduce(contig, op=op.torch_op, group=self.group, async_op=True)
 
             def fin():
                 if contig is not t:
@@ -375,7 +378,7 @@ class MPICommunication(Communication):
         if op in (MPI.LAND, MPI.LOR) and op.torch_op is None:
             contig = t.to(torch.uint8).contiguous() if t.dtype == torch.bool else (t != 0).to(torch.uint8)
             rop = dist.ReduceOp.MIN if op is MPI.LAND else dist.ReduceOp.MAX
-            work = dist.all_reduce(contig, op=rop, group=self.group, async_op=True)
+            work = _SD.all_reduce(contig, op=rop, group=self.group, async_op=True)
 
             def fin():
                 t.copy_(contig.to(t.dtype))
@@ -464,7 +467,7 @@ class MPICommunication(Communication):
             return [int(n)]
         t = torch.tensor([int(n)], dtype=torch.int64, device=self._small_device())
         out = torch.empty(self.size, dtype=torch.int64, device=t.device)
-        dist.all_gather_into_tensor(out, t, group=self.group)
+        _SD.all_gather_into_tensor(out, t, group=self.group)
         return [int(x) for x in out.tolist()]
 
     def _small_device(self):
@@ -488,7 +491,7 @@ class MPICommunication(Communication):
             padded = torch.zeros((mx,) + rest, dtype=moved.dtype, device=moved.device)
             padded[: moved.shape[0]] = moved
         out = torch.empty((self.size * mx,) + rest, dtype=moved.dtype, device=moved.device)
-        work = dist.all_gather_into_tensor(out, padded, group=self.group, async_op=True)
+        work = _SD.all_gather_into_tensor(out, padded, group=self.group, async_op=True)
 
         def fin():
             if all(c == mx for c in counts):
@@ -667,10 +670,10 @@ class MPICommunication(Communication):
         flat_out = torch.empty(sum(out_sizes), dtype=wire, device=device)
         if flat_in.is_complex():
             fi, fo = torch.view_as_real(flat_in).reshape(-1), torch.view_as_real(flat_out).reshape(-1)
-            work = dist.all_to_all_single(fo, fi, [2 * s for s in out_sizes], [2 * s for s in in_sizes],
+            work = _SD.all_to_all_single(fo, fi, [2 * s for s in out_sizes], [2 * s for s in in_sizes],
                                           group=self.group, async_op=True)
         else:
-            work = dist.all_to_all_single(flat_out, flat_in, out_sizes, in_sizes, group=self.group, async_op=True)
+            work = _SD.all_to_all_single(flat_out, flat_in, out_sizes, in_sizes, group=self.group, async_op=True)
 
         def fin():
             res, off = [], 0
@@ -728,7 +731,7 @@ class MPICommunication(Communication):
         if not isinstance(t, torch.Tensor):
             return self.isend(buf, dest, tag)
         src = _wire_dtype(t).contiguous()
-        work = dist.isend(src, dst=self._g(dest), group=self.group, tag=self._tag(tag))
+        work = _SD.isend(src, dst=self._g(dest), group=self.group, tag=self._tag(tag))
         return MPIRequest(work, result=src)
 
     def Send(self, buf, dest: int, tag: int = 0):
@@ -744,7 +747,7 @@ class MPICommunication(Communication):
         dst = t if (t.is_contiguous() and t.dtype != torch.bool) else torch.empty_like(_wire_dtype(t)).contiguous()
         if source == MPI.ANY_SOURCE:
             raise NotImplementedError("ANY_SOURCE receives are not supported over RCCL; name the peer")
-        work = dist.irecv(dst, src=self._g(source), group=self.group, tag=self._tag(tag))
+        work = _SD.irecv(dst, src=self._g(source), group=self.group, tag=self._tag(tag))
 
         def fin():
             if dst is not t:
@@ -771,7 +774,7 @@ class MPICommunication(Communication):
             out = torch.empty(tuple(recv_shape), dtype=wire, device=device)
             ops.append(dist.P2POp(dist.irecv, out, self._g(source), self.group))
         if ops:
-            for w in dist.batch_isend_irecv(ops):
+            for w in _SD.batch_isend_irecv(ops):
                 w.wait()
         if out is not None and dtype == torch.bool:
             out = out.to(torch.bool)
@@ -837,8 +840,8 @@ class MPICommunication(Communication):
 
     def isend(self, obj: Any, dest: int, tag: int = 0) -> MPIRequest:
         size, payload = self._obj_to_tensor(obj)
-        w1 = dist.isend(size, dst=self._g(dest), group=self.group, tag=self._tag(tag))
-        w2 = dist.isend(payload, dst=self._g(dest), group=self.group, tag=self._tag(tag))
+        w1 = _SD.isend(size, dst=self._g(dest), group=self.group, tag=self._tag(tag))
+        w2 = _SD.isend(payload, dst=self._g(dest), group=self.group, tag=self._tag(tag))
         return MPIRequest([w1, w2], result=(size, payload))
 
     def send(self, obj: Any, dest: int, tag: int = 0):
@@ -847,9 +850,9 @@ class MPICommunication(Communication):
     def recv(self, buf=None, source: int = 0, tag: int = 0, status=None) -> Any:
         dev = self._obj_device()
         size = torch.empty(1, dtype=torch.int64, device=dev)
-        dist.recv(size, src=self._g(source), group=self.group, tag=self._tag(tag))
+        _SD.recv(size, src=self._g(source), group=self.group, tag=self._tag(tag))
         payload = torch.empty(int(size.item()), dtype=torch.uint8, device=dev)
-        dist.recv(payload, src=self._g(source), group=self.group, tag=self._tag(tag))
+        _SD.recv(payload, src=self._g(source), group=self.group, tag=self._tag(tag))
         return pickle.loads(payload.cpu().numpy().tobytes())
 
     def irecv(self, buf=None, source: int = 0, tag: int = 0) -> MPIRequest:

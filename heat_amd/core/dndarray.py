@@ -306,6 +306,8 @@ class DNDarray:
         shape[s] = halo_size
         import torch.distributed as dist
 
+        from ..parallel import staging as _SD
+
         ops, recv_prev, recv_next = [], None, None
         comm = self.comm
         wire = torch.uint8 if a.dtype == torch.bool else a.dtype
@@ -317,7 +319,7 @@ class DNDarray:
             ops.append(dist.P2POp(dist.isend, last.to(wire).contiguous(), comm._g(next_r), comm.group))
             recv_next = torch.empty(shape, dtype=wire, device=a.device)
             ops.append(dist.P2POp(dist.irecv, recv_next, comm._g(next_r), comm.group))
-        for w in dist.batch_isend_irecv(ops) if ops else []:
+        for w in _SD.batch_isend_irecv(ops) if ops else []:
             w.wait()
         self.__halo_prev = None if recv_prev is None else recv_prev.to(a.dtype)
         self.__halo_next = None if recv_next is None else recv_next.to(a.dtype)

@@ -22,6 +22,8 @@ import numpy as np
 import os
 
 import torch
+
+from ...parallel import staging as _SD
 import torch.distributed as dist
 
 from .. import _operations, factories, types
@@ -85,7 +87,7 @@ def _reduce_scatter(partial: torch.Tensor, comm, axis: int) -> torch.Tensor:
     wire_in, wire_out = inp, out
     if inp.dtype == torch.bool:
         wire_in, wire_out = inp.to(torch.uint8), out.to(torch.uint8)
-    dist.reduce_scatter_tensor(wire_out, wire_in, op=dist.ReduceOp.SUM, group=comm.group)
+    _SD.reduce_scatter_tensor(wire_out, wire_in, op=dist.ReduceOp.SUM, group=comm.group)
     res = wire_out[: counts[comm.rank]]
     return res.movedim(0, axis).contiguous()
 

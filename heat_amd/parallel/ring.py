@@ -13,6 +13,8 @@ from typing import Callable, List
 import torch
 import torch.distributed as dist
 
+from . import staging as _SD
+
 
 def ring_pass(block: torch.Tensor, fn: Callable[[torch.Tensor, int], None], comm, sizes: List[int] = None):
     """Visit every rank's ``block`` in ring order (own first), overlapping transfer and compute.
@@ -36,7 +38,7 @@ def ring_pass(block: torch.Tensor, fn: Callable[[torch.Tensor, int], None], comm
             recv = torch.empty((sizes[incoming],) + rest, dtype=cur.dtype, device=cur.device)
             ops = [dist.P2POp(dist.isend, cur, comm._g(nxt), comm.group),
                    dist.P2POp(dist.irecv, recv, comm._g(prv), comm.group)]
-            works = dist.batch_isend_irecv(ops)
+            works = _SD.batch_isend_irecv(ops)
         fn(cur, src)
         for w in works:
             w.wait()

@@ -11,6 +11,8 @@ from __future__ import annotations
 from typing import Callable, Iterator, List, Optional, Union
 
 import torch
+
+from ...parallel import staging as _SD
 import torch.distributed as dist
 from torch.utils import data as torch_data
 
@@ -144,7 +146,7 @@ def dataset_ishuffle(dataset, attrs: List[list]):
         rcv = torch.empty_like(snd)
         ops = [dist.P2POp(dist.isend, snd, comm._g(dest), comm.group),
                dist.P2POp(dist.irecv, rcv, comm._g(src), comm.group)]
-        works = dist.batch_isend_irecv(ops)
+        works = _SD.batch_isend_irecv(ops)
         pending.append((data_attr, ht_attr, works, snd, rcv))
     dataset._ishuffle_pending = pending
     return dataset

@@ -55,7 +55,8 @@ def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None
     return outs
 
 
-def run_distributed_batch(module: str, names, nprocs: int, timeout: int = 1200):
+def run_distributed_batch(module: str, names, nprocs: int, timeout: int = 1200, env_extra=None,
+                          keep_gpu: bool = False):
     """Run the check functions ``names`` of ``module`` in one job of ``nprocs`` ranks; returns
     {name: (ok, error)} (checks missing from the report - a job that died - count as failed)."""
     import json
@@ -69,8 +70,12 @@ def run_distributed_batch(module: str, names, nprocs: int, timeout: int = 1200):
         env = dict(os.environ)
         env.update({"RANK": str(r), "WORLD_SIZE": str(nprocs), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(nprocs),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HEAT_COMM_BACKEND": "gloo",
-                    "HEAT_COMM_TIMEOUT": "120", "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "",
-                    "OMP_NUM_THREADS": "1", "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+                    "HEAT_COMM_TIMEOUT": "120", "OMP_NUM_THREADS": "1",
+                    "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        if not keep_gpu:
+            env.update({"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+        if env_extra:
+            env.update(env_extra)
         procs.append(subprocess.Popen([sys.executable, "-m", "tests._dist_batch_runner", out_path, module] + list(names),
                                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []

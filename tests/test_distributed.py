@@ -14,11 +14,12 @@ CASES = [(m, n) for m, mod in MODULES.items() for n in dir(mod) if n.startswith(
 _BATCH = {}
 
 
-def _batch(module, nprocs):
-    key = (module, nprocs)
+def _batch(module, nprocs, staged=False):
+    key = (module, nprocs, staged)
     if key not in _BATCH:
         names = [n for m, n in CASES if m == module]
-        _BATCH[key] = run_distributed_batch(module, names, nprocs)
+        env = {"HEAT_COMM_FORCE_STAGING": "1"} if staged else None
+        _BATCH[key] = run_distributed_batch(module, names, nprocs, env_extra=env)
     return _BATCH[key]
 
 
@@ -28,4 +29,14 @@ def test_distributed(module, name, nprocs):
     ok, err = _batch(module, nprocs)[name]
     if not ok:
         run_distributed(module + ":" + name, nprocs)  # raises with the full per-rank log
+        pytest.fail("check {} failed in the batched job but passed alone:\n{}".format(name, err))
+
+
+@pytest.mark.parametrize("module,name", CASES)
+def test_distributed_host_staged(module, name):
+    """Every collective through the host-staging wrappers (``parallel/staging.py``: copy out,
+    gloo, copy back on ``wait()``), the path device buffers take on a gloo-only group."""
+    ok, err = _batch(module, 3, staged=True)[name]
+    if not ok:
+        run_distributed(module + ":" + name, 3, env_extra={"HEAT_COMM_FORCE_STAGING": "1"})
         pytest.fail("check {} failed in the batched job but passed alone:\n{}".format(name, err))

@@ -1,0 +1,35 @@
+"""The multi-process checks with DEVICE buffers: 2 ranks share the one GPU of the test box
+(RCCL refuses two ranks on one device, so the world group is gloo and every collective goes
+through the host-staging wrappers of ``parallel/staging.py``). Every split-aware path the CPU
+suite covers - Allreduce/Allgatherv/exchange/Bcast, ring passes, halos, native arg-reduce and
+top-k, distributed Householder QR, k-means, cdist, moments - runs here on ``cuda:0`` tensors and
+the native kernels, with the same NumPy oracles as ``test_distributed.py``."""
+import pytest
+import torch
+
+from . import dist_checks, dist_checks_edge
+from ._dist import run_distributed, run_distributed_batch
+
+pytestmark = pytest.mark.gpu
+
+MODULES = {"tests.dist_checks": dist_checks, "tests.dist_checks_edge": dist_checks_edge}
+CASES = [(m, n) for m, mod in MODULES.items() for n in dir(mod) if n.startswith("check_")
+         and getattr(getattr(mod, n), "__module__", m) == m]
+ENV = {"HEAT_AMD_DEFAULT_DEVICE": "gpu", "HEAT_COMM_TIMEOUT": "60"}
+_BATCH = {}
+
+
+def _batch(module):
+    if module not in _BATCH:
+        names = [n for m, n in CASES if m == module]
+        _BATCH[module] = run_distributed_batch(module, names, 2, timeout=300, env_extra=ENV, keep_gpu=True)
+    return _BATCH[module]
+
+
+@pytest.mark.parametrize("module,name", CASES)
+def test_distributed_on_device(module, name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ok, err = _batch(module)[name]
+    if not ok:
+        pytest.fail("check {} failed with device buffers:\n{}".format(name, err))
