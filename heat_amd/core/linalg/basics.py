@@ -24,6 +24,7 @@ import os
 import torch
 
 from ...parallel import staging as _SD
+from ...parallel.ring import ring_pass
 import torch.distributed as dist
 
 from .. import _operations, factories, types
@@ -155,8 +156,24 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# Distributed operand size (bytes, whole array) from which matmul streams its panels around the
+# ring (memory O(local + 2 panels), every transfer overlapped with the previous panel's GEMM)
+# instead of all-gathering the whole operand in one collective (lower latency for small operands).
+_RING_MIN_BYTES = int(os.environ.get("HEAT_MATMUL_RING_BYTES", str(256 << 20)))
+
+
+def _stream_panels(x: DNDarray, comm) -> bool:
+    return comm.size > 1 and x.gnumel * x.larray.element_size() >= _RING_MIN_BYTES
+
+
 def matmul(a: DNDarray, b: DNDarray, allow_resplit: bool = False) -> DNDarray:
-    """Matrix product ``a @ b`` of 1-D/2-D DNDarrays with the reference's split rules."""
+    """Matrix product ``a @ b`` of 1-D/2-D DNDarrays with the reference's split rules.
+
+    Reference ``linalg/basics.py:483-750`` pipelines block broadcasts with one-step lookahead;
+    here the operand that must travel is passed around the ring in its natural row/column panels
+    (``parallel.ring.ring_pass``: the next panel is in flight while the current one's GEMM runs),
+    or, below ``_RING_MIN_BYTES``, all-gathered once. A contraction-split product is local GEMMs
+    plus one reduce-scatter."""
     if not isinstance(a, DNDarray) or not isinstance(b, DNDarray):
         raise TypeError("matmul requires two DNDarrays")
     if a.gshape[-1] != b.gshape[0]:
@@ -181,9 +198,10 @@ def matmul(a: DNDarray, b: DNDarray, allow_resplit: bool = False) -> DNDarray:
         return DNDarray(t, tuple(gshape), og_type, split, dev, comm, balanced)
 
     A, B = a.larray.to(tt), b.larray.to(tt)
-    dist_a, dist_b = a.is_distributed(), b.is_distributed()
-    sa = a.split if dist_a else None
-    sb = b.split if dist_b else None
+    # a world of one follows the same split rules (the result keeps the split the reference gives)
+    solo = comm.size == 1
+    sa = a.split if (a.is_distributed() or solo) else None
+    sb = b.split if (b.is_distributed() or solo) else None
 
     # vector cases ------------------------------------------------------------------------
     if a.ndim == 1 and b.ndim == 1:
@@ -230,12 +248,44 @@ def matmul(a: DNDarray, b: DNDarray, allow_resplit: bool = False) -> DNDarray:
     if sa is None and sb == 1:
         return squeeze_out(_mm(A, B), 1, balanced=b.balanced)
     if sa == 0 and sb == 1:
+        counts, displs = b.counts_displs()
+        if _stream_panels(b, comm):
+            # C[:, cols of q] = A_local @ B_q for every rank's column panel, streamed around the ring
+            C = torch.empty((A.shape[0], Q), dtype=tt, device=A.device)
+
+            def panel(blk, q):
+                C[:, displs[q]: displs[q] + counts[q]] = _mm(A, blk.t())
+
+            ring_pass(B.t().contiguous(), panel, comm, list(counts))
+            return squeeze_out(C, 0, balanced=a.balanced)
         Bf = comm.allgather_tensor(B.contiguous(), 1, b.split_counts())
         return squeeze_out(_mm(A, Bf), 0, balanced=a.balanced)
     if sa == 0 and sb == 0:
+        counts, displs = b.counts_displs()
+        if _stream_panels(b, comm):
+            # C = sum_q A_local[:, rows of q] @ B_q, B's row panels streamed around the ring
+            C = torch.zeros((A.shape[0], B.shape[1]), dtype=tt, device=A.device)
+
+            def panel(blk, q):
+                if counts[q]:
+                    C.add_(_mm(A[:, displs[q]: displs[q] + counts[q]], blk))
+
+            ring_pass(B.contiguous(), panel, comm, list(counts))
+            return squeeze_out(C, 0, balanced=a.balanced)
         Bf = comm.allgather_tensor(B.contiguous(), 0, b.split_counts())
         return squeeze_out(_mm(A, Bf), 0, balanced=a.balanced)
     if sa == 1 and sb == 1:
+        if not vec_a and _stream_panels(a, comm):
+            counts, displs = a.counts_displs()
+            # C_local = sum_q A_q @ B_local[rows of q], A's column panels streamed around the ring
+            C = torch.zeros((L, B.shape[1]), dtype=tt, device=B.device)
+
+            def panel(blk, q):
+                if counts[q]:
+                    C.add_(_mm(blk.t(), B[displs[q]: displs[q] + counts[q]]))
+
+            ring_pass(A.t().contiguous(), panel, comm, list(counts))
+            return squeeze_out(C, 1, balanced=b.balanced)
         Af = comm.allgather_tensor(A.contiguous(), 1, a.split_counts() if not vec_a else None)
         return squeeze_out(_mm(Af, B), 1, balanced=b.balanced)
     # contraction axis distributed: partial products + reduce-scatter

@@ -11,7 +11,8 @@ GEMMs with one all-reduce of V^T C per panel) - backward stable for any conditio
 split-0 input uses TSQR - one local QR per rank, ONE all-gather of the p small R factors, a
 redundant QR of the stacked R on every rank (no tree latency: p <= 8 per node) and one local
 GEMM ``Q_r @ Q2_r`` to form Q. The reference's binary merge tree with per-tile sends and string tags
-(``qr.py:477-846``) disappears.
+(``qr.py:477-846``) disappears. Column-split input stays column-split (``_qr_split1``: Householder
+panel factorisation by the owner, reflector broadcast, H_j^T applied by the later ranks).
 
 Q mode: the reference returns a complete m x m Q. That is kept for matrices whose complete Q
 fits comfortably in memory (``mode=None`` -> "complete" when m*m elements <= 2**28); beyond that
@@ -74,9 +75,19 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
             q, r = _local_qr(t, calc_q)
         else:
             q, r = torch.linalg.qr(t, mode=mode)
-        R = DNDarray(r, tuple(r.shape), dtype, None if a.split is None else a.split, a.device, a.comm, True)
-        Q = DNDarray(q, tuple(q.shape), dtype, None if a.split is None else 0, a.device, a.comm, True) if calc_q else None
+        # the same normalisation as every distributed path: diag(R) >= 0
+        k = min(r.shape)
+        d = torch.sign(torch.diagonal(r[:k, :k]))
+        d = torch.where(d == 0, torch.ones_like(d), d)
+        r = torch.cat([d.unsqueeze(1) * r[:k], r[k:]], 0)
+        if q is not None:
+            q = torch.cat([q[:, :k] * d.unsqueeze(0), q[:, k:]], 1)
+        R = DNDarray(r, tuple(r.shape), dtype, a.split, a.device, a.comm, True)
+        Q = DNDarray(q, tuple(q.shape), dtype, a.split, a.device, a.comm, True) if calc_q else None
         return QR(Q, R)
+
+    if a.split == 1 and m >= n and (mode == "reduced" or m == n):
+        return _qr_split1(a, dtype, calc_q)
 
     if mode == "complete" and (m < n * a.comm.size or m <= n):
         # small or wide matrices: the factors are not smaller than the input; factor replicated
@@ -113,6 +124,100 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
     if a.split == 1:
         Q = _resplit(Q, 1)
     return QR(Q, R)
+
+
+def _qr_split1(a: DNDarray, dtype, calc_q: bool):
+    """Column-split QR without redistributing rows (reference ``qr.py:849-1018``, panel
+    broadcast): rank j, in column order, factors rows [c_j, m) of its (already updated) column
+    panel with the blocked Householder kernels (``ops.householder_factor``) and broadcasts the
+    reflectors + compact-WY T blocks; every later rank applies H_j^T to its own panel. Q is then
+    accumulated backwards (Q_k = H_0 ... H_k E_k) with a second broadcast of each rank's
+    reflectors. Backward stable for any conditioning; Q and R come out split along axis 1 with the
+    input's column partition; memory O(local + 1 panel)."""
+    from ... import ops
+
+    comm = a.comm
+    tt = dtype.torch_type()
+    m, n = a.gshape
+    counts, displs = a.counts_displs()
+    me, p = comm.rank, comm.size
+    dev = a.larray.device
+    A = a.larray.to(tt).contiguous().clone()
+    nb = ops.householder_block(A)
+    mine = None      # (reflectors, panels) of this rank's column panel
+    signs = {}       # sign(diag R_jj) of every panel j <= me
+
+    def panel_shapes(j):
+        rows, nj = m - displs[j], counts[j]
+        return (rows, nj), [(k0, min(nb, nj - k0)) for k0 in range(0, nj, nb)]
+
+    def send(j, fact):
+        """Broadcast panel j's reflectors and T blocks from rank j; returns them on every rank."""
+        shape, blocks = panel_shapes(j)
+        if j == me:
+            V, panels = fact
+            T = torch.zeros((len(blocks), nb, nb), dtype=tt, device=dev)
+            for i, (_, nc, Tm) in enumerate(panels):
+                T[i, :nc, :nc] = Tm
+        else:
+            V = torch.empty(shape, dtype=tt, device=dev)
+            T = torch.empty((len(blocks), nb, nb), dtype=tt, device=dev)
+        comm.Bcast(V, root=j)
+        comm.Bcast(T, root=j)
+        return V, [(k0, nc, T[i, :nc, :nc]) for i, (k0, nc) in enumerate(blocks)]
+
+    def diag_signs(V, nj):
+        d = torch.sign(torch.diagonal(V[:nj, :nj]))
+        return torch.where(d == 0, torch.ones_like(d), d)
+
+    last = max((j for j in range(p) if counts[j]), default=-1)
+    for j in range(p):
+        nj = counts[j]
+        if nj == 0:
+            continue
+        fact = None
+        if j == me:
+            fact = ops.householder_factor(A[displs[j]:], 0, m - displs[j])
+            mine = fact
+            A[displs[j]:] = fact[0]
+        if j == last:
+            if j == me:
+                signs[j] = diag_signs(fact[0], nj)
+            break
+        V, panels = send(j, fact)
+        signs[j] = diag_signs(V, nj)
+        if me > j and counts[me]:
+            ops.householder_apply(V, panels, A[displs[j]:], 0, transpose=True)
+
+    # R: rows of panel j (< me) were produced by H_j^T, this rank's diagonal block is triu(V)
+    nloc = counts[me]
+    R = A.new_zeros((n, nloc))
+    if nloc:
+        top = displs[me]
+        R[:top] = A[:top]
+        R[top: top + nloc] = torch.triu(A[top: top + nloc])
+        for j, d in signs.items():
+            R[displs[j]: displs[j] + counts[j]] *= d.unsqueeze(1)
+    Rd = DNDarray(R, (n, n), dtype, 1, a.device, comm, a.balanced)
+    if not calc_q:
+        return QR(None, Rd)
+    # Q_k = H_0 H_1 ... H_k [0; I; 0]: own reflectors first, then every earlier panel's, in
+    # descending order (panel j's reflectors are broadcast a second time)
+    Q = A.new_zeros((m, nloc))
+    if nloc:
+        Q[displs[me]: displs[me] + nloc] = torch.eye(nloc, dtype=tt, device=dev)
+    for j in range(last, -1, -1):
+        if counts[j] == 0:
+            continue
+        if j == me:
+            ops.householder_apply(mine[0], mine[1], Q[displs[j]:], 0, transpose=False, identity_start=True)
+        if any(counts[k] for k in range(j + 1, p)):
+            V, panels = send(j, mine if j == me else None)
+            if me > j and nloc:
+                ops.householder_apply(V, panels, Q[displs[j]:], 0, transpose=False)
+    if nloc:
+        Q *= signs[me].unsqueeze(0)
+    return QR(DNDarray(Q, (m, n), dtype, 1, a.device, comm, a.balanced), Rd)
 
 
 def _resplit(x: DNDarray, axis):

@@ -163,7 +163,8 @@ class DataParallelMultiGPU(tnn.Module):
             raise TypeError("optimizer must be a DASO optimizer")
         self.comm = comm
         if optimizer.loc_gpus > 1 and optimizer.local_comm is not None and optimizer.local_comm.group is not None:
-            dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+            p0 = next(module.parameters(), None)
+            dev = p0.device.index if p0 is not None and p0.is_cuda else None
             module = tnn.parallel.DistributedDataParallel(module, device_ids=[dev] if dev is not None else None,
                                                           process_group=optimizer.local_comm.group)
         self.module = module

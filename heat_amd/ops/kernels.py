@@ -16,7 +16,8 @@ from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
-           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr"]
+           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr",
+           "householder_factor", "householder_apply", "householder_block"]
 
 _NUM_CUS = {}
 
@@ -958,6 +959,35 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
 
     Returns (this rank's rows of the reduced Q or None, R [min(m, n), n] replicated), with
     diag(R) >= 0."""
+    A, panels = householder_factor(local, g0, m_total, allreduce)
+    dev, dt = A.device, A.dtype
+    m_r, n = A.shape
+    kmax = min(m_total, n)
+    red = allreduce or (lambda t: t)
+    # R: the upper triangle of global rows [0, kmax), gathered from their owners by the all-reduce
+    R = torch.zeros((kmax, n), dtype=dt, device=dev)
+    lo, hi = max(g0, 0), min(g0 + m_r, kmax)
+    if hi > lo:
+        R[lo:hi] = torch.triu(A[lo - g0: hi - g0], diagonal=lo)
+    red(R)
+    d = torch.sign(torch.diagonal(R))
+    d = torch.where(d == 0, torch.ones_like(d), d)
+    R = d.unsqueeze(1) * R
+    if not calc_q:
+        return None, R
+    Q = torch.zeros((m_r, kmax), dtype=dt, device=dev)
+    if hi > lo:
+        Q[lo - g0: hi - g0, lo:hi] = torch.eye(hi - lo, dtype=dt, device=dev)
+    householder_apply(A, panels, Q, g0, transpose=False, allreduce=allreduce, identity_start=True)
+    return Q * d.unsqueeze(0), R
+
+
+def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] = None, allreduce=None):
+    """The factorisation half of :func:`householder_qr`: returns (A, panels) - A holds R in its
+    upper triangle and the reflectors below it (LAPACK geqrf layout, rows [g0, g0 + m_r) of the
+    global matrix), ``panels`` the compact-WY blocks as [(k0, nc, T)]."""
+    m_r, n = local.shape
+    m_total = m_r if m_total is None else m_total
     native = local.is_cuda and use_native(local)
     L = lib() if native else None
     nb = L.ha_hh_nb() if native else 32
@@ -965,7 +995,6 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
     dev = local.device
     dt = local.dtype
     code = 0 if dt == torch.float32 else 1
-    m_r, n = local.shape
     kmax = min(m_total, n)
     A = local.contiguous().clone()
     st = ctypes.c_void_p(stream_ptr(dev)) if native else None
@@ -1004,27 +1033,33 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
             W = _vtc(V, C, native, st)   # fp64 reduction over all rows
             red(W)
             C.addmm_(V, (Tm.double().T @ W).to(dt), alpha=-1.0)
-    # R: the upper triangle of global rows [0, kmax), gathered from their owners by the all-reduce
-    R = torch.zeros((kmax, n), dtype=dt, device=dev)
-    lo, hi = max(g0, 0), min(g0 + m_r, kmax)
-    if hi > lo:
-        R[lo:hi] = torch.triu(A[lo - g0: hi - g0], diagonal=lo)
-    red(R)
-    d = torch.sign(torch.diagonal(R))
-    d = torch.where(d == 0, torch.ones_like(d), d)
-    R = d.unsqueeze(1) * R
-    if not calc_q:
-        return None, R
-    Q = torch.zeros((m_r, kmax), dtype=dt, device=dev)
-    if hi > lo:
-        Q[lo - g0: hi - g0, lo:hi] = torch.eye(hi - lo, dtype=dt, device=dev)
-    for k0, nc, Tm in reversed(panels):
+    return A, panels
+
+
+def householder_block(t: Optional[torch.Tensor] = None) -> int:
+    """Panel width of the blocked Householder factorisation of ``t``'s device/dtype."""
+    return lib().ha_hh_nb() if t is not None and t.is_cuda and use_native(t) else 32
+
+
+def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, transpose: bool = True,
+                      allreduce=None, identity_start: bool = False) -> torch.Tensor:
+    """Apply the orthogonal factor of a :func:`householder_factor` result to C in place (rows of
+    C aligned with the rows of A): Q^T C (``transpose``) or Q C, block by block as
+    C -= V (T^T|T (V^T C)) with the V^T C products accumulated in fp64."""
+    native = A.is_cuda and use_native(A)
+    st = ctypes.c_void_p(stream_ptr(A.device)) if native else None
+    red = allreduce or (lambda t: t)
+    rows = torch.arange(g0, g0 + A.shape[0], device=A.device).unsqueeze(1)
+    for k0, nc, Tm in (panels if transpose else list(reversed(panels))):
         V = _hh_v(A, rows, k0, nc)
-        Qc = Q[:, k0:]
-        W = _vtc(V, Qc, native, st)
+        # C = [I; 0] accumulation: columns before k0 are still unit vectors that V (zero above
+        # global row k0) does not touch
+        Cc = C[:, k0:] if identity_start else C
+        W = _vtc(V, Cc, native, st)
         red(W)
-        Qc.addmm_(V, (Tm.double() @ W).to(dt), alpha=-1.0)
-    return Q * d.unsqueeze(0), R
+        Tt = Tm.double().T if transpose else Tm.double()
+        Cc.addmm_(V, (Tt @ W).to(C.dtype), alpha=-1.0)
+    return C
 
 
 def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:

@@ -380,3 +380,52 @@ def check_netcdf_modes_unlimited_slices():
             raise AssertionError("must raise")
         except ValueError:
             pass
+
+
+def check_matmul_ring_streamed():
+    """Panel-streamed matmul (``linalg/basics.py`` ring path, threshold forced to 0) for every
+    split pair, including ranks that hold empty panels (p > the split extent)."""
+    from heat_amd.core.linalg import basics
+
+    old = basics._RING_MIN_BYTES
+    basics._RING_MIN_BYTES = 0
+    try:
+        rng = np.random.default_rng(61)
+        for (m, k, n) in ((9, 7, 5), (3, 2, 4), (17, 1, 6)):
+            a = rng.standard_normal((m, k))
+            b = rng.standard_normal((k, n))
+            for sa in (None, 0, 1):
+                for sb in (None, 0, 1):
+                    C = ht.array(a, split=sa) @ ht.array(b, split=sb)
+                    assert np.allclose(C.numpy(), a @ b, rtol=1e-10, atol=1e-12), (m, k, n, sa, sb)
+                    if sa == 0 and sb in (0, 1):
+                        assert C.split == 0
+            v = rng.standard_normal(k)
+            V = ht.array(v, split=0)
+            assert np.allclose(ht.matmul(ht.array(a, split=1), V).numpy(), a @ v)
+            assert np.allclose(ht.matmul(ht.array(a, split=0), V).numpy(), a @ v)
+    finally:
+        basics._RING_MIN_BYTES = old
+
+
+def check_qr_split1_panels():
+    """Column-split QR keeps the column split (Householder panel factorisation by the owner,
+    reflector broadcasts): orthogonal Q, A = QR, upper-triangular R, also for cond(A) = 1e10 and
+    for ranks with no columns."""
+    rng = np.random.default_rng(23)
+    for m, n, cond in ((120, 17, 1.0), (64, 40, 1e10), (50, 50, 1e3), (40, 3, 1.0)):
+        u, _ = np.linalg.qr(rng.standard_normal((m, n)))
+        v, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        a = (u * np.logspace(0, -np.log10(cond), n)) @ v.T
+        for mode in ("reduced", None):
+            if mode is None and m != n:
+                continue
+            q, r = ht.linalg.qr(ht.array(a, split=1), mode=mode or "complete")
+            assert q.split == 1 and r.split == 1
+            qn, rn = q.numpy(), r.numpy()
+            assert np.abs(qn.T @ qn - np.eye(n)).max() < 1e-12, np.abs(qn.T @ qn - np.eye(n)).max()
+            assert np.abs(qn @ rn - a).max() < 1e-12 * np.abs(a).max() * 10
+            assert np.allclose(rn, np.triu(rn))
+            assert np.all(np.diag(rn) >= 0)
+            _, r_only = ht.linalg.qr(ht.array(a, split=1), mode="reduced", calc_q=False)
+            assert np.allclose(r_only.numpy(), rn, atol=1e-10)
