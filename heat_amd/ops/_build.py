@@ -34,6 +34,17 @@ def headers():
     return sorted(glob.glob(os.path.join(CSRC, "*.h")))
 
 
+def file_flags(src: str) -> list:
+    """Extra per-source flags from a ``// hipcc-flags: ...`` line in the file's first 40 lines
+    (e.g. ``-fno-slp-vectorize`` for MFMA kernels: SLP-packed f32 VALU beside MFMAs costs ~5x a
+    scalar op's issue slot on gfx950)."""
+    with open(src) as f:
+        for _, line in zip(range(40), f):
+            if line.startswith("// hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
@@ -69,7 +80,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     jobs = max(1, min(len(objs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
     try:
         with ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(lambda so: run([hipcc()] + flags + ["-c", so[0], "-o", so[1]]), zip(sources(), objs)))
+            list(ex.map(lambda so: run([hipcc()] + flags + file_flags(so[0]) + ["-c", so[0], "-o", so[1]]),
+                        zip(sources(), objs)))
         run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", tmp])
     except subprocess.CalledProcessError as e:
         os.unlink(tmp)

@@ -1,3 +1,4 @@
+// hipcc-flags: -fno-slp-vectorize
 // K-means assignment on the FP16 matrix cores with a 3-term split ("f16x3"): ~fp32-GEMM accuracy
 // at 16x the per-instruction MFMA rate of the f32-input MFMA (v_mfma_f32_32x32x16_f16: 16K MACs
 // in 32 cycles/SIMD vs v_mfma_f32_32x32x2_f32: 2K MACs in 64).
@@ -149,9 +150,15 @@ __global__ __launch_bounds__(256) void h3_pack_centroids(const float* __restrict
   *reinterpret_cast<halfx8*>(image + base + 64 * 8 + (int64_t)lane * 8) = lo;
 }
 
-// the per-pair score of 2 adjacent accumulator values: s_x (x.c - |c|^2/2) = D r_c - s_x u_c
+// the per-pair score of 2 adjacent accumulator values: s_x (x.c - |c|^2/2) = D r_c - s_x u_c.
+// Scalar f32 ops on purpose (the file is built with -fno-slp-vectorize): a v_pk_fma_f32 /
+// v_pk_mul_f32 issued beside MFMAs costs ~5x the issue slot of a scalar v_fma_f32 on gfx950, and
+// this epilogue runs in the MFMA gaps.
 __device__ __forceinline__ floatx2 h3_score2(floatx2 acc, floatx2 r, floatx2 u, floatx2 nsx) {
-  return __builtin_elementwise_fma(acc, r, nsx * u);
+  floatx2 o;
+  o[0] = fmaf(acc[0], r[0], nsx[0] * u[0]);
+  o[1] = fmaf(acc[1], r[1], nsx[1] * u[1]);
+  return o;
 }
 
 // Assignment kernel. A wave keeps NPB 32-point blocks (hi/lo fragments) in registers; the packed
