@@ -28,7 +28,16 @@
 namespace {
 
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+// fp32 -> bf16 bits, round to nearest even (finite input)
+__device__ __forceinline__ unsigned h3_bf16_rn(float x) {
+  const unsigned b = __float_as_uint(x);
+  return (b + 0x7FFFu + ((b >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float h3_bf16_f(unsigned b) { return __uint_as_float(b << 16); }
 
 template <int FPAD, int NPB_ = 2>
 struct H3Cfg {
@@ -87,7 +96,8 @@ __global__ __launch_bounds__(256) void h3_pack_points(const float* __restrict__ 
 //   features h*F2 + 8 ks .. +8) of c * s_c split into fp16 hi / lo.
 template <int FPAD>
 __global__ __launch_bounds__(256) void h3_cscale(const float* __restrict__ C, int k, int f, int64_t ldc, int kpad,
-                                                 float* __restrict__ ur, float* __restrict__ meta) {
+                                                 float* __restrict__ ur, float* __restrict__ meta,
+                                                 unsigned* __restrict__ vimg) {
   constexpr int G8 = FPAD / 8;  // lanes per centroid (divides 64)
   constexpr int CB = H3Cfg<FPAD>::CB;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -108,15 +118,31 @@ __global__ __launch_bounds__(256) void h3_cscale(const float* __restrict__ C, in
   }
   if (g8 != 0 || c >= kpad) return;
   float* urc = ur + (int64_t)(c / CB) * 2 * CB + c % CB;
+  // rank-1 A fragment of the -s_c u_c term (see h3_assign_p): lane j of tile c/32 holds its three
+  // bf16 pieces in k-slots 0..2, lane j + 32 (k-slots 8..15) zeros
+  unsigned* vc = vimg + ((int64_t)(c / 32) * 64 + c % 32) * 2;
+  vc[64] = 0u;
+  vc[65] = 0u;
   if (!live) {
     urc[0] = __builtin_huge_valf();
     urc[CB] = 1.f;
+    vc[0] = 0xFF80u;  // -inf, 0
+    vc[1] = 0u;
     return;
   }
   int e = 0;
   if (mx > 0.f && mx < __builtin_huge_valf()) frexpf(mx, &e);
   urc[0] = 0.5f * sq;
   urc[CB] = ldexpf(1.f, e);
+  {
+    const float y = -ldexpf(0.5f * sq, -e);  // -s_c u_c, split into hi + mid + lo (24 bits)
+    const unsigned hi = h3_bf16_rn(y);
+    const float r1 = y - h3_bf16_f(hi);
+    const unsigned mid = h3_bf16_rn(r1);
+    const unsigned lo = h3_bf16_rn(r1 - h3_bf16_f(mid));
+    vc[0] = hi | (mid << 16);
+    vc[1] = lo;
+  }
   if (mx > 0.f && mx < __builtin_huge_valf())
     atomicMax(reinterpret_cast<unsigned int*>(meta + 1), __float_as_uint(mx));
   if (sq > 0.f && sq < __builtin_huge_valf())
@@ -193,6 +219,7 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
   const int64_t pbase = blk * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
 
   halfx8 bhi[NPB][KS], blo[NPB][KS];
+  bf16x8 bsx[NPB];
   float sx[NPB], nsx[NPB], xsq[NPB];
   int64_t prow[NPB];
 #pragma unroll
@@ -216,6 +243,10 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
     sx[pb] = sxv[row];
     nsx[pb] = -sx[pb];
     xsq[pb] = q;
+    // B fragment of the rank-1 term: s_x (a power of two: exact in bf16) in k-slots 0..2
+    const unsigned sb = __float_as_uint(sx[pb]) >> 16;
+    const u32x4 bw = {h ? 0u : (sb | (sb << 16)), h ? 0u : sb, 0u, 0u};
+    bsx[pb] = __builtin_bit_cast(bf16x8, bw);
   }
   float best[NPB];
   int btile[NPB];
@@ -231,31 +262,23 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
   constexpr int PIECES = CHUNK_H * 2 / 1024;  // 1 KB (64 lanes x 16 B) per DMA instruction
   // two chunk buffers: the epilogue of a chunk's last tile runs during the next chunk's first
   // tile and still reads its u/r from the previous buffer
-  constexpr int BUF = CHUNK_H * 2 + CB * 8;
+  constexpr int VPIECES = CB * 16 / 1024;  // rank-1 fragments: 512 B per 32-centroid tile
+  constexpr int BUF = CHUNK_H * 2 + CB * 8 + CB * 16;
+  const unsigned* vimg = reinterpret_cast<const unsigned*>(meta + 4);
   floatx16 acc[2][NPB];
   const float* pu = nullptr;  // LDS u/r of the tile whose epilogue is pending
   int ptile = -1;
   auto epilogue = [&](const floatx16 (&ac)[NPB], const float* pu_, int tile) {
-    // u and r of the tile straight from LDS (the chunk buffer is still live: see the loop)
-    floatx4 cn[4], cr[4];
+    // r of the tile straight from LDS (the chunk buffer is still live: see the loop); the
+    // accumulator already holds s_c s_x (x.c - u_c) (rank-1 MFMA), so the score is ONE multiply
+    floatx4 cr[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      cn[g] = *reinterpret_cast<const floatx4*>(pu_ + 8 * g + 4 * h);
-      cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
-    }
+    for (int g = 0; g < 4; ++g) cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb) {
-      const floatx2 sx2 = {nsx[pb], nsx[pb]};
       float w[16];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const floatx2 c2 = {cn[q >> 1][(2 * q) & 3], cn[q >> 1][(2 * q + 1) & 3]};
-        const floatx2 rc2 = {cr[q >> 1][(2 * q) & 3], cr[q >> 1][(2 * q + 1) & 3]};
-        const floatx2 a2 = {ac[pb][2 * q], ac[pb][2 * q + 1]};
-        const floatx2 r2 = h3_score2(a2, rc2, c2, sx2);
-        w[2 * q] = r2[0];
-        w[2 * q + 1] = r2[1];
-      }
+      for (int q = 0; q < 16; ++q) w[q] = ac[pb][q] * cr[q >> 2][q & 3];
       float m = w[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) m = fmaxf(m, w[r]);
@@ -277,12 +300,18 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
       if (wave == 0 && lane < CB / 2)  // u and r of the chunk (adjacent)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
                                          (__attribute__((address_space(3))) void*)(dst + CHUNK_H * 2), 16, 0, 0);
+#pragma unroll
+      for (int pc = wave; pc < VPIECES; pc += 4)  // rank-1 fragments of the chunk's tiles
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(vimg) + (int64_t)ch * CB * 16 + pc * 1024 + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H * 2 + CB * 8 + pc * 1024),
+                                         16, 0, 0);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
     const unsigned char* buf = smem + (ch & 1) * BUF;
     const _Float16* img = reinterpret_cast<const _Float16*>(buf);
     const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
+    const unsigned* vb = reinterpret_cast<const unsigned*>(buf + CHUNK_H * 2 + CB * 8);
 #pragma unroll
     for (int cb = 0; cb < CB / 32; ++cb) {
       const int cur = cb & 1;  // CB/32 is even: ping-pong slot is compile-time
@@ -300,12 +329,21 @@ __global__ __launch_bounds__(256, MINB) void h3_assign_p(const _Float16* __restr
           acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
         }
       }
+      {
+        // + s_x (-s_c u_c) as one bf16 MFMA (3 pieces x s_x, exact products, fp32 accumulation)
+        const uint2 vv = *reinterpret_cast<const uint2*>(vb + (cb * 64 + lane) * 2);
+        const u32x4 aw = {vv.x, vv.y, 0u, 0u};
+        const bf16x8 av = __builtin_bit_cast(bf16x8, aw);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb)
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bsx[pb], acc[cur][pb], 0, 0, 0);
+      }
       // epilogue of the previous tile (independent of the MFMAs above)
       if (ptile >= 0) epilogue(acc[cur ^ 1], pu, ptile);
       ptile = ch * (CB / 32) + cb;
       pu = ub + cb * 32;
 #pragma unroll
-      for (int i = 0; i < 3 * KS * NPB; ++i) {
+      for (int i = 0; i < (3 * KS + 1) * NPB; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to 4 VALU
       }
@@ -875,7 +913,9 @@ HA_EXPORT int64_t ha_h3_workspace_bytes(int k, int f) {
   if (fpad < 0 || k <= 0) return -1;
   const int cb = fpad >= 128 ? 64 : 128;
   const int64_t kpad = (int64_t)(k + cb - 1) / cb * cb;
-  return kpad * fpad * 2 * 2 + kpad * 8 + 16;  // image + (u, r) per chunk + meta {-, max|c|_inf, u_max, -}
+  // image + (u, r) per chunk + meta {-, max|c|_inf, u_max, -} + rank-1 u-term fragments (64 lanes x
+  // 8 B per 32-centroid tile)
+  return kpad * fpad * 2 * 2 + kpad * 8 + 16 + kpad * 16;
 }
 
 HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f, const float* C, int k, int64_t ldc,
@@ -896,10 +936,10 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
     constexpr int NPB = FP >= 128 ? 1 : 2, MINB = 2;  /* 2 chunk buffers (~66 KB) per WG: 2 WGs/CU */                                        \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta);                              \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
-    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8);                                          \
+    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8 + KC::CB * 16);                            \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                         \
     hipFuncSetAttribute(reinterpret_cast<const void*>(h3_assign_p<FP, NPB, true, MINB>),                    \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                              \
@@ -951,7 +991,7 @@ HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_
     using KC = H3Cfg<FP, NPB>;                                                                              \
     using K1 = H3Cfg<FP, NPB1>;                                                                             \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta);                              \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
     const size_t lds1 = 2 * ((size_t)K1::CHUNK_H + K1::CB * 8);                                                   \
@@ -960,7 +1000,7 @@ HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);                             \
     hipLaunchKernelGGL((h1_filter<FP, NPB1, MINB1>), dim3(blocks1), dim3(256), lds1, s, p, sx, n, image, u, meta, \
                        kpad / K1::CB, labels, amb_rows, amb_count);                                        \
-    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8);                                          \
+    const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8 + KC::CB * 16);                            \
     const int64_t maxb = (n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG;                                        \
     const unsigned blocks = (unsigned)(maxb < (int64_t)ncu * MINB ? maxb : (int64_t)ncu * MINB);            \
     hipFuncSetAttribute(reinterpret_cast<const void*>(h3_assign_p<FP, NPB, true, MINB, true>),              \
@@ -1013,7 +1053,7 @@ HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, 
   case FP: {                                                                                                 \
     using KC = H3Cfg<FP, 1>;                                                                                 \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                           \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, m, f, ldc, kpad, u, meta);                               \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, m, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));          \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),   \
                        dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                \
     const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 8;                                                 \
@@ -1079,7 +1119,7 @@ HA_EXPORT int ha_h3_assign_r(const void* planes, const float* sx, int64_t n, int
     constexpr int NPB = FP >= 128 ? 1 : 2;                                                                  \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta);                              \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
     for (int ph = 0; ph < phases; ++ph) {                                                                   \
