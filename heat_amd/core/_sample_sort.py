@@ -18,6 +18,18 @@ import torch
 from .dndarray import _chunk_counts
 
 
+def local_sort(t: torch.Tensor, dim: int = -1, descending: bool = False):
+    """Stable ``torch.sort`` semantics; device float32 / int32 data goes to the native LSD radix
+    sort (``ops.sort_rows``, csrc/radix.hip)."""
+    from .. import ops
+
+    if ops.radix_sort_supported(t):
+        moved = t.movedim(dim, -1)
+        v, i = ops.sort_rows(moved, descending)
+        return v.movedim(-1, dim), i.movedim(-1, dim)
+    return torch.sort(t, dim=dim, descending=descending, stable=True)
+
+
 def _overlap(lo: np.ndarray, hi: np.ndarray, a: int, b: int) -> np.ndarray:
     """Length of the intersection of every interval [lo, hi) with [a, b)."""
     return np.clip(np.minimum(hi, b) - np.maximum(lo, a), 0, None)
@@ -36,7 +48,7 @@ def sort_columns(cols: torch.Tensor, gidx: torch.Tensor, comm, n_total: int):
     p, me = comm.size, comm.rank
     C, nloc = cols.shape
     dev = cols.device
-    vals, order = torch.sort(cols, dim=1, stable=True)
+    vals, order = local_sort(cols, 1)
     idx = gidx[order]
     ar_p = torch.arange(1, p, device=dev)
     # p-1 regular samples per rank and column -> p-1 pivots per column (same on every rank)
@@ -63,7 +75,7 @@ def sort_columns(cols: torch.Tensor, gidx: torch.Tensor, comm, n_total: int):
     # merge: order by (column, value); stable, so ties keep source-rank (= global position) order
     colid = torch.repeat_interleave(torch.arange(C, device=dev).repeat(p),
                                     torch.as_tensor(recv_cnt.reshape(-1), device=dev))
-    mv, o = torch.sort(mv, stable=True)
+    mv, o = local_sort(mv)
     o2 = torch.sort(colid[o], stable=True)[1]
     mv, mi = mv[o2], mi[o[o2]]
     # rebalance: column c on rank r now holds sorted positions [start[c, r], start[c, r] + held[c, r])

@@ -833,7 +833,7 @@ def sort(a: DNDarray, axis: int = -1, descending: bool = False, out: Optional[DN
         raise TypeError("expected a to be a DNDarray")
     axis = sanitize_axis(a.gshape, axis)
     if not a.is_distributed() or axis != a.split:
-        vals, idx = torch.sort(a.larray, dim=axis, descending=descending, stable=True)
+        vals, idx = _sample_sort.local_sort(a.larray, axis, descending)
         v = DNDarray(vals, a.gshape, a.dtype, a.split, a.device, a.comm, a.balanced)
         i = DNDarray(idx, a.gshape, types.int64, a.split, a.device, a.comm, a.balanced)
         if out is not None:

@@ -17,7 +17,8 @@ from . import check, lib, stream_ptr, use_native
 __all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr",
-           "householder_factor", "householder_apply", "householder_block"]
+           "householder_factor", "householder_apply", "householder_block",
+           "radix_sort_supported", "sort_rows"]
 
 _NUM_CUS = {}
 
@@ -1141,3 +1142,31 @@ def _hh_larft_host(Y, tau):
             T[:j, j] = -tj * (T[:j, :j] @ Y[:j, j])
         T[j, j] = tj
     return T.to(tau.dtype)
+
+
+_RADIX_DTYPES = {torch.float32: 0, torch.int32: 1}
+
+
+def radix_sort_supported(t: torch.Tensor) -> bool:
+    """Device float32 / int32 tensors below 2^31 elements go to the native radix sort."""
+    return t.is_cuda and t.dtype in _RADIX_DTYPES and 0 < t.numel() < (1 << 31) - 1 and use_native(t)
+
+
+def sort_rows(x: torch.Tensor, descending: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Stable sort along the last axis (``csrc/radix.hip``: LSD radix, 8-bit digits, row number
+    as the most significant digits of a batch) - ``torch.sort(x, dim=-1, stable=True)``
+    semantics: ties keep their order, NaN sorts last (first when descending), -0.0 ties +0.0.
+    Returns (values, int64 positions)."""
+    shp = x.shape
+    rowlen = shp[-1] if x.dim() else 1
+    xc = x.contiguous()
+    rows = xc.numel() // max(rowlen, 1)
+    vals = torch.empty_like(xc)
+    idx = torch.empty(shp, dtype=torch.int64, device=x.device)
+    if xc.numel() == 0:
+        return vals, idx
+    L = lib()
+    ws = torch.empty(L.ha_radix_workspace_bytes(xc.numel()), dtype=torch.uint8, device=x.device)
+    check(L.ha_radix_sort_rows(_ptr(xc), _RADIX_DTYPES[x.dtype], rows, rowlen, int(descending), _ptr(vals), _ptr(idx),
+                               _ptr(ws), ctypes.c_void_p(stream_ptr(x.device))), "ha_radix_sort_rows")
+    return vals, idx
