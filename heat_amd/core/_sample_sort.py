@@ -23,7 +23,7 @@ def local_sort(t: torch.Tensor, dim: int = -1, descending: bool = False):
     sort (``ops.sort_rows``, csrc/radix.hip)."""
     from .. import ops
 
-    if ops.radix_sort_supported(t):
+    if ops.radix_sort_supported(t, dim):
         moved = t.movedim(dim, -1)
         v, i = ops.sort_rows(moved, descending)
         return v.movedim(-1, dim), i.movedim(-1, dim)

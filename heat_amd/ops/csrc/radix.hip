@@ -13,10 +13,12 @@
 // One pass = three kernels over tiles of 4096 elements (256 threads x 16 items):
 //   rs_hist     per-tile 256-bin histogram in LDS -> hist[digit][tile]
 //   rs_scan     one workgroup per digit: exclusive scan of its row of tile counts, row total
-//   rs_scatter  per tile: base of each digit (a 256-entry scan of the totals in LDS) + the tile's
-//               offset + a stable rank: within a wave from eight ballots (lanes with the same
-//               digit = AND of the per-bit ballot masks), across waves and items from LDS counters
-//               updated in element order.
+//   rs_scatter  per tile: a stable rank of every element (within a wave from eight ballots - lanes
+//               with the same digit = AND of the per-bit ballot masks - and wave-private running
+//               counters in LDS; waves own contiguous quarters of the tile, so only two block
+//               barriers), the tile sorted by digit in LDS, then every digit's run written to its
+//               global place (base of the digit = a 256-entry scan of the totals + the tile's
+//               offset) by consecutive threads.
 #include "common.h"
 
 namespace {
@@ -109,36 +111,36 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const unsigned* __restr
                                                          const unsigned* __restrict__ totals,
                                                          unsigned* __restrict__ okeys, int* __restrict__ opay) {
   __shared__ unsigned s[RS_THREADS];
-  __shared__ unsigned gbase[256];
-  __shared__ unsigned run[256];
-  __shared__ unsigned cw[4][256];
+  __shared__ unsigned gbase[256];   // global start of each digit's run of this tile
+  __shared__ unsigned tdo[256];     // start of each digit's run inside the tile
+  __shared__ unsigned wc[4][256];   // per-wave running counts, then per-wave offsets
+  __shared__ unsigned sk[RS_TILE];  // the tile, locally sorted by digit
+  __shared__ int sp[RS_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   {
     unsigned tot;
     const unsigned ex = rs_block_scan(totals[tid], s, tot);
     gbase[tid] = ex + hist[(int64_t)tid * ntiles + blockIdx.x];
-    run[tid] = 0u;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) cw[w][tid] = 0u;
+    for (int w = 0; w < 4; ++w) wc[w][tid] = 0u;
   }
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t base = (int64_t)blockIdx.x * RS_TILE;
-  unsigned kr[RS_ITEMS];
+  // wave w owns the contiguous quarter [w * 1024, (w + 1) * 1024) of the tile, item by item: the
+  // element order is (wave, item, lane), so ranks taken in that order are stable
+  unsigned kr[RS_ITEMS], rk[RS_ITEMS];
   int pr[RS_ITEMS];
 #pragma unroll
-  for (int i = 0; i < RS_ITEMS; ++i) {  // the whole tile in registers up front (one latency)
-    const int64_t idx = base + i * RS_THREADS + tid;
-    kr[i] = idx < N ? keys[idx] : 0u;
-    pr[i] = idx < N ? pay[idx] : 0;
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    const int64_t e = base + wave * (RS_ITEMS * 64) + i * 64 + lane;
+    kr[i] = e < N ? keys[e] : 0u;
+    pr[i] = e < N ? pay[e] : 0;
   }
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
-    const int64_t idx = base + i * RS_THREADS + tid;
-    const bool valid = idx < N;
-    const unsigned k = kr[i];
-    const int pl = pr[i];
-    const unsigned d = valid ? rs_digit(k, pl, shift, mode, rowlen) : 0u;
+    const bool valid = base + wave * (RS_ITEMS * 64) + i * 64 + lane < N;
+    const unsigned d = rs_digit(kr[i], pr[i], shift, mode, rowlen);
     uint64_t match = __ballot(valid);
 #pragma unroll
     for (int bit = 0; bit < 8; ++bit) {
@@ -146,23 +148,44 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const unsigned* __restr
       const uint64_t bb = __ballot(on);
       match &= on ? bb : ~bb;
     }
-    const unsigned rank = __popcll(match & lt);
-    if (valid && rank == 0u) cw[wave][d] = (unsigned)__popcll(match);  // one leader per digit group
-    __syncthreads();
-    if (valid) {
-      unsigned before = run[d];
-      for (int w = 0; w < wave; ++w) before += cw[w][d];
-      const int64_t pos = (int64_t)gbase[d] + before + rank;
-      if (pos < N) {  // always true for consistent counts; never write out of bounds
-        okeys[pos] = k;
-        opay[pos] = pl;
-      }
-    }
-    __syncthreads();
-    run[tid] += cw[0][tid] + cw[1][tid] + cw[2][tid] + cw[3][tid];
+    const unsigned r = __popcll(match & lt);
+    rk[i] = wc[wave][d] + r;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (valid && r == 0u) wc[wave][d] += (unsigned)__popcll(match);  // one leader per digit group
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  __syncthreads();
+  {
+    const unsigned c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
+    wc[0][tid] = 0u;
+    wc[1][tid] = c0;
+    wc[2][tid] = c0 + c1;
+    wc[3][tid] = c0 + c1 + c2;
+    unsigned tot;
+    tdo[tid] = rs_block_scan(c0 + c1 + c2 + c3, s, tot);
+  }
+  __syncthreads();
 #pragma unroll
-    for (int w = 0; w < 4; ++w) cw[w][tid] = 0u;
-    __syncthreads();
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    if (base + wave * (RS_ITEMS * 64) + i * 64 + lane < N) {
+      const unsigned d = rs_digit(kr[i], pr[i], shift, mode, rowlen);
+      const unsigned lp = tdo[d] + wc[wave][d] + rk[i];
+      sk[lp] = kr[i];
+      sp[lp] = pr[i];
+    }
+  }
+  __syncthreads();
+  // write the digit runs out: consecutive threads -> consecutive addresses within a run
+  const int cnt = (int)(N - base < RS_TILE ? N - base : RS_TILE);
+  for (int j = tid; j < cnt; j += RS_THREADS) {
+    const unsigned k = sk[j];
+    const int pl = sp[j];
+    const unsigned d = rs_digit(k, pl, shift, mode, rowlen);
+    const int64_t pos = (int64_t)gbase[d] + (j - (int)tdo[d]);
+    if (pos < N) {  // always true for consistent counts; never write out of bounds
+      okeys[pos] = k;
+      opay[pos] = pl;
+    }
   }
 }
 
