@@ -361,6 +361,25 @@ class MPICommunication(Communication):
             ar = self._ipc = ipc.IpcAllreduce(self, capacity_bytes=ipc.max_bytes())
         return ar.allreduce_(t)
 
+    def _ipc_allgather(self, moved: torch.Tensor, counts: Sequence[int]):
+        """Direct W-peer xGMI all-gather (``parallel/ipc.py``) of device row blocks when IPC
+        collectives are enabled on a node-local world communicator; None where it does not apply
+        (same SPMD-identical conditions as ``_ipc_allreduce``, plus blocks of whole 32-bit words)."""
+        from ..parallel import ipc
+
+        row = int(np.prod(moved.shape[1:])) * moved.element_size() if moved.dim() > 1 else moved.element_size()
+        if not (ipc.enabled() and moved.is_cuda and self.group is None and moved.is_contiguous()
+                and row % 4 == 0 and max(counts) * row <= ipc.max_bytes()
+                and int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == dist.get_world_size() == self.size):
+            return None
+        ar = getattr(self, "_ipc", None)
+        if ar is None:
+            ar = self._ipc = ipc.IpcAllreduce(self, capacity_bytes=ipc.max_bytes())
+        flat = ar.allgather(moved, [c * row for c in counts])
+        if flat is None:
+            return None
+        return flat.view(moved.dtype).reshape((sum(counts),) + tuple(moved.shape[1:]))
+
     def _reduce_tensor_async(self, t: torch.Tensor, op: Op):
         """All-reduce ``t`` in place (returns (work, finalize))."""
         if op is MPI.SUM and self._ipc_allreduce(t) is not None:
@@ -484,6 +503,9 @@ class MPICommunication(Communication):
         if counts is None:
             counts = self.allgather_sizes(moved.shape[0])
         rest = tuple(moved.shape[1:])
+        got = self._ipc_allgather(moved, counts) if len(counts) else None
+        if got is not None:
+            return _SD.StagedWork(None), (lambda: got.movedim(0, axis) if axis != 0 else got)
         mx = max(counts) if len(counts) else 0
         if all(c == mx for c in counts):
             padded = moved

@@ -1,6 +1,8 @@
-// One-shot intra-node all-reduce over peer (xGMI) mappings of hipIpc-shared buffers (SURVEY N2:
-// the small-message path for the k-means k*f+k sums, moment triples, argmin packs and metadata
-// maps, where RCCL's ring/tree start-up dominates).
+// Intra-node collectives over peer (xGMI) mappings of hipIpc-shared buffers: a
+// one-shot all-reduce (small messages: the k-means k*f+k sums, moment triples, argmin packs,
+// metadata maps, where RCCL's ring/tree start-up dominates), a two-shot reduce-scatter +
+// all-gather all-reduce for larger payloads and a direct W-peer all-gather (ipc_allreduce2,
+// ipc_allgather below).
 //
 // Every rank owns one data buffer (two slots, alternating by call parity) and one signal buffer,
 // both exported with hipIpcGetMemHandle and mapped by every peer. One call = one kernel:
@@ -28,7 +30,8 @@ namespace {
 
 constexpr int IPC_MAX_RANKS = 8;
 constexpr int IPC_MAX_BLOCKS = 64;
-constexpr int IPC_ERR_WORD = IPC_MAX_BLOCKS * IPC_MAX_RANKS;  // uint32 index of the error word
+constexpr int IPC_PHASES = 2;  // barriers per call (two-shot: after the copy, after the reduction)
+constexpr int IPC_ERR_WORD = IPC_PHASES * IPC_MAX_BLOCKS * IPC_MAX_RANKS;  // uint32 index of the error word
 
 struct PeerPtrs {
   void* data[IPC_MAX_RANKS];
@@ -39,6 +42,34 @@ template <typename T>
 __device__ __forceinline__ T poison() {
   if constexpr (std::is_integral<T>::value) return std::numeric_limits<T>::min();  // an implausible sum
   else return std::numeric_limits<T>::quiet_NaN();
+}
+
+// Per-block barrier among the W ranks for phase ph of the call with this epoch: threads 0..W-1
+// release this block's writes and announce them to peer threadIdx.x, then wait for that peer's
+// announcement. Returns false (and records the error word) when a peer misses it.
+template <int W>
+__device__ bool ipc_block_barrier(const PeerPtrs& pp, int rank, int ph, unsigned epoch, int64_t max_spins,
+                                  int* timed_out) {
+  __syncthreads();
+  const int b = blockIdx.x;
+  if (threadIdx.x < W) {
+    const int slotw = (ph * IPC_MAX_BLOCKS + b) * IPC_MAX_RANKS;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(pp.sig[threadIdx.x] + slotw + rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* flag = pp.sig[rank] + slotw + threadIdx.x;
+    int64_t spins = 0;
+    while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (++spins > max_spins) {
+        __hip_atomic_store(pp.sig[rank] + IPC_ERR_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *timed_out = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  return *timed_out == 0;
 }
 
 template <typename T, int W>
@@ -53,26 +84,7 @@ __global__ __launch_bounds__(256) void ipc_allreduce(PeerPtrs pp, int rank, T* _
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
   T* mine = reinterpret_cast<T*>(pp.data[rank]) + slot_off;
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = buf[i];
-  __syncthreads();
-  if (threadIdx.x < W) {
-    // publish this block's slice, then announce it to peer threadIdx.x
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store(pp.sig[threadIdx.x] + b * IPC_MAX_RANKS + rank, epoch, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    unsigned* flag = pp.sig[rank] + b * IPC_MAX_RANKS + threadIdx.x;
-    int64_t spins = 0;
-    while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > max_spins) {
-        __hip_atomic_store(pp.sig[rank] + IPC_ERR_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        timed_out = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  }
-  __syncthreads();
-  if (timed_out) {
+  if (!ipc_block_barrier<W>(pp, rank, 0, epoch, max_spins, &timed_out)) {
     // a peer never arrived: poison this block's output instead of summing stale slots
     for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) buf[i] = poison<T>();
     return;
@@ -91,15 +103,96 @@ __global__ __launch_bounds__(256) void ipc_allreduce(PeerPtrs pp, int rank, T* _
   }
 }
 
+// Two-shot all-reduce for larger payloads: the input is cut into W segments; after the copy
+// barrier rank r sums segment r of every slot (rank order) back into its own slot, and after the
+// second barrier every rank gathers the W reduced segments from their owners' slots. Each rank
+// moves 2 (W-1)/W n elements over the links instead of the one-shot's (W-1) n. Block b handles
+// sub-chunk b of every segment, so both barriers stay per block.
+template <typename T, int W>
+__global__ __launch_bounds__(256) void ipc_allreduce2(PeerPtrs pp, int rank, T* __restrict__ buf, int64_t n,
+                                                      int64_t slot_off, unsigned epoch, int64_t max_spins) {
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  const int64_t seg = (n + W - 1) / W;
+  const int64_t sc = (seg + gridDim.x - 1) / gridDim.x;
+  const int64_t o0 = (int64_t)blockIdx.x * sc;
+  T* mine = reinterpret_cast<T*>(pp.data[rank]) + slot_off;
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    const int64_t lo = q * seg + o0, hi = min(min(lo + sc, (q + 1) * seg), n);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = buf[i];
+  }
+  bool ok = ipc_block_barrier<W>(pp, rank, 0, epoch, max_spins, &timed_out);
+  if (ok) {
+    const T* src[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) src[r] = reinterpret_cast<const T*>(pp.data[r]) + slot_off;
+    const int64_t lo = rank * seg + o0, hi = min(min(lo + sc, (rank + 1) * seg), n);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      T v[W];
+#pragma unroll
+      for (int r = 0; r < W; ++r) v[r] = src[r][i];
+      T acc = v[0];
+#pragma unroll
+      for (int r = 1; r < W; ++r) acc += v[r];
+      mine[i] = acc;  // only this rank reads segment `rank` of its own slot
+    }
+    ok = ipc_block_barrier<W>(pp, rank, 1, epoch, max_spins, &timed_out);
+  } else {
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    const T* sq = reinterpret_cast<const T*>(pp.data[q]) + slot_off;
+    const int64_t lo = q * seg + o0, hi = min(min(lo + sc, (q + 1) * seg), n);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) buf[i] = ok ? sq[i] : poison<T>();
+  }
+}
+
+// Direct all-gather: every rank copies its block (count[rank] 32-bit words) into its slot; after
+// the barrier it pulls every peer's block straight from the peer's slot into out + displ[q] - W-1
+// concurrent reads over the point-to-point xGMI links instead of a ring's W-1 dependent steps.
+struct GatherLayout {
+  int64_t count[IPC_MAX_RANKS];
+  int64_t displ[IPC_MAX_RANKS];
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void ipc_allgather(PeerPtrs pp, int rank, const unsigned* __restrict__ in,
+                                                     unsigned* __restrict__ out, GatherLayout gl, int64_t slot_off,
+                                                     unsigned epoch, int64_t max_spins) {
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  unsigned* mine = reinterpret_cast<unsigned*>(pp.data[rank]) + slot_off;
+  {
+    const int64_t c = gl.count[rank], sc = (c + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * sc, hi = min(lo + sc, c);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = in[i];
+  }
+  const bool ok = ipc_block_barrier<W>(pp, rank, 0, epoch, max_spins, &timed_out);
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    const unsigned* sq = reinterpret_cast<const unsigned*>(pp.data[q]) + slot_off;
+    const int64_t c = gl.count[q], sc = (c + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * sc, hi = min(lo + sc, c);
+    unsigned* o = out + gl.displ[q];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) o[i] = ok ? sq[i] : 0xFFFFFFFFu;
+  }
+}
+
 template <typename T>
 int launch(const PeerPtrs& pp, int world, int rank, T* buf, int64_t n, int64_t slot_off, unsigned epoch,
-           int blocks, int64_t max_spins, hipStream_t s) {
+           int blocks, int64_t max_spins, int two_shot, hipStream_t s) {
   const int64_t chunk = (n + blocks - 1) / blocks;
   const int grid = (int)((n + chunk - 1) / chunk);
 #define HA_IPC(WN)                                                                                          \
   case WN:                                                                                                  \
-    hipLaunchKernelGGL((ipc_allreduce<T, WN>), dim3(grid), dim3(256), 0, s, pp, rank, buf, n, chunk, slot_off, \
-                       epoch, max_spins);                                                                   \
+    if (two_shot)                                                                                           \
+      hipLaunchKernelGGL((ipc_allreduce2<T, WN>), dim3(blocks), dim3(256), 0, s, pp, rank, buf, n, slot_off, \
+                         epoch, max_spins);                                                                 \
+    else                                                                                                    \
+      hipLaunchKernelGGL((ipc_allreduce<T, WN>), dim3(grid), dim3(256), 0, s, pp, rank, buf, n, chunk,      \
+                         slot_off, epoch, max_spins);                                                       \
     break;
   switch (world) {
     HA_IPC(2) HA_IPC(3) HA_IPC(4) HA_IPC(5) HA_IPC(6) HA_IPC(7) HA_IPC(8)
@@ -144,7 +237,7 @@ HA_EXPORT int ha_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipS
 // per slot; ``epoch`` must grow by one per call on every rank.
 HA_EXPORT int ha_ipc_allreduce(void* const* data, void* const* sig, int world, int rank, void* buf, int64_t n,
                                int dtype, int64_t slot_elems, unsigned epoch, int blocks, int64_t max_spins,
-                               void* stream) {
+                               int two_shot, void* stream) {
   if (world < 2 || world > IPC_MAX_RANKS || rank < 0 || rank >= world || n < 0 || n > slot_elems) return HA_BAD_ARG;
   if (n == 0) return HA_OK;
   blocks = blocks < 1 ? 1 : blocks > IPC_MAX_BLOCKS ? IPC_MAX_BLOCKS : blocks;
@@ -156,11 +249,48 @@ HA_EXPORT int ha_ipc_allreduce(void* const* data, void* const* sig, int world, i
   const int64_t slot_off = (epoch & 1u) ? slot_elems : 0;
   hipStream_t s = (hipStream_t)stream;
   switch (dtype) {
-    case 0: return launch<float>(pp, world, rank, (float*)buf, n, slot_off, epoch, blocks, max_spins, s);
-    case 1: return launch<double>(pp, world, rank, (double*)buf, n, slot_off, epoch, blocks, max_spins, s);
-    case 2: return launch<int64_t>(pp, world, rank, (int64_t*)buf, n, slot_off, epoch, blocks, max_spins, s);
+    case 0: return launch<float>(pp, world, rank, (float*)buf, n, slot_off, epoch, blocks, max_spins, two_shot, s);
+    case 1: return launch<double>(pp, world, rank, (double*)buf, n, slot_off, epoch, blocks, max_spins, two_shot, s);
+    case 2:
+      return launch<int64_t>(pp, world, rank, (int64_t*)buf, n, slot_off, epoch, blocks, max_spins, two_shot, s);
     default: return HA_UNSUPPORTED;
   }
+}
+
+// All-gather of 32-bit words: ``in`` holds counts[rank] words, ``out`` receives every rank's block
+// at displs[q] (words). slot_words: words per slot (>= every count). Same epoch rule as above.
+HA_EXPORT int ha_ipc_allgather(void* const* data, void* const* sig, int world, int rank, const void* in, void* out,
+                               const int64_t* counts, const int64_t* displs, int64_t slot_words, unsigned epoch,
+                               int blocks, int64_t max_spins, void* stream) {
+  if (world < 2 || world > IPC_MAX_RANKS || rank < 0 || rank >= world) return HA_BAD_ARG;
+  GatherLayout gl{};
+  int64_t total = 0;
+  for (int r = 0; r < world; ++r) {
+    if (counts[r] < 0 || counts[r] > slot_words) return HA_BAD_ARG;
+    gl.count[r] = counts[r];
+    gl.displ[r] = displs[r];
+    total += counts[r];
+  }
+  if (total == 0) return HA_OK;
+  blocks = blocks < 1 ? 1 : blocks > IPC_MAX_BLOCKS ? IPC_MAX_BLOCKS : blocks;
+  PeerPtrs pp{};
+  for (int r = 0; r < world; ++r) {
+    pp.data[r] = data[r];
+    pp.sig[r] = reinterpret_cast<unsigned*>(sig[r]);
+  }
+  const int64_t slot_off = (epoch & 1u) ? slot_words : 0;
+  hipStream_t s = (hipStream_t)stream;
+#define HA_AG(WN)                                                                                           \
+  case WN:                                                                                                  \
+    hipLaunchKernelGGL((ipc_allgather<WN>), dim3(blocks), dim3(256), 0, s, pp, rank, (const unsigned*)in,    \
+                       (unsigned*)out, gl, slot_off, epoch, max_spins);                                     \
+    break;
+  switch (world) {
+    HA_AG(2) HA_AG(3) HA_AG(4) HA_AG(5) HA_AG(6) HA_AG(7) HA_AG(8)
+    default: return HA_UNSUPPORTED;
+  }
+#undef HA_AG
+  return ha_launch_status();
 }
 
 // Stream-ordered copy of the error word into host memory (pinned, or any host pointer the runtime

@@ -1,6 +1,7 @@
 """
-Intra-node one-shot all-reduce over hipIpc-mapped peer buffers (kernel in
-``ops/csrc/ipc_allreduce.hip``).
+Intra-node collectives over hipIpc-mapped peer buffers (kernels in
+``ops/csrc/ipc_allreduce.hip``): one-shot all-reduce, two-shot (reduce-scatter + all-gather)
+all-reduce above ``HEAT_IPC_TWOSHOT_BYTES``, and a direct W-peer all-gather.
 
 For the small payloads the framework reduces once per algorithmic step (k-means' packed k*f + k
 sums, moment triples, arg-reduction packs, metadata maps) one kernel does the whole collective:
@@ -39,7 +40,10 @@ def _lib():
             ("ha_ipc_open", c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
             ("ha_ipc_close", c_int, [c_void_p]),
             ("ha_ipc_allreduce", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p,
-                                         c_int64, c_int, c_int64, c_uint, c_int, c_int64, c_void_p]),
+                                         c_int64, c_int, c_int64, c_uint, c_int, c_int64, c_int, c_void_p]),
+            ("ha_ipc_allgather", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p,
+                                         c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64), c_int64, c_uint,
+                                         c_int, c_int64, c_void_p]),
             ("ha_ipc_error", c_int, [c_void_p, c_int]),
             ("ha_ipc_error_async", c_int, [c_void_p, c_void_p, c_void_p])):
         fn = getattr(L, name)
@@ -58,8 +62,9 @@ def _check(rc: int, what: str):
 
 
 class IpcAllreduce:
-    """One-shot SUM all-reduce among the ranks of ``comm`` (all on this node, one GPU each, or
-    several ranks sharing a GPU in tests). ``capacity_bytes``: the largest payload."""
+    """SUM all-reduce (one-shot / two-shot) and all-gather among the ranks of ``comm`` (all on
+    this node, one GPU each, or several ranks sharing a GPU in tests). ``capacity_bytes``: the
+    largest all-reduce payload / per-rank all-gather block."""
 
     def __init__(self, comm, capacity_bytes: int = 4 << 20, blocks: int = 32, timeout_spins: int = 4_000_000):
         L = _lib()
@@ -70,6 +75,7 @@ class IpcAllreduce:
         self.capacity = int(capacity_bytes)
         self.blocks = max(1, min(int(blocks), L.ha_ipc_max_blocks()))
         self.spins = int(timeout_spins)
+        self.two_shot_bytes = two_shot_bytes()
         self.epoch = 0
         self.device = torch.device("cuda", torch.cuda.current_device())
         hs = L.ha_ipc_handle_size()
@@ -132,6 +138,38 @@ class IpcAllreduce:
         """Block until every issued call has finished and raise if any of them timed out."""
         self._poll(wait=True)
 
+    def _after(self, stream):
+        _check(self._L.ha_ipc_error_async(ctypes.c_void_p(self._own[1]), ctypes.c_void_p(self._err_host.data_ptr()),
+                                          ctypes.c_void_p(stream.cuda_stream)), "error copy")
+        if self._err_event is None:
+            self._err_event = torch.cuda.Event()
+        self._err_event.record(stream)
+
+    def allgather(self, t: torch.Tensor, counts_bytes) -> Optional[torch.Tensor]:
+        """Concatenation of every rank's contiguous device tensor ``t`` (rank q holds
+        ``counts_bytes[q]`` bytes) as a flat uint8 tensor on the current stream: every rank pulls
+        its W-1 peers' blocks directly from their slots. None when a block is not a multiple of 4
+        bytes or exceeds the slot."""
+        counts_bytes = [int(c) for c in counts_bytes]
+        if any(c % 4 or c > self.capacity for c in counts_bytes) or not t.is_contiguous() or not t.is_cuda:
+            return None
+        self._poll()
+        self.epoch += 1
+        words = [c // 4 for c in counts_bytes]
+        displ = [0] * self.world
+        for q in range(1, self.world):
+            displ[q] = displ[q - 1] + words[q - 1]
+        out = torch.empty(sum(counts_bytes), dtype=torch.uint8, device=t.device)
+        arr = ctypes.c_int64 * self.world
+        stream = torch.cuda.current_stream(t.device)
+        rc = self._L.ha_ipc_allgather(self._data, self._sig, self.world, self.rank, ctypes.c_void_p(t.data_ptr()),
+                                      ctypes.c_void_p(out.data_ptr()), arr(*words), arr(*displ), self.capacity // 4,
+                                      self.epoch & 0xFFFFFFFF, self.blocks, self.spins,
+                                      ctypes.c_void_p(stream.cuda_stream))
+        _check(rc, "all-gather launch")
+        self._after(stream)
+        return out
+
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place SUM of ``t`` over the ranks, ordered on the current stream. Raises
         :class:`IpcTimeoutError` when an EARLIER call timed out (this rank's view); a timed-out
@@ -141,17 +179,13 @@ class IpcAllreduce:
         self._poll()
         self.epoch += 1
         es = t.element_size()
+        two_shot = int(t.numel() * es > self.two_shot_bytes)
+        stream = torch.cuda.current_stream(t.device)
         rc = self._L.ha_ipc_allreduce(self._data, self._sig, self.world, self.rank, ctypes.c_void_p(t.data_ptr()),
                                       t.numel(), _DTYPES[t.dtype], self.capacity // es, self.epoch & 0xFFFFFFFF,
-                                      self.blocks, self.spins,
-                                      ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream))
+                                      self.blocks, self.spins, two_shot, ctypes.c_void_p(stream.cuda_stream))
         _check(rc, "launch")
-        stream = torch.cuda.current_stream(t.device)
-        _check(self._L.ha_ipc_error_async(ctypes.c_void_p(self._own[1]), ctypes.c_void_p(self._err_host.data_ptr()),
-                                          ctypes.c_void_p(stream.cuda_stream)), "error copy")
-        if self._err_event is None:
-            self._err_event = torch.cuda.Event()
-        self._err_event.record(stream)
+        self._after(stream)
         return t
 
     def error(self, clear: bool = False) -> int:
@@ -174,7 +208,13 @@ def enabled() -> bool:
 
 
 def max_bytes() -> int:
-    return int(os.environ.get("HEAT_IPC_MAX_BYTES", str(1 << 20)))
+    return int(os.environ.get("HEAT_IPC_MAX_BYTES", str(16 << 20)))
+
+
+def two_shot_bytes() -> int:
+    """Payload above which the all-reduce runs two-shot (each rank moves 2(W-1)/W of the data
+    instead of (W-1)x)."""
+    return int(os.environ.get("HEAT_IPC_TWOSHOT_BYTES", str(256 << 10)))
 
 
 def node_local(comm) -> bool:

@@ -108,3 +108,86 @@ def check_ipc_timeout_is_loud():
     else:
         time.sleep(0.5)
     comm.Barrier()
+
+
+def check_ipc_allgather_and_two_shot():
+    """Direct W-peer all-gather (uneven and empty blocks, float32 / int64 / bf16 rows) and the
+    two-shot all-reduce above the threshold, against host-built expectations; then the same
+    through ``MPICommunication.allgather_tensor`` with HEAT_IPC_ALLREDUCE=1."""
+    comm = ht.MPI_WORLD
+    p, r = comm.size, comm.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ar = IpcAllreduce(comm, capacity_bytes=4 << 20, blocks=16, timeout_spins=2_000_000)
+    for it in range(10):
+        for dtype, width in ((torch.float32, 3), (torch.int64, 1), (torch.bfloat16, 4)):
+            g = torch.Generator().manual_seed(31 * it + width)
+            counts = [int(c) for c in torch.randint(0, 700, (p,), generator=g)]
+            if it == 0:
+                counts[0] = 0
+            blocks = [(torch.randn(c, width, generator=g) * 100).to(dtype) for c in counts]
+            row = width * torch.tensor([], dtype=dtype).element_size()
+            out = ar.allgather(blocks[r].to(dev).contiguous(), [c * row for c in counts])
+            assert out is not None
+            got = out.view(dtype).reshape(-1, width).cpu()
+            assert torch.equal(got, torch.cat(blocks)), (it, dtype)
+    # two-shot all-reduce (payload > HEAT_IPC_TWOSHOT_BYTES), including n not divisible by p
+    for n in (300_001, 1 << 19):
+        full, ref = _inputs(900 + n, n, p, torch.float32)
+        t = full[r].clone().to(dev)
+        ar.allreduce_(t)
+        assert torch.equal(t.cpu(), ref)
+    ar.check()
+    ar.close()
+    os.environ["HEAT_IPC_ALLREDUCE"] = "1"
+    x = torch.arange(r * 10, r * 10 + 10 + r, dtype=torch.float32, device=dev).reshape(-1, 1).repeat(1, 4)
+    allx = comm.allgather_tensor(x, 0)
+    exp = torch.cat([torch.arange(q * 10, q * 10 + 10 + q, dtype=torch.float32).reshape(-1, 1).repeat(1, 4)
+                     for q in range(p)])
+    assert torch.equal(allx.cpu(), exp)
+    assert getattr(comm, "_ipc", None) is not None, "the IPC all-gather was not taken"
+    y = ht.random.randn(1000, 8, split=0, device="gpu")
+    yn = y.numpy()  # gathers through the IPC path
+    assert yn.shape == (1000, 8)
+    comm._ipc.check()
+
+
+def bench_ipc():
+    """Latency / bandwidth of the IPC collectives vs payload (rank 0 prints JSON lines). With the
+    ranks sharing one GPU the 'links' are local HBM: this measures the protocol (launch, barriers,
+    copies), not xGMI."""
+    import json
+    import time
+
+    comm = ht.MPI_WORLD
+    p, r = comm.size, comm.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ar = IpcAllreduce(comm, capacity_bytes=64 << 20, blocks=64, timeout_spins=50_000_000)
+    for nbytes in (4 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+        t = torch.ones(nbytes // 4, device=dev)
+        res = {"world": p, "bytes": nbytes}
+        for name, ts in (("one_shot", 1 << 62), ("two_shot", 0)):
+            ar.two_shot_bytes = ts
+            for _ in range(3):
+                ar.allreduce_(t)
+            torch.cuda.synchronize()
+            comm.Barrier()
+            reps = 20
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ar.allreduce_(t)
+            torch.cuda.synchronize()
+            res[name + "_us"] = round((time.perf_counter() - t0) / reps * 1e6, 1)
+        blk = torch.ones(nbytes // 4 // p, device=dev)
+        for _ in range(3):
+            ar.allgather(blk, [blk.numel() * 4] * p)
+        torch.cuda.synchronize()
+        comm.Barrier()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            ar.allgather(blk, [blk.numel() * 4] * p)
+        torch.cuda.synchronize()
+        res["allgather_us"] = round((time.perf_counter() - t0) / 20 * 1e6, 1)
+        if r == 0:
+            print(json.dumps(res), flush=True)
+    ar.check()
+    ar.close()
