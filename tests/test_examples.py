@@ -13,6 +13,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ("examples/classification/demo_knn.py", [], "fold accuracies"),
     ("examples/lasso/demo.py", [], "lambda="),
     ("examples/nn/mnist.py", ["--epochs", "1", "--samples", "512"], "epoch 0"),
+    ("examples/nn/imagenet.py", ["--epochs", "2", "--samples", "256", "--batch-size", "16", "--image-size", "32",
+                                 "--width", "8", "--classes", "10", "--layers", "1,1"], '"example": "imagenet"'),
+    ("examples/nn/imagenet-DASO.py", ["--epochs", "3", "--samples", "256", "--batch-size", "16", "--image-size",
+                                      "32", "--width", "8", "--classes", "10", "--layers", "1,1"],
+     '"example": "imagenet-DASO"'),
 ])
 def test_example(script, args, expect):
     env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
