@@ -50,14 +50,18 @@ def binary_op(operation: Callable, t1, t2, out: Optional[DNDarray] = None, where
     """Element-wise ``operation(t1, t2)`` with NumPy broadcasting and heat split semantics."""
     fn_kwargs = fn_kwargs or {}
     if not isinstance(t1, DNDarray) and not _is_scalar(t1):
-        if isinstance(t1, (list, tuple, np.ndarray, torch.Tensor)):
+        # sequences are rejected like the reference (_operations.py:65-80); NumPy arrays and torch
+        # tensors are promoted to (replicated) DNDarrays
+        if isinstance(t1, (np.ndarray, torch.Tensor)):
             from .factories import array
 
             t1 = array(t1, device=t2.device if isinstance(t2, DNDarray) else None)
         else:
             raise TypeError("Only DNDarrays and numeric scalars are supported, but input was {}".format(type(t1)))
     if not isinstance(t2, DNDarray) and not _is_scalar(t2):
-        if isinstance(t2, (list, tuple, np.ndarray, torch.Tensor)):
+        # sequences are rejected like the reference (_operations.py:65-80); NumPy arrays and torch
+        # tensors are promoted to (replicated) DNDarrays
+        if isinstance(t2, (np.ndarray, torch.Tensor)):
             from .factories import array
 
             t2 = array(t2, device=t1.device if isinstance(t1, DNDarray) else None)
