@@ -748,10 +748,31 @@ class MPICommunication(Communication):
         # RCCL has no tags: ordering per (src, dst) pair is FIFO; gloo honours them
         return int(tag) if tag is not None and tag >= 0 else 0
 
+    def _mailbox(self):
+        """Messages a rank sends to itself (MPI allows it; torch.distributed has no self-send):
+        FIFO per tag, matched by the receive when it is waited on."""
+        box = getattr(self, "_self_box", None)
+        if box is None:
+            import collections
+
+            box = self._self_box = collections.defaultdict(collections.deque)
+        return box
+
+    def _take_self(self, tag):
+        box = self._mailbox()
+        if tag is None or tag == MPI.ANY_TAG:
+            tag = next((k for k, q in box.items() if q), None)
+        if tag is None or not box[self._tag(tag)]:
+            raise RuntimeError("receive from self without a matching send posted before the wait")
+        return box[self._tag(tag)].popleft()
+
     def Isend(self, buf, dest: int, tag: int = 0) -> MPIRequest:
         t = _as_tensor(buf)
         if not isinstance(t, torch.Tensor):
             return self.isend(buf, dest, tag)
+        if dest == self.rank:
+            self._mailbox()[self._tag(tag)].append(t.clone())
+            return MPIRequest()
         src = _wire_dtype(t).contiguous()
         work = _SD.isend(src, dst=self._g(dest), group=self.group, tag=self._tag(tag))
         return MPIRequest(work, result=src)
@@ -767,6 +788,8 @@ class MPICommunication(Communication):
         if isinstance(buf, tuple):
             t = _as_tensor(buf[0])
         dst = t if (t.is_contiguous() and t.dtype != torch.bool) else torch.empty_like(_wire_dtype(t)).contiguous()
+        if source == self.rank:
+            return MPIRequest(None, lambda: t.copy_(self._take_self(tag).reshape(t.shape).to(t.dtype)))
         if source == MPI.ANY_SOURCE:
             raise NotImplementedError("ANY_SOURCE receives are not supported over RCCL; name the peer")
         work = _SD.irecv(dst, src=self._g(source), group=self.group, tag=self._tag(tag))
@@ -861,6 +884,9 @@ class MPICommunication(Communication):
         return size, payload
 
     def isend(self, obj: Any, dest: int, tag: int = 0) -> MPIRequest:
+        if dest == self.rank:
+            self._mailbox()[self._tag(tag)].append(pickle.dumps(obj))
+            return MPIRequest()
         size, payload = self._obj_to_tensor(obj)
         w1 = _SD.isend(size, dst=self._g(dest), group=self.group, tag=self._tag(tag))
         w2 = _SD.isend(payload, dst=self._g(dest), group=self.group, tag=self._tag(tag))
@@ -870,6 +896,8 @@ class MPICommunication(Communication):
         self.isend(obj, dest, tag).Wait()
 
     def recv(self, buf=None, source: int = 0, tag: int = 0, status=None) -> Any:
+        if source == self.rank:
+            return pickle.loads(self._take_self(tag))
         dev = self._obj_device()
         size = torch.empty(1, dtype=torch.int64, device=dev)
         _SD.recv(size, src=self._g(source), group=self.group, tag=self._tag(tag))
