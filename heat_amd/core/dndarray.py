@@ -478,14 +478,14 @@ class DNDarray:
 
     def redistribute_(self, lshape_map: torch.Tensor = None, target_map: torch.Tensor = None) -> None:
         """Redistribute the split axis so that rank r holds ``target_map[r, split]`` rows."""
+        if target_map is not None and not isinstance(target_map, torch.Tensor):
+            raise TypeError("target_map must be a torch.Tensor, currently {}".format(type(target_map)))
+        if lshape_map is not None and not isinstance(lshape_map, torch.Tensor):
+            raise TypeError("lshape_map must be a torch.Tensor, currently {}".format(type(lshape_map)))
         if not self.is_distributed():
             return
         if target_map is None:
             return self.balance_()
-        if not isinstance(target_map, torch.Tensor):
-            raise TypeError("target_map must be a torch.Tensor, currently {}".format(type(target_map)))
-        if lshape_map is not None and not isinstance(lshape_map, torch.Tensor):
-            raise TypeError("lshape_map must be a torch.Tensor, currently {}".format(type(lshape_map)))
         tgt = [int(x) for x in target_map[:, self.split].tolist()]
         if sum(tgt) != self.gshape[self.split]:
             raise ValueError("Sum along the split axis of the target map must be equal to the shape in that "
