@@ -154,10 +154,10 @@ def concatenate(arrays: Sequence[DNDarray], axis: int = 0) -> DNDarray:
     for a in arrays:
         if not isinstance(a, DNDarray):
             raise TypeError("All arrays must be DNDarrays, got {}".format(type(a)))
-    if len(arrays) == 1:
-        return arrays[0].copy()
     nd = arrays[0].ndim
     axis = sanitize_axis(arrays[0].gshape, axis)
+    if len(arrays) == 1:
+        return arrays[0].copy()
     for a in arrays[1:]:
         if a.ndim != nd:
             raise ValueError("DNDarrays must have the same number of dimensions")
@@ -255,7 +255,17 @@ def _at_least_2d_row(a: DNDarray) -> DNDarray:
 
 
 def vstack(arrays: Sequence[DNDarray]) -> DNDarray:
-    return concatenate([_at_least_2d_row(a) for a in arrays], axis=0)
+    """Stack row-wise; 1-D inputs become rows. A distributed 1-D input joins a row-split stack as
+    a row split along axis 0 (reference ``row_stack``: reshape to (1, n) keeping split 0)."""
+    arrays = list(arrays)
+    target = next((a.split for a in arrays if a.ndim > 1 and a.split is not None), 0)
+    rows = []
+    for a in arrays:
+        r = _at_least_2d_row(a)
+        if a.ndim == 1 and a.split is not None and r.split != target:
+            r = resplit(r, target)
+        rows.append(r)
+    return concatenate(rows, axis=0)
 
 
 row_stack = vstack
@@ -541,8 +551,13 @@ def pad(array: DNDarray, pad_width, mode: str = "constant", constant_values=0) -
     """Constant padding (NumPy ``pad_width`` conventions); the result is balanced."""
     if not isinstance(array, DNDarray):
         raise TypeError("expected array to be a ht.DNDarray, but was {}".format(type(array)))
+    if not isinstance(mode, str):
+        raise TypeError("expected mode to be a string, but was {}".format(type(mode)))
     if mode != "constant":
         raise NotImplementedError("only mode='constant' is supported, got {}".format(mode))
+    if not isinstance(pad_width, (int, tuple, list)):
+        raise TypeError("expected pad_width to be an integer or a sequence (tuple or list), but was {}".format(
+            type(pad_width)))
     nd = array.ndim
     if isinstance(pad_width, int):
         widths = [(pad_width, pad_width)] * nd

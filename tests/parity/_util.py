@@ -19,9 +19,8 @@ def raises(exc, fn, *args, **kwargs):
     except exc:
         return
     except Exception as e:  # noqa: B902 - reported
-        raise AssertionError("{} raised {} instead of {}".format(getattr(fn, "__name__", fn), type(e).__name__,
-                                                                  exc.__name__))
-    raise AssertionError("{} did not raise {}".format(getattr(fn, "__name__", fn), exc.__name__))
+        raise AssertionError("{} raised {} instead of {}".format(getattr(fn, "__name__", fn), type(e).__name__, exc))
+    raise AssertionError("{} did not raise {}".format(getattr(fn, "__name__", fn), exc))
 
 
 def close(a, expected, rtol=1e-5, atol=1e-6):
