@@ -143,6 +143,8 @@ def binary_op(operation: Callable, t1, t2, out: Optional[DNDarray] = None, where
             raise TypeError("expected out to be None or a DNDarray, but was {}".format(type(out)))
         if tuple(out.gshape) != tuple(gshape):
             raise ValueError("Expecting output buffer of shape {}, got {}".format(gshape, out.shape))
+        if out.split != split:
+            raise ValueError("Expecting output buffer with split {}, got {}".format(split, out.split))
         if where is not True and where is not None:
             w = where.larray if isinstance(where, DNDarray) else where
             out.larray.copy_(torch.where(w, result.to(out.larray.dtype), out.larray))
@@ -229,12 +231,13 @@ def reduce_op(x: DNDarray, partial_op: Callable, reduction_op: Op, axis=None, ou
         fill = neutral if neutral is not None else 0
         t = torch.full(shp, fill, dtype=t.dtype, device=t.device)
     if x.ndim == 0:
+        # a full reduction yields shape (1,) like the reference (_operations.py:416-417)
         partial = partial_op(t.reshape(1), dim=0, keepdim=False, **kwargs)
-        gshape, out_split = (), None
+        gshape, out_split = (1,), None
     else:
         partial = _reduce_local(partial_op, t, axis, keepdim, **kwargs)
         if axis is None:
-            gshape = tuple([1] * x.ndim) if keepdim else ()
+            gshape = tuple([1] * x.ndim) if keepdim else (1,)
             out_split = None
         else:
             axes = (axis,) if isinstance(axis, int) else axis
@@ -255,12 +258,18 @@ def reduce_op(x: DNDarray, partial_op: Callable, reduction_op: Op, axis=None, ou
     if isinstance(partial, tuple):
         partial = partial[0]
     partial = partial.reshape(gshape) if partial.numel() == int(np.prod(gshape)) and out_split is None else partial
+    res = DNDarray(partial, gshape, types.canonical_heat_type(partial.dtype), out_split, x.device, x.comm, balanced)
     if out is not None:
         if tuple(out.gshape) != tuple(gshape):
             raise ValueError("Expecting output buffer of shape {}, got {}".format(gshape, out.shape))
+        if out.split != out_split and x.comm.size > 1:
+            from .manipulations import resplit
+
+            res = resplit(res, out.split)
+        partial = res.larray
         out.larray = partial.to(out.larray.dtype) if out.larray.shape != partial.shape else out.larray.copy_(partial)
         return out
-    return DNDarray(partial, gshape, types.canonical_heat_type(partial.dtype), out_split, x.device, x.comm, balanced)
+    return res
 
 
 def cum_op(x: DNDarray, partial_op: Callable, exscan_op: Op, final_op: Callable, neutral, axis: int, dtype=None,

@@ -209,9 +209,13 @@ def _as_tensor(buf):
     return buf
 
 
+# dtypes neither gloo nor RCCL move: bool travels as uint8, int16 as int32 (cast back on arrival)
+_WIRE = {torch.bool: torch.uint8, torch.int16: torch.int32}
+
+
 def _wire_dtype(t: torch.Tensor) -> torch.Tensor:
-    """bool travels as uint8 (gloo has no bool reductions; RCCL handles uint8 natively)."""
-    return t.to(torch.uint8) if t.dtype == torch.bool else t
+    w = _WIRE.get(t.dtype)
+    return t.to(w) if w is not None else t
 
 
 class MPICommunication(Communication):
@@ -386,12 +390,12 @@ class MPICommunication(Communication):
             return None, None  # stream-ordered on the current stream: nothing to wait for
         native = op.torch_op is not None and t.dtype != torch.bool and (not t.is_complex() or op is MPI.SUM)
         if native:
-            contig = t if t.is_contiguous() else t.contiguous()
+            contig = _wire_dtype(t) if t.is_contiguous() else _wire_dtype(t).contiguous()
             work = _SD.all_reduce(contig, op=op.torch_op, group=self.group, async_op=True)
 
             def fin():
                 if contig is not t:
-                    t.copy_(contig)
+                    t.copy_(contig.to(t.dtype) if contig.dtype != t.dtype else contig)
 
             return work, fin
         if op in (MPI.LAND, MPI.LOR) and op.torch_op is None:
@@ -684,7 +688,7 @@ class MPICommunication(Communication):
             return None, lambda: [blk]
         ref = next((b for b in send_blocks if b is not None), None)
         dtype, device = ref.dtype, ref.device
-        wire = torch.uint8 if dtype == torch.bool else dtype
+        wire = _WIRE.get(dtype, dtype)
         in_sizes = [int(b.numel()) for b in send_blocks]
         out_sizes = [int(np.prod(s)) if len(s) else 1 for s in recv_shapes]
         flat_in = torch.cat([b.reshape(-1).to(wire) for b in send_blocks]) if sum(in_sizes) else \
@@ -787,7 +791,7 @@ class MPICommunication(Communication):
         t = _as_tensor(buf)
         if isinstance(buf, tuple):
             t = _as_tensor(buf[0])
-        dst = t if (t.is_contiguous() and t.dtype != torch.bool) else torch.empty_like(_wire_dtype(t)).contiguous()
+        dst = t if (t.is_contiguous() and t.dtype not in _WIRE) else torch.empty_like(_wire_dtype(t)).contiguous()
         if source == self.rank:
             return MPIRequest(None, lambda: t.copy_(self._take_self(tag).reshape(t.shape).to(t.dtype)))
         if source == MPI.ANY_SOURCE:
@@ -815,14 +819,14 @@ class MPICommunication(Communication):
             device = device or send.device
         if source is not None:
             dtype = dtype or torch.float32
-            wire = torch.uint8 if dtype == torch.bool else dtype
+            wire = _WIRE.get(dtype, dtype)
             out = torch.empty(tuple(recv_shape), dtype=wire, device=device)
             ops.append(dist.P2POp(dist.irecv, out, self._g(source), self.group))
         if ops:
             for w in _SD.batch_isend_irecv(ops):
                 w.wait()
-        if out is not None and dtype == torch.bool:
-            out = out.to(torch.bool)
+        if out is not None and out.dtype != dtype:
+            out = out.to(dtype)
         return out
 
     # ---------------------------------------------------------------- pickled object ops

@@ -628,7 +628,18 @@ class DNDarray:
         adv = any(isinstance(k, torch.Tensor) for k in out)
         return tuple(out), adv
 
+    def _coordinate_key(self, key):
+        """An integer DNDarray key of shape (k, ndim) - e.g. the output of :func:`nonzero` - holds
+        one element coordinate per row, like the reference (dndarray.py:694-707, 1381-1386):
+        turn it into a tuple of per-dimension index arrays."""
+        if (isinstance(key, DNDarray) and self.ndim >= 2 and key.ndim == self.ndim
+                and key.gshape[-1] == self.ndim and not types.heat_type_is_inexact(key.dtype)
+                and key.dtype is not types.bool):
+            return tuple(key[:, i] for i in range(self.ndim))
+        return key
+
     def __getitem__(self, key) -> "DNDarray":
+        key = self._coordinate_key(key)
         # full boolean mask with matching distribution: purely local, result split 0 (unbalanced)
         if isinstance(key, DNDarray) and key.dtype is types.bool and key.gshape == self.gshape:
             if key.split == self.split or not self.is_distributed():
@@ -904,6 +915,7 @@ class DNDarray:
         the selection: each rank fetches exactly the part it writes (owner-computes request/reply),
         after at most one all-to-all resplit of the value (reference dndarray.py:1334-1549
         redistributes the value with point-to-point chains instead)."""
+        key = self._coordinate_key(key)
         value_d = value if isinstance(value, DNDarray) and value.is_distributed() else None
         if isinstance(value, DNDarray):
             vt = None if value_d is not None else value.larray

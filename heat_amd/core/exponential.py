@@ -58,7 +58,7 @@ def sqrt(x, out=None) -> DNDarray:
 
 
 def square(x, out=None) -> DNDarray:
-    return _operations.local_op(torch.square, x, out, no_cast=True)
+    return _operations.local_op(torch.square, x, out)
 
 
 for _n in ("exp", "expm1", "exp2", "log", "log2", "log10", "log1p", "sqrt", "square"):

@@ -96,9 +96,10 @@ def array(obj, dtype=None, copy: bool = True, ndmin: int = 0, order: str = "C", 
         obj.device if isinstance(obj, torch.Tensor) else devices.get_device().torch_device)
 
     if isinstance(obj, torch.Tensor):
-        t = obj.detach()
+        t = obj.detach() if obj.requires_grad else obj
         t = t.to(device=tdev, dtype=dtype.torch_type() if dtype is not None else t.dtype)
-        if copy and t is obj:
+        if copy and t.numel() and t.data_ptr() == obj.data_ptr():
+            # copy=True never aliases the caller's tensor (copy=False keeps the very object)
             t = t.clone()
     else:
         if isinstance(obj, np.ndarray):
@@ -234,6 +235,10 @@ def ones_like(a, dtype=None, split=None, device=None, comm=None, order="C") -> D
 
 
 def full(shape, fill_value, dtype=types.float32, split=None, device=None, comm=None, order="C") -> DNDarray:
+    if isinstance(fill_value, complex) and not types.heat_type_is_complexfloating(types.canonical_heat_type(dtype)):
+        # a complex fill value makes the default (real) dtype complex, like the reference
+        dtype = types.complex64 if types.canonical_heat_type(dtype) is not types.float64 else types.complex128
+
     def local_factory(lshape, dtype, device):
         return torch.full(lshape, fill_value, dtype=dtype, device=device)
 
@@ -250,6 +255,10 @@ def eye(shape, dtype=types.float32, split=None, device=None, comm=None, order="C
         gshape = (shape, shape)
     else:
         gshape = tuple(shape) if len(shape) > 1 else (shape[0], shape[0])
+    if not all(isinstance(n, (int, np.integer)) for n in gshape):
+        raise TypeError("eye shape must be an int or a tuple of ints, got {}".format(shape))
+    if any(n < 0 for n in gshape):
+        raise ValueError("negative dimensions are not allowed: {}".format(gshape))
     split = sanitize_axis(gshape, split)
     device = devices.sanitize_device(device)
     comm = sanitize_comm(comm)

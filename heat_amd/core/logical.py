@@ -4,6 +4,7 @@ from __future__ import annotations
 
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _operations, types
@@ -48,13 +49,20 @@ def isclose(x, y, rtol: float = 1e-05, atol: float = 1e-08, equal_nan: bool = Fa
             a, b = a.to(common), b.to(common)
         return torch.isclose(a, b, rtol=rtol, atol=atol, equal_nan=equal_nan)
 
+    for v in (x, y):
+        if not isinstance(v, (DNDarray, int, float, bool, np.number)):
+            raise TypeError("Only DNDarrays and numeric scalars are supported, got {}".format(type(v)))
     if not isinstance(x, DNDarray) and not isinstance(y, DNDarray):
-        raise TypeError("Expected at least one DNDarray")
+        # two scalars: a plain bool like the reference
+        return bool(abs(x - y) <= atol + rtol * abs(y) or (equal_nan and x != x and y != y))
     return _operations.binary_op(_isclose, x, y)
 
 
 def allclose(x, y, rtol: float = 1e-05, atol: float = 1e-08, equal_nan: bool = False) -> bool:
     """True when every element pair is close (one all-reduce of a boolean)."""
+    for v in (x, y):
+        if not isinstance(v, (DNDarray, int, float, bool, np.number)):
+            raise TypeError("Only DNDarrays and numeric scalars are supported, got {}".format(type(v)))
     if not isinstance(x, DNDarray):
         x = _as_array(x, y)
     if not isinstance(y, DNDarray):

@@ -11,8 +11,8 @@ __all__ = ["abs", "absolute", "ceil", "clip", "fabs", "floor", "modf", "round", 
 
 def abs(x, out=None, dtype=None) -> DNDarray:
     """Element-wise absolute value (optionally cast to ``dtype``)."""
-    if dtype is not None and not issubclass(types.canonical_heat_type(dtype), types.datatype):
-        raise TypeError("dtype must be a heat data type")
+    if dtype is not None and not (isinstance(dtype, type) and issubclass(dtype, types.datatype)):
+        raise TypeError("dtype must be a heat data type, got {}".format(dtype))
     res = _operations.local_op(torch.abs, x, out, no_cast=True)
     if dtype is not None:
         res = res.astype(dtype, copy=False)
@@ -24,6 +24,8 @@ absolute = abs
 
 def fabs(x, out=None) -> DNDarray:
     """Absolute value as floating point."""
+    if not isinstance(x, DNDarray):
+        raise TypeError("expected x to be a DNDarray, but was {}".format(type(x)))
     return abs(x, out, dtype=None if types.heat_type_is_inexact(x.dtype) else types.promote_types(x.dtype, types.float32))
 
 
@@ -41,8 +43,8 @@ def trunc(x, out=None) -> DNDarray:
 
 def round(x, decimals: int = 0, out=None, dtype=None) -> DNDarray:
     """Round half to even to the given number of decimals."""
-    if dtype is not None and not issubclass(types.canonical_heat_type(dtype), types.datatype):
-        raise TypeError("dtype must be a heat data type")
+    if dtype is not None and not (isinstance(dtype, type) and issubclass(dtype, types.datatype)):
+        raise TypeError("dtype must be a heat data type, got {}".format(dtype))
 
     def _round(t, decimals=decimals):
         if decimals == 0:
@@ -73,8 +75,12 @@ def modf(x, out=None):
     integral = trunc(x)
     fractional = x - integral
     if out is not None:
-        if not isinstance(out, tuple) or len(out) != 2:
-            raise TypeError("expected out to be None or a tuple of two DNDarrays")
+        if not isinstance(out, tuple):
+            raise TypeError("expected out to be None or a tuple of two DNDarrays, got {}".format(type(out)))
+        if len(out) != 2:
+            raise ValueError("expected out to be a tuple of two DNDarrays, got {} entries".format(len(out)))
+        if not all(isinstance(o, DNDarray) for o in out):
+            raise TypeError("expected out to hold two DNDarrays")
         out[0].larray.copy_(fractional.larray)
         out[1].larray.copy_(integral.larray)
         return out

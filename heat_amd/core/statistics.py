@@ -12,6 +12,7 @@ the custom ``MPI_ARGMAX`` callbacks (``statistics.py:1139-1207``).
 """
 from __future__ import annotations
 
+from builtins import max as _bmax
 from typing import Optional, Tuple, Union
 
 import numpy as np
@@ -90,14 +91,36 @@ def _wrap(x: DNDarray, t: torch.Tensor, gshape, split, balanced, dtype=None):
     return DNDarray(t.to(dtype.torch_type()), tuple(gshape), dtype, split, x.device, x.comm, balanced)
 
 
+def _moment_axis(x: DNDarray, axis):
+    """Validate a mean/var axis like the reference (statistics.py:853-866): a str axis is a
+    TypeError; tuples/lists with non-int or repeated entries, tensors and out-of-range axes are
+    ValueErrors."""
+    if axis is None:
+        return None
+    if isinstance(axis, torch.Tensor):
+        raise ValueError("axis must be None, an int or a tuple of ints, not a tensor")
+    if isinstance(axis, (list, tuple)):
+        if not all(isinstance(a, (int, np.integer)) and not isinstance(a, bool) for a in axis):
+            raise ValueError("axis entries must be ints, got {}".format(axis))
+        axis = tuple(int(a) for a in axis)
+        if len(set(a % _bmax(1, x.ndim) if -x.ndim <= a < x.ndim else a for a in axis)) != len(axis):
+            raise ValueError("repeated axis in {}".format(axis))
+        for a in axis:
+            if not -x.ndim <= a < _bmax(1, x.ndim):
+                raise ValueError("axis {} is out of bounds for {} dimensions".format(a, x.ndim))
+        return axis
+    if not isinstance(axis, (int, np.integer)) or isinstance(axis, bool):
+        raise TypeError("axis must be None, int or tuple, but was {}".format(type(axis)))
+    if not -x.ndim <= axis < _bmax(1, x.ndim):
+        raise ValueError("axis {} is out of bounds for {} dimensions".format(axis, x.ndim))
+    return int(axis)
+
+
 def mean(x: DNDarray, axis=None) -> DNDarray:
     """Arithmetic mean (single pass + one all-gather of (n, mean, M2) triples when split)."""
     if not isinstance(x, DNDarray):
         raise TypeError("expected x to be a ht.DNDarray, but was {}".format(type(x)))
-    if axis is not None and not isinstance(axis, (int, tuple, list, np.integer)):
-        raise TypeError("axis must be None, int or tuple, but was {}".format(type(axis)))
-    if isinstance(axis, list):
-        axis = tuple(axis)
+    axis = _moment_axis(x, axis)
     if types.heat_type_is_complexfloating(x.dtype):
         from . import arithmetics
 
@@ -114,14 +137,13 @@ def var(x: DNDarray, axis=None, ddof: int = 0, **kwargs) -> DNDarray:
         raise TypeError("expected x to be a ht.DNDarray, but was {}".format(type(x)))
     if "bessel" in kwargs:
         ddof = 1 if kwargs["bessel"] else 0
-    if not isinstance(ddof, int):
+    if not isinstance(ddof, (int, np.integer)) or isinstance(ddof, bool):
         raise TypeError("ddof must be an integer, got {}".format(type(ddof)))
-    if ddof not in (0, 1):
+    if ddof < 0:
+        raise ValueError("ddof must be non-negative, got {}".format(ddof))
+    if ddof > 1:
         raise NotImplementedError("only ddof 0 and 1 are supported, got {}".format(ddof))
-    if axis is not None and not isinstance(axis, (int, tuple, list, np.integer)):
-        raise TypeError("axis must be None, int or tuple, but was {}".format(type(axis)))
-    if isinstance(axis, list):
-        axis = tuple(axis)
+    axis = _moment_axis(x, axis)
     n, mu, m2, gshape, split, bal = _moments(x, axis)
     v = m2 / (n - ddof)
     return _wrap(x, v, gshape, split, bal, _result_dtype(x))
@@ -136,6 +158,9 @@ def std(x: DNDarray, axis=None, ddof: int = 0, **kwargs) -> DNDarray:
 
 def _central_moment_sums(x: DNDarray, axis, powers=(2, 3, 4)):
     """Two-pass central moments: global mean, then sums of (x - mean)^k (one all-reduce)."""
+    if axis is not None and (not isinstance(axis, (int, np.integer)) or isinstance(axis, bool)):
+        raise TypeError("axis must be None or an int, got {}".format(type(axis)))
+    sanitize_axis(x.gshape, axis)
     mu = mean(x, axis)
     t = x.larray.double()
     axis_s = sanitize_axis(x.gshape, axis)
@@ -233,6 +258,8 @@ def _argext(x: DNDarray, axis, out, largest: bool, keepdim: bool = False):
     if axis is not None and not isinstance(axis, (int, np.integer)):
         raise TypeError("axis must be None or an int, but was {}".format(type(axis)))
     axis = sanitize_axis(x.gshape, axis)
+    if out is not None and (not isinstance(out, DNDarray) or out.dtype is not types.int64):
+        raise TypeError("out must be an int64 DNDarray, got {}".format(getattr(out, "dtype", type(out))))
     t = x.larray
     fn = torch.argmax if largest else torch.argmin
     if t.is_cuda and x.gnumel and ops.argreduce_supported(t, x.gnumel if axis is None else x.gshape[axis]):
@@ -266,7 +293,7 @@ def _argext(x: DNDarray, axis, out, largest: bool, keepdim: bool = False):
             res = torch.tensor(int(best[1]), dtype=torch.int64, device=t.device)
         else:
             res = fn(t.reshape(-1))
-        gshape = (1,) * x.ndim if keepdim else ()
+        gshape = (1,) * x.ndim if keepdim else (1,)
         res = res.reshape(gshape)
         r = DNDarray(res, gshape, types.int64, None, x.device, x.comm, True)
     elif x.is_distributed() and axis == x.split:
@@ -298,10 +325,10 @@ def _argext(x: DNDarray, axis, out, largest: bool, keepdim: bool = False):
             split = x.split
         else:
             gshape = tuple(s for i, s in enumerate(x.gshape) if i != axis)
-            split = None if x.split is None else (x.split if x.split < axis else x.split - 1)
+            split = None if x.split in (None, axis) else (x.split if x.split < axis else x.split - 1)
         r = DNDarray(res, gshape, types.int64, split, x.device, x.comm, x.balanced)
     if out is not None:
-        out.larray = r.larray.to(out.larray.dtype)
+        out.larray = r.larray
         return out
     return r
 
@@ -318,7 +345,7 @@ def _argext_native(x: DNDarray, axis, largest: bool, keepdim: bool) -> DNDarray:
                                    x.split if dist_split else None)
         if dist_split:
             x.comm.Allreduce(MPI.IN_PLACE, keys, MPI.MAX)
-        gshape = (1,) * x.ndim if keepdim else ()
+        gshape = (1,) * x.ndim if keepdim else (1,)
         res = ops.argreduce_decode(keys).reshape(gshape)
         return DNDarray(res, gshape, types.int64, None, x.device, x.comm, True)
     along_split = dist_split and axis == x.split
@@ -354,6 +381,8 @@ def average(x: DNDarray, axis=None, weights: Optional[DNDarray] = None, returned
     """Weighted average along ``axis``."""
     from . import arithmetics
 
+    if not isinstance(x, DNDarray):
+        raise TypeError("expected x to be a ht.DNDarray, but was {}".format(type(x)))
     if weights is None:
         result = mean(x, axis)
         if returned:
@@ -361,7 +390,7 @@ def average(x: DNDarray, axis=None, weights: Optional[DNDarray] = None, returned
             return result, factories.full_like(result, cnt)
         return result
     if not isinstance(weights, DNDarray):
-        weights = factories.array(weights, device=x.device, comm=x.comm)
+        raise TypeError("weights must be a DNDarray, got {}".format(type(weights)))
     if weights.gshape != x.gshape:
         if axis is None:
             raise TypeError("Axis must be specified when shapes of x and weights differ.")
@@ -381,6 +410,9 @@ def average(x: DNDarray, axis=None, weights: Optional[DNDarray] = None, returned
         if wsplit is not None:
             w = resplit(w, axis)
     else:
+        if weights.split != x.split:
+            raise NotImplementedError("weights of x's shape must have x's split {}, got {}".format(
+                x.split, weights.split))
         w = weights
     wsum = arithmetics.sum(w, axis=axis) if w.gshape == x.gshape else None
     num = arithmetics.sum(x * w, axis=axis)
@@ -422,7 +454,9 @@ def bincount(x: DNDarray, weights: Optional[DNDarray] = None, minlength: int = 0
         w = weights.larray.reshape(-1)
         if weights.split != x.split:
             raise ValueError("weights and x must have the same split")
-    counts = torch.bincount(t, weights=w, minlength=length)
+    counts = torch.bincount(t, weights=None if w is None else w.to(torch.float64), minlength=length)
+    # an empty local block must agree with the others on dtype (float64 with weights, like NumPy)
+    counts = counts.to(torch.int64 if w is None else torch.float64)
     if x.is_distributed():
         counts = counts.contiguous()
         x.comm.Allreduce(MPI.IN_PLACE, counts, MPI.SUM)
@@ -490,6 +524,12 @@ def percentile(x: DNDarray, q, axis: Optional[int] = None, out: Optional[DNDarra
     """q-th percentile(s) along ``axis`` (distributed sort along the split axis)."""
     from .manipulations import flatten, sort
 
+    if not isinstance(x, DNDarray):
+        raise TypeError("expected x to be a ht.DNDarray, but was {}".format(type(x)))
+    if isinstance(q, np.ndarray):
+        raise TypeError("q must be a scalar, list, tuple or DNDarray, got a NumPy array")
+    if out is not None and not isinstance(out, DNDarray):
+        raise TypeError("out must be a DNDarray, got {}".format(type(out)))
     if interpolation not in ("linear", "lower", "higher", "midpoint", "nearest"):
         raise ValueError("Invalid interpolation method {}".format(interpolation))
     scalar_q = np.isscalar(q) or (isinstance(q, DNDarray) and q.ndim == 0)
@@ -529,6 +569,10 @@ def percentile(x: DNDarray, q, axis: Optional[int] = None, out: Optional[DNDarra
         for lo, hi, frac in positions:
             lo_v = picked.narrow(ax, where[lo], 1).squeeze(ax).to(tdt)
             hi_v = picked.narrow(ax, where[hi], 1).squeeze(ax).to(tdt)
+            if interpolation == "nearest":
+                # NumPy rounds a half position to the even index
+                res.append(hi_v if frac > 0.5 or (frac == 0.5 and hi % 2 == 0) else lo_v)
+                continue
             res.append(_interp(lo_v, hi_v, torch.tensor(frac, dtype=tdt, device=lo_v.device), interpolation))
         r = torch.stack(res)
         split = None
@@ -556,6 +600,12 @@ def percentile(x: DNDarray, q, axis: Optional[int] = None, out: Optional[DNDarra
     res = DNDarray(r.to(rdtype.torch_type()).contiguous(), gshape, rdtype, split, x.device, x.comm,
                    True if split is None else src.balanced)
     if out is not None:
+        if out.dtype is not rdtype:
+            raise TypeError("out must have dtype {}, got {}".format(rdtype, out.dtype))
+        if tuple(out.gshape) != tuple(gshape):
+            raise ValueError("out must have shape {}, got {}".format(gshape, out.gshape))
+        if out.split != split:
+            raise ValueError("out must have split {}, got {}".format(split, out.split))
         out.larray = res.larray
         return out
     return res
@@ -573,33 +623,33 @@ def cov(m: DNDarray, y: Optional[DNDarray] = None, rowvar: bool = True, bias: bo
     from .linalg.basics import matmul, transpose
     from .manipulations import concatenate
 
+    from .manipulations import expand_dims
+
     if ddof is not None and not isinstance(ddof, int):
         raise TypeError("ddof must be integer")
     if not isinstance(m, DNDarray):
         raise TypeError("m must be a DNDarray")
+    if y is not None and not isinstance(y, DNDarray):
+        raise TypeError("y must be None or a DNDarray")
     if m.ndim > 2:
         raise ValueError("m has more than 2 dimensions")
-    if m.ndim == 1:
-        from .manipulations import expand_dims
-
-        m = expand_dims(m, 0)
-        rowvar = True
-    x = m if rowvar else transpose(m)
+    if y is not None and y.ndim > 2:
+        raise ValueError("y has more than 2 dimensions")
+    # NumPy semantics: a 1-D m or y is one variable (a row), whatever rowvar says
+    x = expand_dims(m, 0) if m.ndim == 1 else (m if rowvar or m.gshape[0] == 1 else transpose(m))
     if y is not None:
-        if y.ndim == 1:
-            from .manipulations import expand_dims
-
-            y = expand_dims(y, 0)
-        yy = y if rowvar or y.gshape[0] == 1 else transpose(y)
+        yy = expand_dims(y, 0) if y.ndim == 1 else (y if rowvar or y.gshape[0] == 1 else transpose(y))
+        if yy.gshape[1] != x.gshape[1]:
+            raise RuntimeError("m and y must have the same number of observations")
         x = concatenate([x, yy], axis=0)
     if not types.heat_type_is_inexact(x.dtype):
         x = x.astype(types.float64)
     if ddof is None:
         ddof = 0 if bias else 1
     n = x.gshape[1]
+    if ddof > n:
+        raise ValueError("ddof {} must not exceed the number of observations {}".format(ddof, n))
     avg = mean(x, axis=1)
-    from .manipulations import expand_dims
-
     xc = x - expand_dims(avg, 1)
     c = matmul(xc, transpose(xc))
     c = c / float(n - ddof)

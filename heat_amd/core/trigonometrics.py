@@ -40,10 +40,11 @@ rad2deg = degrees = _u(torch.rad2deg)
 def arctan2(x1, x2, out=None) -> DNDarray:
     """Element-wise arc tangent of x1/x2 choosing the quadrant correctly."""
     def _atan2(a, b):
+        # exact types promote like the reference's local ops: int64 -> float64, others -> float32
         if not a.is_floating_point():
-            a = a.float()
+            a = a.double() if a.dtype == torch.int64 else a.float()
         if not b.is_floating_point():
-            b = b.float()
+            b = b.double() if b.dtype == torch.int64 else b.float()
         return torch.atan2(a, b)
 
     return _operations.binary_op(_atan2, x1, x2, out)

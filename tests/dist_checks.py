@@ -20,6 +20,10 @@ def _rng(seed=0):
 def assert_array_equal(a: ht.DNDarray, expected, rtol=1e-5, atol=1e-6, check_split_chunks=True):
     """Global shape + local chunk + values (after gathering) against a NumPy array."""
     expected = np.asarray(expected)
+    if expected.shape == () and tuple(a.gshape) == (1,):
+        # full reductions (sum/prod/min/max/argmin/any/...) have shape (1,) like the reference's
+        # (_operations.py:416-417), where NumPy returns a scalar
+        expected = expected.reshape(1)
     assert tuple(a.gshape) == tuple(expected.shape), "shape {} != {}".format(a.gshape, expected.shape)
     if check_split_chunks and a.split is not None and a.balanced:
         _, lshape, _ = a.comm.chunk(a.gshape, a.split)

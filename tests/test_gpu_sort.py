@@ -58,7 +58,8 @@ def test_ht_sort_uses_radix(gpu):
     import heat_amd as ht
     from heat_amd import ops
 
-    assert ops.radix_sort_supported(torch.zeros(5000, 7, device="cuda"), 0)
+    assert ops.radix_sort_supported(torch.zeros(5000, 16, device="cuda"), 0)
+    assert ops.radix_sort_supported(torch.zeros(16, 5000, device="cuda"), 1)
 
     a = np.random.default_rng(3).standard_normal((5000, 7)).astype(np.float32)
     for axis in (0, 1):
