@@ -44,10 +44,9 @@ def transpose(a: DNDarray, axes: Optional[List[int]] = None) -> DNDarray:
     if axes is None:
         axes = list(reversed(range(nd)))
     else:
-        try:
-            axes = list(axes)
-        except TypeError:
-            raise ValueError("axes must be an iterable containing ints")
+        if isinstance(axes, str) or not hasattr(axes, "__iter__"):
+            raise TypeError("axes must be an iterable containing ints, got {}".format(type(axes)))
+        axes = list(axes)
         if len(axes) != nd:
             raise ValueError("axes do not match tensor shape")
         for i, ax in enumerate(axes):
@@ -166,6 +165,29 @@ def _stream_panels(x: DNDarray, comm) -> bool:
     return comm.size > 1 and x.gnumel * x.larray.element_size() >= _RING_MIN_BYTES
 
 
+def _batched_matmul(a: DNDarray, b: DNDarray) -> DNDarray:
+    """Stacks of matrices (an extension: the reference's matmul is 2-D only). The batch
+    dimensions must match; a split along a batch dimension stays local (one batched GEMM per
+    rank), a split matrix dimension is replicated first."""
+    from ..manipulations import resplit
+
+    if a.ndim != b.ndim or a.gshape[:-2] != b.gshape[:-2]:
+        raise ValueError("batched matmul needs equal batch dimensions, got {} and {}".format(a.gshape, b.gshape))
+    if a.gshape[-1] != b.gshape[-2]:
+        raise ValueError("If the last dimension of a ({}) is not the same size as the second-to-last dimension "
+                         "of b. ({})".format(a.gshape[-1], b.gshape[-2]))
+    nb = a.ndim - 2
+    split = a.split if a.split is not None and a.split < nb else (b.split if b.split is not None and b.split < nb
+                                                                   else None)
+    a = a if a.split == split else resplit(a, split)
+    b = b if b.split == split else resplit(b, split)
+    c_type = types.promote_types(a.dtype, b.dtype)
+    tt = c_type.torch_type()
+    res = torch.matmul(a.larray.to(tt), b.larray.to(tt))
+    gshape = a.gshape[:-1] + (b.gshape[-1],)
+    return DNDarray(res, gshape, c_type, split, a.device, a.comm, a.balanced if split is not None else True)
+
+
 def matmul(a: DNDarray, b: DNDarray, allow_resplit: bool = False) -> DNDarray:
     """Matrix product ``a @ b`` of 1-D/2-D DNDarrays with the reference's split rules.
 
@@ -176,6 +198,8 @@ def matmul(a: DNDarray, b: DNDarray, allow_resplit: bool = False) -> DNDarray:
     plus one reduce-scatter."""
     if not isinstance(a, DNDarray) or not isinstance(b, DNDarray):
         raise TypeError("matmul requires two DNDarrays")
+    if a.ndim > 2 or b.ndim > 2:
+        return _batched_matmul(a, b)
     if a.gshape[-1] != b.gshape[0]:
         raise ValueError("If the last dimension of a ({}) is not the same size as the second-to-last dimension "
                          "of b. ({})".format(a.gshape[-1], b.gshape[-2] if b.ndim > 1 else b.gshape[0]))
@@ -360,10 +384,11 @@ DNDarray.dot = lambda self, b, out=None: dot(self, b, out)
 def outer(a: DNDarray, b: DNDarray, out: Optional[DNDarray] = None, split: Optional[int] = None) -> DNDarray:
     """Outer product of two vectors (one all-gather of the other operand instead of a ring)."""
     if not isinstance(a, DNDarray) or not isinstance(b, DNDarray):
-        from .. import factories as f
-
-        a = a if isinstance(a, DNDarray) else f.array(a)
-        b = b if isinstance(b, DNDarray) else f.array(b)
+        raise TypeError("a and b must be DNDarrays, got {} and {}".format(type(a), type(b)))
+    if a.ndim == 0 or b.ndim == 0:
+        raise RuntimeError("outer requires arrays of at least one dimension")
+    if out is not None and not isinstance(out, DNDarray):
+        raise TypeError("out must be a DNDarray, got {}".format(type(out)))
     if a.ndim > 1:
         a = a.flatten()
     if b.ndim > 1:
@@ -392,7 +417,15 @@ def outer(a: DNDarray, b: DNDarray, out: Optional[DNDarray] = None, split: Optio
         out_arr = DNDarray(torch.outer(fa, lb), gshape, dtype, 1, a.device, comm,
                            b.balanced if b.split == 0 else True)
     if out is not None:
-        out.larray = out_arr.larray
+        if out.gshape != out_arr.gshape:
+            raise ValueError("out must have shape {}, got {}".format(out_arr.gshape, out.gshape))
+        if split is not None and out.split != split:
+            raise ValueError("out must have split {}, got {}".format(split, out.split))
+        if out.split != out_arr.split:
+            from ..manipulations import resplit
+
+            out_arr = resplit(out_arr, out.split)
+        out.larray = out_arr.larray.to(out.larray.dtype)
         return out
     return out_arr
 
@@ -417,12 +450,25 @@ def trace(a: DNDarray, offset: int = 0, axis1: int = 0, axis2: int = 1, dtype=No
             raise TypeError("`a` must be a DNDarray, list or tuple, is {}".format(type(a)))
     if a.ndim < 2:
         raise ValueError("`a` must contain at least 2 dimensions")
+    for v, name in ((axis1, "axis1"), (axis2, "axis2"), (offset, "offset")):
+        if not isinstance(v, (int, np.integer)) or isinstance(v, bool):
+            raise TypeError("{} must be an integer, got {}".format(name, type(v)))
+    if out is not None and not isinstance(out, DNDarray):
+        raise TypeError("out must be a DNDarray, got {}".format(type(out)))
+    if isinstance(dtype, str):
+        raise ValueError("dtype must be a heat or torch type, not the string {!r}".format(dtype))
     d = manipulations.diagonal(a, offset=offset, dim1=axis1, dim2=axis2)
     if dtype is not None:
         d = d.astype(dtype)
     s = arithmetics.sum(d, axis=-1)
     if out is not None:
-        out.larray = s.larray
+        if a.ndim == 2:
+            raise ValueError("the trace of a 2-D array is a scalar: out= is only for n-D input")
+        if out.gshape != s.gshape:
+            raise ValueError("out must have shape {}, got {}".format(s.gshape, out.gshape))
+        if out.split != s.split:
+            s = manipulations.resplit(s, out.split)
+        out.larray = s.larray.to(out.larray.dtype)
         return out
     if a.ndim == 2:
         return s.item()
@@ -508,6 +554,10 @@ def vector_norm(x: DNDarray, axis=None, keepdims: bool = False, ord=None) -> DND
     if ord == 0:
         return arithmetics.sum(xa != 0, axis=ax, keepdim=keepdims).astype(xa.dtype)
     if ord is None or ord == 2:
+        if types.heat_type_is_complexfloating(x.dtype):
+            # |z|^2 = re^2 + im^2 without the rounding of a sqrt followed by a square
+            sq = _operations.local_op(lambda t: torch.view_as_real(t).square().sum(-1), x, no_cast=True)
+            return exponential.sqrt(arithmetics.sum(sq, axis=ax, keepdim=keepdims))
         return exponential.sqrt(arithmetics.sum(xa * xa, axis=ax, keepdim=keepdims))
     if ord == 1:
         return arithmetics.sum(xa, axis=ax, keepdim=keepdims)
@@ -521,7 +571,9 @@ def matrix_norm(x: DNDarray, axis: Optional[Tuple[int, int]] = None, keepdims: b
     if x.ndim < 2:
         raise ValueError("Input must be a matrix (ndim >= 2)")
     if axis is None:
-        axis = (x.ndim - 2, x.ndim - 1)
+        if x.ndim > 2:
+            raise ValueError("axis must be given for arrays of more than 2 dimensions")
+        axis = (0, 1)
     if not isinstance(axis, (tuple, list)) or len(axis) != 2:
         raise TypeError("axis must be a 2-tuple")
     row, col = sanitize_axis(x.gshape, tuple(axis))

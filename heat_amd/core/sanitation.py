@@ -60,7 +60,11 @@ def sanitize_out(out: Any, output_shape: Tuple, output_split: int, output_device
         raise ValueError("Expecting output buffer of shape {}, got {}".format(output_shape, out.shape))
     if out.split != output_split:
         raise ValueError("Split axis of output buffer is inconsistent with split semantics (see documentation).")
-    if out.device != output_device:
+    if output_device is not None:
+        from .devices import sanitize_device
+
+        output_device = sanitize_device(output_device)
+    if output_device is not None and out.device != output_device:
         raise ValueError("Device mismatch: out is on {}, should be on {}".format(out.device, output_device))
 
 
