@@ -207,6 +207,8 @@ def load_hdf5(path: str, dataset: str, dtype=types.float32, load_fraction: float
         raise TypeError("path must be str, not {}".format(type(path)))
     if not isinstance(dataset, str):
         raise TypeError("dataset must be str, not {}".format(type(dataset)))
+    if split is not None and (not isinstance(split, int) or isinstance(split, bool)):
+        raise TypeError("split must be None or an int, not {}".format(type(split)))
     if not isinstance(load_fraction, float):
         raise TypeError("load_fraction must be float, but is {}".format(type(load_fraction)))
     if load_fraction <= 0.0 or load_fraction > 1.0:
@@ -216,7 +218,10 @@ def load_hdf5(path: str, dataset: str, dtype=types.float32, load_fraction: float
     htype = types.canonical_heat_type(dtype)
     handle = h5py.File(path, "r") if h5py is not None else _h5lite.open_file(path)
     try:
-        data = handle[dataset]
+        try:
+            data = handle[dataset]
+        except KeyError:
+            raise IOError("no dataset {!r} in {}".format(dataset, path)) from None
         gshape = list(data.shape)
         if split is not None:
             split = sanitize_axis(tuple(gshape), split)
@@ -327,9 +332,22 @@ def load_netcdf(path: str, variable: str, dtype=types.float32, split: Optional[i
         raise TypeError("path must be str, not {}".format(type(path)))
     if not isinstance(variable, str):
         raise TypeError("dataset must be str, not {}".format(type(variable)))
+    if split is not None and (not isinstance(split, int) or isinstance(split, bool)):
+        raise TypeError("split must be None or an int, not {}".format(type(split)))
     comm = sanitize_comm(comm)
     device = devices.sanitize_device(device)
     htype = types.canonical_heat_type(dtype)
+    try:
+        local, gshape, split = _nc_read_local(path, variable, split, comm)
+    except KeyError:
+        raise IOError("no variable {!r} in {}".format(variable, path)) from None
+    t = torch.from_numpy(np.ascontiguousarray(local).astype(local.dtype.newbyteorder("=")))
+    t = t.to(device=device.torch_device, dtype=htype.torch_type())
+    return DNDarray(t, gshape, htype, split, device, comm, True)
+
+
+def _nc_read_local(path: str, variable: str, split, comm):
+    """This rank's hyperslab of a netCDF variable: (numpy block, global shape, split)."""
     if nc is not None:
         with nc.Dataset(path, "r") as handle:
             data = handle[variable]
@@ -351,9 +369,7 @@ def load_netcdf(path: str, variable: str, dtype=types.float32, split: Optional[i
             split = sanitize_axis(gshape, split)
             local = np.array(data[_hyperslab(gshape, split, comm)])
             del data  # the mmap must not be referenced when the file closes
-    t = torch.from_numpy(np.ascontiguousarray(local).astype(local.dtype.newbyteorder("=")))
-    t = t.to(device=device.torch_device, dtype=htype.torch_type())
-    return DNDarray(t, gshape, htype, split, device, comm, True)
+    return local, gshape, split
 
 
 _NC_TYPES = {1: np.dtype("i1"), 2: np.dtype("S1"), 3: np.dtype(">i2"), 4: np.dtype(">i4"), 5: np.dtype(">f4"),

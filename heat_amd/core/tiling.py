@@ -5,7 +5,8 @@ Tile views of DNDarrays (reference ``heat/core/tiling.py``: ``SplitTiles`` 14, `
 ``SplitTiles`` divides EVERY dimension like the split axis would be divided (the chunking rule),
 so tile (i, j, ...) of a split array lives on the rank owning block i of the split axis. It is the
 tile grid behind resplit. ``SquareDiagTiles`` provides square diagonal tiles for tiled matrix
-algorithms; QR in this framework is TSQR and does not need it, the class is kept for API parity.
+algorithms (tile bookkeeping with the reference's boundaries: ``tiles_per_proc`` tiles per rank
+along the split axis, the other axis cut at the same indices).
 """
 from __future__ import annotations
 
@@ -255,4 +256,29 @@ class SquareDiagTiles:
         if t is not None:
             t[...] = value
 
-    local_set = __setitem__
+    def local_set(self, key, value):
+        """Set the part of tile ``key`` (local tile coordinates) this rank holds."""
+        self[self.local_to_global(key, self.__DNDarray.comm.rank)] = value
+
+    def local_to_global(self, key, rank: int) -> Tuple[int, int]:
+        """Global tile coordinates of the local tile ``key = (row, col)`` of ``rank``: the tile
+        index along the split axis is offset by the tiles of the lower ranks."""
+        i, j = key
+        arr = self.__DNDarray
+        if arr.split is None:
+            return i, j
+        off = sum(self.__tiles_per_proc[:rank])
+        return (i + off, j) if arr.split == 0 else (i, j + off)
+
+    def match_tiles(self, tiles_to_match: "SquareDiagTiles") -> None:
+        """Adopt the row boundaries of ``tiles_to_match`` (e.g. Q matching R in a tiled QR): the
+        rows of this array are cut where the other array's rows are cut."""
+        if not isinstance(tiles_to_match, SquareDiagTiles):
+            raise TypeError("tiles_to_match must be a SquareDiagTiles, got {}".format(type(tiles_to_match)))
+        n = self.__DNDarray.gshape[0]
+        rows = [r for r in tiles_to_match.row_indices if r < n] or [0]
+        self.__row_inds = rows
+        if self.__DNDarray.split == 0:
+            ends = [0] + torch.cumsum(self.__lshape_map[:, 0], 0).tolist()
+            self.__tiles_per_proc = [len([r for r in rows if ends[q] <= r < ends[q + 1]])
+                                     for q in range(len(ends) - 1)]

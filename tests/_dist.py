@@ -58,7 +58,16 @@ def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None
 def run_distributed_batch(module: str, names, nprocs: int, timeout: int = 1200, env_extra=None,
                           keep_gpu: bool = False):
     """Run the check functions ``names`` of ``module`` in one job of ``nprocs`` ranks; returns
-    {name: (ok, error)} (checks missing from the report - a job that died - count as failed)."""
+    {name: (ok, error)} (checks missing from the report - a job that died - count as failed).
+    A job whose rendezvous port was taken by a concurrent job (pytest -n) is started again."""
+    for attempt in range(3):
+        res = _run_batch_once(module, names, nprocs, timeout, env_extra, keep_gpu)
+        if not any("EADDRINUSE" in (err or "") for ok, err in res.values() if not ok):
+            break
+    return res
+
+
+def _run_batch_once(module, names, nprocs, timeout, env_extra, keep_gpu):
     import json
     import tempfile
 
