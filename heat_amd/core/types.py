@@ -43,7 +43,7 @@ class datatype:
         if n == 0:
             value = ((0,),)
         if len(value) > 1:
-            value = (value,)
+            raise TypeError("{} takes at most one positional argument, got {}".format(cls.__name__, n))
         value = value[0]
         from .dndarray import DNDarray
 
@@ -57,7 +57,8 @@ class datatype:
 
     @classmethod
     def char(cls):
-        return cls._char
+        """The type's array-protocol code like the reference ('i4', 'f4', 'c8', bool: 'u1')."""
+        return _TYPESTR.get(cls, cls._char)
 
 
 class bool(datatype):
@@ -162,6 +163,8 @@ _ORDER = (bool, uint8, int8, int16, int32, int64, float32, float64, complex64, c
 _CODE = {t: i for i, t in enumerate(_ORDER)}
 
 _by_char = {t._char: t for t in _ORDER}
+_TYPESTR = {bool: "u1", uint8: "u1", int8: "i1", int16: "i2", int32: "i4", int64: "i8", float32: "f4",
+            float64: "f8", complex64: "c8", complex128: "c16"}
 _by_str = {
     "b1": bool, "u": uint8, "u1": uint8, "i1": int8, "i2": int16, "i4": int32, "i8": int64,
     "f4": float32, "f8": float64, "c8": complex64, "c16": complex128,
@@ -216,7 +219,9 @@ def heat_type_of(obj) -> Type[datatype]:
         try:
             return canonical_heat_type(np.asarray(obj).dtype)
         except Exception:
-            pass
+            # mixed sequences: the type of the first element, like the reference
+            if len(obj):
+                return heat_type_of(obj[0])
     if isinstance(obj, type):
         return canonical_heat_type(obj)
     raise TypeError("data type of {} is not understood".format(obj))
