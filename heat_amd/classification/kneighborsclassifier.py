@@ -45,6 +45,9 @@ class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
             raise ValueError("x must be two-dimensional, but was {}".format(x.ndim))
         if x.gshape[0] != y.gshape[0]:
             raise ValueError("Number of samples x and y samples mismatch, got {}, {}".format(x.gshape[0], y.gshape[0]))
+        if y.split != x.split and x.comm.size > 1:
+            # labels travel with their samples: y takes x's distribution
+            y = ht.resplit(y, x.split if x.split == 0 else None)
         self.x = x
         self.n_samples_fit_ = x.gshape[0]
         if y.ndim == 1:

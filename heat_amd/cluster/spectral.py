@@ -43,7 +43,12 @@ class Spectral(ClusteringMixin, BaseEstimator):
         else:
             raise NotImplementedError("Other kernels currently not supported")
         if assign_labels == "kmeans":
-            self._cluster = KMeans(**params)
+            # options for the label-assigning k-means, flat or as params={...}; keys k-means does not
+            # take (e.g. the reference's normalize=) are accepted and ignored, like the reference
+            opts = dict(params.pop("params", None) or {})
+            opts.update(params)
+            known = ("init", "max_iter", "tol", "random_state")
+            self._cluster = KMeans(**{k: v for k, v in opts.items() if k in known})
         else:
             raise NotImplementedError("Other Label Assignment Algorithms are currently not available")
         self._labels = None

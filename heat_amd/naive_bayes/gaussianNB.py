@@ -24,6 +24,14 @@ __all__ = ["GaussianNB"]
 class GaussianNB(ClassificationMixin, BaseEstimator):
     """Gaussian Naive Bayes with online updates (``partial_fit``)."""
 
+    @property
+    def epsilon_(self) -> DNDarray:
+        """Variance floor added to every class variance: var_smoothing * max feature variance
+        (shape (1,), like the reference); an AttributeError before the first fit."""
+        if getattr(self, "_epsilon", None) is None:
+            raise AttributeError("'GaussianNB' object has no attribute 'epsilon_' (not fitted yet)")
+        return ht.array([self._epsilon], dtype=ht.float64)
+
     def __init__(self, priors=None, var_smoothing: float = 1e-9):
         self.priors = priors
         self.var_smoothing = var_smoothing
@@ -72,7 +80,7 @@ class GaussianNB(ClassificationMixin, BaseEstimator):
                 raise ValueError("sample_weight.shape == {}, expected {}!".format(sample_weight.shape, (n_samples,)))
         X = x.larray if x.larray.is_floating_point() else x.larray.double()
         dt = X.dtype
-        self.epsilon_ = self.var_smoothing * float(ht.var(x, axis=0).max().item())
+        self._epsilon = self.var_smoothing * float(ht.var(x, axis=0).max().item())
         if _refit:
             self.classes_ = None
         first = getattr(self, "classes_", None) is None
@@ -97,17 +105,27 @@ class GaussianNB(ClassificationMixin, BaseEstimator):
                     raise ValueError("Priors must be non-negative.")
                 self.class_prior_ = pri
         else:
+            if classes is not None:
+                cl_new = classes._gathered() if classes.is_distributed() else classes.larray
+                if cl_new.numel() != self.classes_.larray.numel() or not bool(
+                        (cl_new.to(self.classes_.larray.device) == self.classes_.larray).all()):
+                    raise ValueError("classes={} is not the same as on the last call to partial_fit, was {}".format(
+                        cl_new.tolist(), self.classes_.larray.tolist()))
             if x.gshape[1] != self.theta_.gshape[1]:
                 raise ValueError("Number of features {} does not match previous data {}.".format(
                     x.gshape[1], self.theta_.gshape[1]))
-            self.sigma_.larray -= self.epsilon_
+            self.sigma_.larray -= self._epsilon
         cl = self.classes_.larray
         yl = self._local_rows(y, x).to(cl.dtype).to(X.device)
         idx = torch.searchsorted(cl.contiguous(), yl.contiguous())
         bad = (idx >= cl.numel()) | (cl[idx.clamp(max=cl.numel() - 1)] != yl)
-        if bool(bad.any()) if yl.numel() else False:
+        any_bad = bool(bad.any()) if yl.numel() else False
+        if x.is_distributed():
+            # every rank must raise together (a lone raise would leave the others in a collective)
+            any_bad = bool(x.comm.allreduce(int(any_bad), MPI.MAX))
+        if any_bad:
             raise ValueError("The target label(s) {} in y do not exist in the initial classes {}".format(
-                torch.unique(yl[bad]).tolist(), cl.tolist()))
+                torch.unique(yl[bad]).tolist() if yl.numel() else [], cl.tolist()))
         k = cl.numel()
         f = X.shape[1]
         w = self._local_rows(sample_weight, x).to(torch.float64) if sample_weight is not None else \
@@ -138,7 +156,7 @@ class GaussianNB(ClassificationMixin, BaseEstimator):
         var_new = m2_tot / safe
         upd = (cnt > 0).unsqueeze(1)
         self.theta_.larray = torch.where(upd, mu_new, mu_old).to(dt)
-        self.sigma_.larray = (torch.where(upd, var_new, var_old) + self.epsilon_).to(dt)
+        self.sigma_.larray = (torch.where(upd, var_new, var_old) + self._epsilon).to(dt)
         self.class_count_.larray = n_tot.to(self.class_count_.larray.dtype)
         if self.priors is None:
             self.class_prior_ = ht.array((n_tot / n_tot.sum()).to(torch.float64), device=x.device, comm=x.comm)
@@ -146,6 +164,8 @@ class GaussianNB(ClassificationMixin, BaseEstimator):
 
     # ----------------------------------------------------------------- prediction
     def _joint_log_likelihood(self, x: DNDarray) -> DNDarray:
+        if not isinstance(x, DNDarray):
+            raise ValueError("input needs to be a ht.DNDarray, but was {}".format(type(x)))
         X = x.larray if x.larray.is_floating_point() else x.larray.double()
         theta = self.theta_.larray.to(X.dtype)
         sigma = self.sigma_.larray.to(X.dtype)

@@ -104,7 +104,9 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
     comm = X.comm
     dx, dy = X.is_distributed(), Y.is_distributed()
     if not dx and not dy:
-        return DNDarray(_local(metric, x, y, sigma).to(tt), (m, n), dtype, None, X.device, comm, True)
+        # the split rules hold in a world of one too
+        out_split = 0 if X.split == 0 else (1 if Y.split == 0 else None)
+        return DNDarray(_local(metric, x, y, sigma).to(tt), (m, n), dtype, out_split, X.device, comm, True)
     if dx and not dy:
         return DNDarray(_local(metric, x, y, sigma).to(tt), (m, n), dtype, 0, X.device, comm, X.balanced)
     if not dx and dy:
@@ -145,7 +147,7 @@ def _dist_callable(X: DNDarray, Y: Optional[DNDarray], fn: Callable) -> DNDarray
     elif Y.is_distributed():
         split = 1
     else:
-        split = None
+        split = 0 if X.split == 0 else (1 if Y.split == 0 else None)
     return DNDarray(fn(x, y).to(tt), (m, n), dtype, split, X.device, X.comm, True)
 
 
