@@ -71,6 +71,9 @@ class DASO:
                  max_global_skips: int = 8, sending_chunk_size: int = 10_000_000,
                  downcast_type: torch.dtype = torch.bfloat16, use_mpi_groups: bool = True,
                  skip_reduction_factor: int = 2, local_skip_factor: int = 4, verbose: bool = False):
+        if scheduler is not None and not (isinstance(scheduler, type) or hasattr(scheduler, "step")):
+            raise TypeError("scheduler must be None or a torch lr_scheduler (class), currently {}".format(
+                type(scheduler)))
         self._check_types(local_optimizer, total_epochs, comm, warmup_epochs, cooldown_epochs, stability_level,
                           max_global_skips, sending_chunk_size, downcast_type, use_mpi_groups, skip_reduction_factor,
                           local_skip_factor, verbose)
@@ -140,12 +143,14 @@ class DASO:
                           ("cooldown_epochs", cooldown_epochs), ("max_global_skips", max_global_skips),
                           ("sending_chunk_size", sending_chunk_size), ("skip_reduction_factor", skip_reduction_factor),
                           ("local_skip_factor", local_skip_factor)):
-            if not isinstance(val, int):
+            if not isinstance(val, int) or isinstance(val, bool):
                 raise TypeError("{} must be an int, currently {}".format(name, type(val)))
+            if val < 0:
+                raise ValueError("{} must be >= 0, currently {}".format(name, val))
         if not isinstance(stability_level, float):
             raise TypeError("stability_level must be a float, currently {}".format(type(stability_level)))
         if downcast_type not in (torch.bfloat16, torch.half, torch.float):
-            raise ValueError("downcast_type must be in [torch.bfloat16, torch.half, torch.float], currently "
+            raise TypeError("downcast_type must be in [torch.bfloat16, torch.half, torch.float], currently "
                              "{}".format(downcast_type))
         if not isinstance(use_mpi_groups, bool) or not isinstance(verbose, bool):
             raise TypeError("use_mpi_groups and verbose must be bools")

@@ -6,9 +6,17 @@ except ImportError:  # torchvision is optional
     _tvt = None
 
 
+class TorchvisionMissing(AttributeError):
+    """torchvision is not installed (an AttributeError, so ``getattr`` with a default and ``hasattr``
+    keep working like for any missing attribute)."""
+
+
 def __getattr__(name):
+    if name.startswith("__"):
+        raise AttributeError(name)
     if _tvt is None:
-        raise ImportError("torchvision is not installed; heat_amd.utils.vision_transforms needs it")
+        raise TorchvisionMissing("torchvision is not installed; heat_amd.utils.vision_transforms.{} needs it"
+                                 .format(name))
     try:
         return getattr(_tvt, name)
     except AttributeError:

@@ -126,7 +126,26 @@ def test_sanitize_memory_layout():
     raises(NotImplementedError, ht.array, a2, order="K")
 
 
-def test_devices():
+def test_get_default_device_cpu():
+    prev = ht.get_device()
+    try:
+        ht.use_device("cpu")
+        assert ht.get_device() is ht.cpu
+    finally:
+        ht.use_device(prev)
+
+
+def test_get_default_device_gpu():
+    if torch.cuda.is_available():
+        prev = ht.get_device()
+        try:
+            ht.use_device("gpu")
+            assert ht.get_device() is ht.gpu
+        finally:
+            ht.use_device(prev)
+
+
+def test_sanitize_device_cpu():
     assert ht.sanitize_device("cpu") is ht.cpu
     assert ht.sanitize_device("cPu") is ht.cpu
     assert ht.sanitize_device("  CPU  ") is ht.cpu
@@ -134,6 +153,17 @@ def test_devices():
     assert ht.sanitize_device(None) is ht.get_device()
     raises(ValueError, ht.sanitize_device, "fpu")
     raises(ValueError, ht.sanitize_device, 1)
+
+
+def test_sanitize_device_gpu():
+    if torch.cuda.is_available():
+        for name in ("gpu", "gPu", "  GPU  "):
+            assert ht.sanitize_device(name) is ht.gpu
+        assert ht.sanitize_device(ht.gpu) is ht.gpu
+    raises(ValueError, ht.sanitize_device, "fpu")
+
+
+def test_set_default_device_cpu():
     prev = ht.get_device()
     try:
         ht.use_device("cpu")
@@ -142,6 +172,22 @@ def test_devices():
         assert ht.get_device() is ht.cpu
         ht.use_device(None)
         assert ht.get_device() is ht.cpu
+        raises(ValueError, ht.use_device, "fpu")
+        raises(ValueError, ht.use_device, 1)
+    finally:
+        ht.use_device(prev)
+
+
+def test_set_default_device_gpu():
+    prev = ht.get_device()
+    try:
+        if torch.cuda.is_available():
+            ht.use_device("gpu")
+            assert ht.get_device() is ht.gpu
+            ht.use_device(ht.gpu)
+            assert ht.get_device() is ht.gpu
+            ht.use_device(None)
+            assert ht.get_device() is ht.gpu
         raises(ValueError, ht.use_device, "fpu")
         raises(ValueError, ht.use_device, 1)
     finally:
