@@ -710,6 +710,40 @@ class MPICommunication(Communication):
 
         return work, fin
 
+    def exchange_axis_async(self, send: torch.Tensor, send_axis: int, scounts, recv_shape, recv_axis: int, rcounts):
+        """Personalised exchange of the blocks ``send.narrow(send_axis, ., scounts[q])`` (to rank q);
+        the block from rank r lands in ``recv.narrow(recv_axis, ., rcounts[r])`` of a new tensor of
+        ``recv_shape``. The send blocks are packed into one buffer and the receive buffer unpacked
+        in one pass each (native ``pack.hip`` kernels on the GPU), the wire is the raw bytes (any
+        dtype, one ``all_to_all_single``). Returns (work or None, finalize -> recv tensor)."""
+        from ..ops import kernels as _k
+
+        recv_shape = tuple(int(x) for x in recv_shape)
+        if self.size == 1:
+            out = send.reshape(recv_shape) if tuple(send.shape) == recv_shape else send
+            return None, lambda: out
+        packed = _k.pack_blocks(send, send_axis, scounts)
+        so, _, sr = _k._rows_view(tuple(send.shape), send_axis)
+        ro, _, rr = _k._rows_view(recv_shape, recv_axis)
+        es = send.element_size()
+        in_b = [so * int(c) * sr * es for c in scounts]
+        out_b = [ro * int(c) * rr * es for c in rcounts]
+        flat_out = torch.empty(int(np.prod(recv_shape)) if recv_shape else 1, dtype=send.dtype, device=send.device)
+        src_b = packed.contiguous().view(torch.uint8) if packed.numel() else torch.empty(0, dtype=torch.uint8,
+                                                                                           device=send.device)
+        dst_b = flat_out.view(torch.uint8) if flat_out.numel() else torch.empty(0, dtype=torch.uint8,
+                                                                                device=send.device)
+        work = _SD.all_to_all_single(dst_b, src_b, out_b, in_b, group=self.group, async_op=True)
+        return work, lambda: _k.unpack_blocks(flat_out, recv_shape, recv_axis, rcounts)
+
+    def exchange_axis(self, send, send_axis, scounts, recv_shape, recv_axis, rcounts) -> torch.Tensor:
+        """Blocking :meth:`exchange_axis_async`."""
+        self._trace("Alltoallv", send)
+        work, fin = self.exchange_axis_async(send, send_axis, scounts, recv_shape, recv_axis, rcounts)
+        if work is not None:
+            work.wait()
+        return fin()
+
     def _alltoall_impl(self, sendbuf, recvbuf, send_axis, recv_axis) -> MPIRequest:
         send, scounts, _ = self._unpack_v(sendbuf)
         recv, rcounts, _ = self._unpack_v(recvbuf)
@@ -721,20 +755,13 @@ class MPICommunication(Communication):
             rcounts = self.counts_displs_shape(recv.shape, recv_axis)[0]
         scounts = [int(c) for c in scounts]
         rcounts = [int(c) for c in rcounts]
-        blocks, off = [], 0
-        for r in range(self.size):
-            blocks.append(send.narrow(send_axis, off, scounts[r]))
-            off += scounts[r]
-        shapes = []
-        for r in range(self.size):
-            s = list(recv.shape)
-            s[recv_axis] = rcounts[r]
-            shapes.append(tuple(s))
         self._trace("Alltoallv", send)
-        work, fin = self._exchange_async(blocks, shapes)
+        work, fin = self.exchange_axis_async(send, send_axis, scounts, tuple(recv.shape), recv_axis, rcounts)
 
         def done():
-            recv.copy_(torch.cat(fin(), dim=recv_axis))
+            res = fin()
+            if res.data_ptr() != recv.data_ptr():
+                recv.copy_(res.reshape(recv.shape))
 
         return MPIRequest(work, done)
 

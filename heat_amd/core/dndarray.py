@@ -520,16 +520,11 @@ class DNDarray:
             old, p, rank = self.split, self.comm.size, self.comm.rank
             src_counts = self.split_counts()
             dst_counts = _chunk_counts(self.gshape[axis], p)
-            dst = _partition_bounds(dst_counts)
-            blocks = [self.__array.narrow(axis, dst[q][0], dst_counts[q]) for q in range(p)]
-            shapes = []
-            for r in range(p):
-                sh = list(self.gshape)
-                sh[old] = src_counts[r]
-                sh[axis] = dst_counts[rank]
-                shapes.append(tuple(sh))
-            parts = self.comm.exchange(blocks, shapes)
-            self.__array = torch.cat(parts, dim=old)
+            # (rows of old) x (columns of axis) tiles in ONE all-to-all; packing and unpacking are
+            # single passes (native pack.hip kernels on the GPU)
+            rshape = list(self.gshape)
+            rshape[axis] = dst_counts[rank]
+            self.__array = self.comm.exchange_axis(self.__array, axis, dst_counts, rshape, old, src_counts)
         self.__split = axis
         self.__balanced = True
         self.__lshape_map = None

@@ -358,7 +358,7 @@ def _argext_native(x: DNDarray, axis, largest: bool, keepdim: bool) -> DNDarray:
         gshape = tuple(1 if i == axis else s for i, s in enumerate(x.gshape))
     else:
         gshape = tuple(s for i, s in enumerate(x.gshape) if i != axis)
-    if along_split or x.split is None:
+    if along_split or x.split is None or x.split == axis:
         return DNDarray(res, gshape, types.int64, None, x.device, x.comm, True)
     split = x.split if (keepdim or x.split < axis) else x.split - 1
     return DNDarray(res, gshape, types.int64, split, x.device, x.comm, x.balanced)

@@ -32,7 +32,7 @@ def iris(split: Optional[int] = 0, device=None, comm=None, seed: int = 0) -> Tup
     """(150 x 4 float32 features, 150 int64 labels) with iris-like class structure."""
     X, y = _iris_numpy(seed)
     return (ht.array(X, split=split, device=device, comm=comm),
-            ht.array(y, split=split, device=device, comm=comm))
+            ht.array(y, split=split if split in (None, 0) else None, device=device, comm=comm))
 
 
 def write_iris_csv(path: str, seed: int = 0, sep: str = ";") -> str:

@@ -1179,3 +1179,70 @@ def sort_rows(x: torch.Tensor, descending: bool = False) -> Tuple[torch.Tensor, 
     check(L.ha_radix_sort_rows(_ptr(xc), _RADIX_DTYPES[x.dtype], rows, rowlen, int(descending), _ptr(vals), _ptr(idx),
                                _ptr(ws), ctypes.c_void_p(stream_ptr(x.device))), "ha_radix_sort_rows")
     return vals, idx
+
+
+# --------------------------------------------------------------------------------------------
+# block pack / unpack for personalised exchanges (csrc/pack.hip)
+# --------------------------------------------------------------------------------------------
+def _rows_view(shape, axis):
+    O = int(np.prod(shape[:axis])) if axis else 1
+    S = int(shape[axis])
+    R = int(np.prod(shape[axis + 1:])) if axis + 1 < len(shape) else 1
+    return O, S, R
+
+
+def _block_offsets(counts):
+    off = [0]
+    for c in counts:
+        off.append(off[-1] + int(c))
+    return off
+
+
+def pack_supported(t: torch.Tensor) -> bool:
+    """Device tensors of at most 256 blocks go through the native pack kernel."""
+    return t.is_cuda and use_native(t) and hasattr(lib(), "ha_rows_permute")
+
+
+def pack_blocks(t: torch.Tensor, axis: int, counts) -> torch.Tensor:
+    """The blocks ``t.narrow(axis, off_q, counts[q])`` one after the other, each in C order, as ONE
+    flat tensor (the send buffer of an all-to-all) - a single pass over ``t``."""
+    counts = [int(c) for c in counts]
+    if not pack_supported(t) or len(counts) > 256:
+        parts = [t.narrow(axis, o, c).reshape(-1) for o, c in zip(_block_offsets(counts)[:-1], counts)]
+        return torch.cat(parts) if parts else t.new_empty(0)
+    src = t.contiguous()
+    O, S, R = _rows_view(src.shape, axis)
+    assert sum(counts) == S, (counts, S)
+    out = torch.empty(src.numel(), dtype=src.dtype, device=src.device)
+    off = np.asarray(_block_offsets(counts), dtype=np.int64)
+    check(lib().ha_rows_permute(_ptr(src), _ptr(out), O, S, R * src.element_size(),
+                                off.ctypes.data_as(ctypes.c_void_p), len(counts), 0,
+                                ctypes.c_void_p(stream_ptr(src.device))), "ha_rows_permute")
+    return out
+
+
+def unpack_blocks(flat: torch.Tensor, shape, axis: int, counts, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Inverse of :func:`pack_blocks`: the tensor of ``shape`` whose blocks along ``axis``
+    (``counts[q]`` rows each) arrive one after the other in ``flat`` - a single pass."""
+    counts = [int(c) for c in counts]
+    shape = tuple(int(s) for s in shape)
+    if out is None:
+        out = torch.empty(shape, dtype=flat.dtype, device=flat.device)
+    if not pack_supported(flat) or len(counts) > 256 or not out.is_contiguous():
+        parts, pos = [], 0
+        for c in counts:
+            sh = list(shape)
+            sh[axis] = c
+            n = int(np.prod(sh))
+            parts.append(flat[pos: pos + n].reshape(sh))
+            pos += n
+        out.copy_(torch.cat(parts, dim=axis))
+        return out
+    O, S, R = _rows_view(shape, axis)
+    assert sum(counts) == S and flat.numel() == O * S * R, (counts, shape, flat.numel())
+    off = np.asarray(_block_offsets(counts), dtype=np.int64)
+    src = flat.contiguous()
+    check(lib().ha_rows_permute(_ptr(src), _ptr(out), O, S, R * src.element_size(),
+                                off.ctypes.data_as(ctypes.c_void_p), len(counts), 1,
+                                ctypes.c_void_p(stream_ptr(src.device))), "ha_rows_permute")
+    return out

@@ -52,7 +52,7 @@ def test_array():
     t2 = ht.array([[1.0, 2.0, 3.0]] * 3, split=0)
     assert t2.dtype == ht.float32 and t2.gshape == (3, 3) and t2.split == 0
     _chunk_ok(t2)
-    assert (t2.larray == torch.tensor([1.0, 2.0, 3.0])).all()
+    assert (t2.larray.cpu() == torch.tensor([1.0, 2.0, 3.0])).all()
     x = np.arange(60.0).reshape(3, 4, 5)
     for s in splits(3):
         h = ht.array(x, split=s)
