@@ -295,7 +295,24 @@ class MPICommunication(Communication):
         out[axis] = self.size * counts[self.rank]
         return counts, displs, tuple(out)
 
+    def _check_stream(self, name, t):
+        """HEAT_DEBUG_STREAMS=1: a collective on a device tensor must be issued on
+        the stream the native kernels last launched on, or after that stream has drained;
+        otherwise RCCL (ordered behind the CURRENT stream) may read data a kernel on the other
+        stream has not written yet."""
+        from .. import ops
+
+        if not (ops.DEBUG_STREAMS and isinstance(t, torch.Tensor) and t.is_cuda):
+            return
+        last = ops.LAST_LAUNCH_STREAM.get(t.device.index)
+        cur = torch.cuda.current_stream(t.device)
+        if last is not None and last != cur and not last.query():
+            raise RuntimeError("stream-ordering race: {} issued on stream {} while native kernels on stream {} are "
+                               "still running; synchronise the streams (e.g. cur.wait_stream(other)) first"
+                               .format(name, cur.cuda_stream, last.cuda_stream))
+
     def _trace(self, name, t=None):
+        self._check_stream(name, t)
         if self._debug and self.size > 1:
             sig = "{}|{}|{}".format(name, None if t is None else t.dtype,
                                     None if t is None else tuple(t.shape) if name.startswith(("All", "Bcast")) else "")

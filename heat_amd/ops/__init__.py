@@ -103,8 +103,18 @@ def use_native(t: torch.Tensor) -> bool:
     raise RuntimeError("heat_amd native kernel library is not available for a device tensor: {}".format(_load_error))
 
 
+# HEAT_DEBUG_STREAMS=1: remember the stream of the last native launch per device so that a
+# collective issued on ANOTHER stream while that one still has work queued is reported as the
+# race it is (see ``core.communication.MPICommunication._check_stream``)
+DEBUG_STREAMS = os.environ.get("HEAT_DEBUG_STREAMS", "0") == "1"
+LAST_LAUNCH_STREAM = {}
+
+
 def stream_ptr(device=None) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    s = torch.cuda.current_stream(device)
+    if DEBUG_STREAMS:
+        LAST_LAUNCH_STREAM[s.device.index] = s
+    return s.cuda_stream
 
 
 def check(rc: int, name: str):

@@ -89,3 +89,35 @@ def test_mnist_example_on_gpu(gpu):
                           "--samples", "2048"], capture_output=True, text=True, timeout=600, cwd=root)
     assert res.returncode == 0, res.stderr[-3000:]
     assert "epoch 1" in res.stdout
+
+
+def test_debug_streams_detects_cross_stream_race(gpu):
+    """HEAT_DEBUG_STREAMS=1: a collective issued on the default stream while a native kernel is
+    still running on a side stream raises; after wait_stream it passes."""
+    import torch
+
+    import heat_amd as ht
+    from heat_amd import ops
+
+    old = ops.DEBUG_STREAMS
+    ops.DEBUG_STREAMS = True
+    try:
+        side = torch.cuda.Stream()
+        x = torch.randn(8192, 8192, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            # ~5 ms of native kernels queued on the side stream (host enqueues far faster)
+            for _ in range(100):
+                ops.moments(x, None)
+        raised = False
+        try:
+            ht.MPI_WORLD.Allreduce(ht.MPI.IN_PLACE, x[:1, :4].clone(), ht.MPI.SUM)
+        except RuntimeError as e:
+            raised = "stream-ordering race" in str(e)
+        torch.cuda.current_stream().wait_stream(side)
+        side.synchronize()
+        ht.MPI_WORLD.Allreduce(ht.MPI.IN_PLACE, x[:1, :4].clone(), ht.MPI.SUM)
+        assert raised
+    finally:
+        ops.DEBUG_STREAMS = old
+        ops.LAST_LAUNCH_STREAM.clear()
