@@ -401,10 +401,31 @@ class MPICommunication(Communication):
             return None
         return flat.view(moved.dtype).reshape((sum(counts),) + tuple(moved.shape[1:]))
 
+    def _native(self):
+        """The native stream-ordered RCCL communicator of this group (``HEAT_COMM_NATIVE=1``,
+        device jobs of several ranks only; created collectively on first use)."""
+        nc = getattr(self, "_native_comm", None)
+        if nc is None:
+            from ..parallel import native_comm
+
+            nc = False
+            if native_comm.enabled() and self.size > 1 and torch.cuda.is_available():
+                nc = native_comm.NativeComm(self)
+            self._native_comm = nc
+        return nc or None
+
     def _reduce_tensor_async(self, t: torch.Tensor, op: Op):
         """All-reduce ``t`` in place (returns (work, finalize))."""
         if op is MPI.SUM and self._ipc_allreduce(t) is not None:
             return None, None  # stream-ordered on the current stream: nothing to wait for
+        opname = {MPI.SUM: "sum", MPI.PROD: "prod", MPI.MAX: "max", MPI.MIN: "min"}.get(op)
+        if t.is_cuda and opname is not None and self._native() is not None and self._native().supports(t, opname):
+            nc = self._native()
+            contig = t if t.is_contiguous() else t.contiguous()
+            nc.allreduce_(contig, opname)  # ordered on the current stream: nothing to wait for
+            if contig is not t:
+                t.copy_(contig)
+            return None, None
         native = op.torch_op is not None and t.dtype != torch.bool and (not t.is_complex() or op is MPI.SUM)
         if native:
             contig = _wire_dtype(t) if t.is_contiguous() else _wire_dtype(t).contiguous()
@@ -750,6 +771,9 @@ class MPICommunication(Communication):
                                                                                            device=send.device)
         dst_b = flat_out.view(torch.uint8) if flat_out.numel() else torch.empty(0, dtype=torch.uint8,
                                                                                 device=send.device)
+        if send.is_cuda and self._native() is not None:
+            self._native().alltoallv_bytes(src_b, in_b, dst_b, out_b)  # on the current stream
+            return None, lambda: _k.unpack_blocks(flat_out, recv_shape, recv_axis, rcounts)
         work = _SD.all_to_all_single(dst_b, src_b, out_b, in_b, group=self.group, async_op=True)
         return work, lambda: _k.unpack_blocks(flat_out, recv_shape, recv_axis, rcounts)
 

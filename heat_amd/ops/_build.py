@@ -82,7 +82,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         with ThreadPoolExecutor(jobs) as ex:
             list(ex.map(lambda so: run([hipcc()] + flags + file_flags(so[0]) + ["-c", so[0], "-o", so[1]]),
                         zip(sources(), objs)))
-        run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", tmp])
+        run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-ldl", "-o", tmp])
     except subprocess.CalledProcessError as e:
         os.unlink(tmp)
         msg = e.stderr.decode() if e.stderr else ""
