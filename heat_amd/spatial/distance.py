@@ -56,7 +56,9 @@ _manhattan_fast = _manhattan
 def cdist(X: DNDarray, Y: Optional[DNDarray] = None, quadratic_expansion: bool = False) -> DNDarray:
     """Euclidean distance matrix ``d(x, y) = sqrt(|x - y|^2)`` of size m x n.
 
-    ``quadratic_expansion=True``: |x|^2 + |y|^2 - 2 x.y on the fp32 matrix cores (fastest);
+    ``quadratic_expansion=True``: |x|^2 + |y|^2 - 2 x.y with the x.y GEMM as a 3-term fp16 split on
+    the FP16 matrix cores (``cdist_f16x3.hip``, fp32-GEMM accuracy; fp64 input uses fp64 math),
+    fastest; like any expansion it cancels to ~sqrt(eps |x|^2) for near-identical rows.
     ``False``: exact difference-based kernel (no cancellation for near-identical rows)."""
     return _dist(X, Y, "euclidean", exact=not quadratic_expansion)
 
