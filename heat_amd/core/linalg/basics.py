@@ -591,9 +591,26 @@ def matrix_norm(x: DNDarray, axis: Optional[Tuple[int, int]] = None, keepdims: b
         s = arithmetics.sum(xa, axis=col, keepdim=True)
         r = statistics.max(s, axis=row, keepdim=True) if ord > 0 else statistics.min(s, axis=row, keepdim=True)
     elif ord in ("nuc", 2, -2):
-        full = x._gathered().to(xa.larray.dtype)
-        fm = full.movedim((row, col), (-2, -1))
-        sv = torch.linalg.svdvals(fm)
+        sv = None
+        if x.ndim == 2 and x.is_distributed():
+            # singular values of a distributed matrix = those of its n x n R factor (tall, split 0)
+            # or of R of the transpose (wide, split 1): one TSQR, no gather of the m x n matrix
+            from .qr import qr as _qr
+
+            m_, n_ = x.gshape
+            src = None
+            if x.split == 0 and m_ >= n_:
+                src = x if (row, col) == (0, 1) else transpose(x)
+            elif x.split == 1 and n_ >= m_:
+                src = transpose(x) if (row, col) == (0, 1) else x
+            if src is not None and src.split == 0 and src.gshape[0] >= src.gshape[1]:
+                R = _qr(src.astype(xa.dtype) if src.dtype != xa.dtype else src, calc_q=False, mode="reduced").R
+                Rl = R._gathered() if R.is_distributed() else R.larray
+                sv = torch.linalg.svdvals(Rl.to(xa.larray.dtype))
+        if sv is None:
+            full = x._gathered().to(xa.larray.dtype)
+            fm = full.movedim((row, col), (-2, -1))
+            sv = torch.linalg.svdvals(fm)
         val = sv.sum(-1) if ord == "nuc" else (sv.max(-1).values if ord == 2 else sv.min(-1).values)
         if keepdims:
             val = val.unsqueeze(-1).unsqueeze(-1).movedim((-2, -1), (row, col))

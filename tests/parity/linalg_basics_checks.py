@@ -74,6 +74,12 @@ def test_matrix_norm():
             close(ht.linalg.matrix_norm(bb, ord=o), np.linalg.norm(B, ord=o), rtol=1e-4)
         mn = ht.linalg.matrix_norm(bb, keepdims=True)
         assert mn.shape == (1, 1)
+    # tall and wide operands: the 2 / -2 / nuc norms come from the TSQR R factor when distributed
+    for shape in ((41, 6), (6, 41)):
+        T = rng(21).standard_normal(shape)
+        for s in splits(2):
+            for o in (2, -2, "nuc", "fro", 1, np.inf):
+                close(ht.linalg.matrix_norm(ht.array(T, split=s), ord=o), np.linalg.norm(T, ord=o), rtol=1e-8)
     M = np.arange(18.0).reshape(2, 3, 3) - 9
     for s in splits(3):
         m = ht.array(M, split=s)
