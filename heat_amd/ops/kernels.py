@@ -14,7 +14,7 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
+__all__ = ["pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr",
            "householder_factor", "householder_apply", "householder_block",

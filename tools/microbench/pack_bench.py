@@ -1,9 +1,13 @@
 """Native one-pass block pack (csrc/pack.hip) vs narrow().contiguous() + torch.cat for the send
 buffer of a split 0 -> split 1 resplit on 8 ranks (a 1e9-byte-class slab)."""
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from heat_amd import ops
 
