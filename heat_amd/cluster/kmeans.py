@@ -70,15 +70,19 @@ class KMeans(_KCluster):
 
     def step(self, x: DNDarray) -> float:
         """One Lloyd iteration on the current centers (initialising them on first use); returns
-        the squared centroid shift. The building block of :meth:`fit`, exposed for streaming use
-        and benchmarking."""
+        the squared centroid shift (a float, or a 0-d device tensor when ``tol`` is None). The
+        building block of :meth:`fit`, exposed for streaming use and benchmarking."""
         if self._cluster_centers is None:
             self._initialize_cluster_centers(x)
             self._n_iter = 0
         X = x.larray if x.larray.is_floating_point() else x.larray.float()
         C = self._cluster_centers.larray.to(X.dtype)
         newC, labels = self._centroid_step(X, C, x.comm, x.is_distributed())
-        shift = float(((C - newC) ** 2).sum())
+        shift = ((C - newC) ** 2).sum()
+        if self.tol is not None:
+            shift = float(shift)  # a convergence test needs the value on the host
+        # tol=None (fixed iteration count): the shift stays a device scalar, no host sync per step,
+        # so the next step's kernels queue while this one runs (like fit())
         self._cluster_centers = DNDarray(newC, newC.shape, self._cluster_centers.dtype, None, x.device, x.comm, True)
         self._inertia = shift
         self._n_iter = (self._n_iter or 0) + 1
