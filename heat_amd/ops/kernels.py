@@ -1213,6 +1213,8 @@ def pack_blocks(t: torch.Tensor, axis: int, counts) -> torch.Tensor:
     src = t.contiguous()
     O, S, R = _rows_view(src.shape, axis)
     assert sum(counts) == S, (counts, S)
+    if O == 1:
+        return src.reshape(-1)  # blocks along the outermost axis are already back to back
     out = torch.empty(src.numel(), dtype=src.dtype, device=src.device)
     off = np.asarray(_block_offsets(counts), dtype=np.int64)
     check(lib().ha_rows_permute(_ptr(src), _ptr(out), O, S, R * src.element_size(),
@@ -1240,6 +1242,9 @@ def unpack_blocks(flat: torch.Tensor, shape, axis: int, counts, out: Optional[to
         return out
     O, S, R = _rows_view(shape, axis)
     assert sum(counts) == S and flat.numel() == O * S * R, (counts, shape, flat.numel())
+    if O == 1:
+        out.view(-1).copy_(flat) if out.data_ptr() != flat.data_ptr() else None
+        return out
     off = np.asarray(_block_offsets(counts), dtype=np.int64)
     src = flat.contiguous()
     check(lib().ha_rows_permute(_ptr(src), _ptr(out), O, S, R * src.element_size(),
