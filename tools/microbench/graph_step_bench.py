@@ -1,0 +1,64 @@
+"""Can one k-means Lloyd step (fp16x3 assign + counting-sort update + centroid division) be
+captured in a HIP graph, and what does replaying it save over eager launches? (n=1.25e7, k=1024,
+f=64, one GPU.)"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import heat_amd as ht  # noqa: E402
+
+
+def main():
+    ht.use_device("gpu")
+    ht.random.seed(1234)
+    x = ht.random.randn(12_500_000, 64, split=0)
+    km = ht.cluster.KMeans(n_clusters=1024, init="random", max_iter=1, tol=None, random_state=42)
+    for _ in range(4):
+        km.step(x)  # warm-up: packs the planes, settles the certified probe
+    torch.cuda.synchronize()
+    X = x.larray
+    C0 = km.cluster_centers_.larray.clone()
+
+    def eager(steps):
+        C = C0.clone()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            C, _ = km._centroid_step(X, C, x.comm, False)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e3, C
+
+    ms_eager, c_eager = eager(20)
+    # capture one step: static input C_in, static output C_out
+    C_in = C0.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            km._centroid_step(X, C_in, x.comm, False)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    rec = {"eager_ms": ms_eager}
+    try:
+        with torch.cuda.graph(g):
+            C_out, _ = km._centroid_step(X, C_in, x.comm, False)
+        C_in.copy_(C0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            g.replay()
+            C_in.copy_(C_out)
+        torch.cuda.synchronize()
+        rec["graph_ms"] = (time.perf_counter() - t0) / 20 * 1e3
+        rec["max_abs_diff_vs_eager"] = float((C_in - c_eager).abs().max())
+    except Exception as e:  # noqa: B902 - report what broke the capture
+        rec["capture_error"] = "{}: {}".format(type(e).__name__, e)[:400]
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
