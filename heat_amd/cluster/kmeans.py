@@ -68,6 +68,43 @@ class KMeans(_KCluster):
         newC = torch.where(gc.unsqueeze(1) > 0, gs / gc.clamp(min=1).unsqueeze(1), C.double()).to(C.dtype)
         return DNDarray(newC, C.shape, self._cluster_centers.dtype, None, x.device, x.comm, True)
 
+    def _graph_ok(self, X: torch.Tensor, comm, distributed: bool) -> bool:
+        """HIP-graph replay of the Lloyd step (``HEAT_KMEANS_GRAPH=1``): device data, no
+        certified-assignment probe in flight (it posts to the host), and collectives that are
+        stream-ordered on the capturing stream (a world of one, or the native communicator)."""
+        import os
+
+        if os.environ.get("HEAT_KMEANS_GRAPH", "0") != "1" or not X.is_cuda:
+            return False
+        if self._certify or self._cert_probe is not None:
+            return False
+        return not distributed or comm._native() is not None
+
+    def _centroid_step_graph(self, X: torch.Tensor, C: torch.Tensor, comm, distributed: bool):
+        """The Lloyd step replayed from a captured HIP graph: ONE launch per iteration instead of
+        ~15 kernel launches and their host overhead. Re-captured when the points, their planes
+        or the shapes change."""
+        key = (X.data_ptr(), tuple(X.shape), tuple(C.shape), C.dtype, self.precision, distributed,
+               id(self._pack_cache))
+        g = getattr(self, "_graph", None)
+        if g is None or self._graph_key != key:
+            self._graph = None
+            c_in = C.clone()
+            side = torch.cuda.Stream(device=X.device)
+            side.wait_stream(torch.cuda.current_stream(X.device))
+            with torch.cuda.stream(side):
+                self._centroid_step(X, c_in, comm, distributed)  # warm the allocator on this stream
+            torch.cuda.current_stream(X.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                c_out, labels = self._centroid_step(X, c_in, comm, distributed)
+            self._graph, self._graph_key = g, key
+            self._graph_io = (c_in, c_out, labels)
+        c_in, c_out, labels = self._graph_io
+        c_in.copy_(C)
+        g.replay()
+        return c_out.clone(), labels
+
     def step(self, x: DNDarray) -> float:
         """One Lloyd iteration on the current centers (initialising them on first use); returns
         the squared centroid shift (a float, or a 0-d device tensor when ``tol`` is None). The
@@ -77,7 +114,10 @@ class KMeans(_KCluster):
             self._n_iter = 0
         X = x.larray if x.larray.is_floating_point() else x.larray.float()
         C = self._cluster_centers.larray.to(X.dtype)
-        newC, labels = self._centroid_step(X, C, x.comm, x.is_distributed())
+        if self._graph_ok(X, x.comm, x.is_distributed()):
+            newC, labels = self._centroid_step_graph(X, C, x.comm, x.is_distributed())
+        else:
+            newC, labels = self._centroid_step(X, C, x.comm, x.is_distributed())
         shift = ((C - newC) ** 2).sum()
         if self.tol is not None:
             shift = float(shift)  # a convergence test needs the value on the host

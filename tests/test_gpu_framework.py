@@ -121,3 +121,26 @@ def test_debug_streams_detects_cross_stream_race(gpu):
     finally:
         ops.DEBUG_STREAMS = old
         ops.LAST_LAUNCH_STREAM.clear()
+
+
+def test_kmeans_graph_replay_matches_eager(gpu, monkeypatch):
+    """HEAT_KMEANS_GRAPH=1: the Lloyd step replayed from a captured HIP graph gives the same
+    centroids as eager launches."""
+    import torch
+
+    import heat_amd as ht
+
+    ht.random.seed(5)
+    x = ht.random.randn(200_000, 64, split=0)
+    res = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("HEAT_KMEANS_GRAPH", mode)
+        km = ht.cluster.KMeans(n_clusters=256, init="random", max_iter=1, tol=None, random_state=1)
+        km._certify = False
+        for _ in range(6):
+            km.step(x)
+        torch.cuda.synchronize()
+        res.append(km.cluster_centers_.larray.clone())
+        if mode == "1":
+            assert getattr(km, "_graph", None) is not None
+    assert torch.allclose(res[0], res[1], rtol=1e-5, atol=1e-5), float((res[0] - res[1]).abs().max())
