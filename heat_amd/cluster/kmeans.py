@@ -44,13 +44,14 @@ class KMeans(_KCluster):
         else:
             labels = self._assign_labels(X, C)
             sums, counts = ops.kmeans_update(X, labels, k)
-        packed = torch.cat([sums.reshape(-1).double(), counts.double()])
+        kf = sums.numel()
+        packed = torch.empty(kf + k, dtype=torch.float64, device=sums.device)
+        packed[:kf].copy_(sums.reshape(-1))
+        packed[kf:].copy_(counts)
         if distributed:
             comm.Allreduce(MPI.IN_PLACE, packed, MPI.SUM)
-        kf = sums.numel()
-        gs = packed[:kf].reshape(sums.shape)
-        gc = packed[kf:]
-        newC = torch.where(gc.unsqueeze(1) > 0, gs / gc.clamp(min=1).unsqueeze(1), C.double()).to(C.dtype)
+        # new centroids + squared shift in one launch (csrc/kmeans_finalize.hip)
+        newC, self._step_shift = ops.kmeans_finalize(packed, C)
         return newC, labels
 
     def _update_centroids(self, x: DNDarray, matching_centroids: DNDarray) -> DNDarray:
@@ -99,10 +100,11 @@ class KMeans(_KCluster):
             with torch.cuda.graph(g):
                 c_out, labels = self._centroid_step(X, c_in, comm, distributed)
             self._graph, self._graph_key = g, key
-            self._graph_io = (c_in, c_out, labels)
-        c_in, c_out, labels = self._graph_io
+            self._graph_io = (c_in, c_out, labels, self._step_shift)
+        c_in, c_out, labels, shift = self._graph_io
         c_in.copy_(C)
         g.replay()
+        self._step_shift = shift.clone()
         return c_out.clone(), labels
 
     def step(self, x: DNDarray) -> float:
@@ -118,7 +120,7 @@ class KMeans(_KCluster):
             newC, labels = self._centroid_step_graph(X, C, x.comm, x.is_distributed())
         else:
             newC, labels = self._centroid_step(X, C, x.comm, x.is_distributed())
-        shift = ((C - newC) ** 2).sum()
+        shift = self._step_shift
         if self.tol is not None:
             shift = float(shift)  # a convergence test needs the value on the host
         # tol=None (fixed iteration count): the shift stays a device scalar, no host sync per step,
@@ -146,7 +148,7 @@ class KMeans(_KCluster):
         for _ in range(self.max_iter):
             self._n_iter += 1
             newC, labels = self._centroid_step(X, C, x.comm, distributed)
-            shift = ((C - newC) ** 2).sum()
+            shift = self._step_shift
             C = newC
             if self.tol is not None:
                 self._inertia = float(shift)

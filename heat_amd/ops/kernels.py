@@ -14,7 +14,7 @@ import torch.nn.functional as F
 
 from . import check, lib, stream_ptr, use_native
 
-__all__ = ["pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
+__all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr",
            "householder_factor", "householder_apply", "householder_block",
@@ -1251,3 +1251,23 @@ def unpack_blocks(flat: torch.Tensor, shape, axis: int, counts, out: Optional[to
                                 off.ctypes.data_as(ctypes.c_void_p), len(counts), 1,
                                 ctypes.c_void_p(stream_ptr(src.device))), "ha_rows_permute")
     return out
+
+
+def kmeans_finalize(packed: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Lloyd epilogue (``csrc/kmeans_finalize.hip``): from ``packed = [sums (k*f) | counts (k)]``
+    (fp64) and the current centroids C (float32, k x f) return (new centroids, squared shift as a
+    0-d fp64 tensor); empty clusters keep their centroid. One launch on the GPU."""
+    k, f = C.shape
+    if packed.is_cuda and C.dtype == torch.float32 and use_native(C) and hasattr(lib(), "ha_km_finalize"):
+        pk = packed.contiguous()
+        Cc = C if C.stride(-1) == 1 else C.contiguous()
+        newC = torch.empty((k, f), dtype=torch.float32, device=C.device)
+        shift = torch.empty((), dtype=torch.float64, device=C.device)
+        check(lib().ha_km_finalize(_ptr(pk), k, f, _ptr(Cc), Cc.stride(0), _ptr(newC), _ptr(shift),
+                                   ctypes.c_void_p(stream_ptr(C.device))), "ha_km_finalize")
+        return newC, shift
+    kf = k * f
+    gs = packed[:kf].reshape(k, f)
+    gc = packed[kf:]
+    newC = torch.where(gc.unsqueeze(1) > 0, gs / gc.clamp(min=1).unsqueeze(1), C.double()).to(C.dtype)
+    return newC, ((C.double() - newC.double()) ** 2).sum()
