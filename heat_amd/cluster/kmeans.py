@@ -77,8 +77,17 @@ class KMeans(_KCluster):
 
         if os.environ.get("HEAT_KMEANS_GRAPH", "0") != "1" or not X.is_cuda:
             return False
+        # Measured on MI355X / ROCm 7 (tools/microbench/graph_debug2.py): with the runtime's graph
+        # packet capture (the default), the second and later replays read stale data written by
+        # earlier nodes (update sums off, centroids diverge to 1e27); with
+        # DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 replays are exact. The variable is read at HIP init, so
+        # graph mode is only taken when the process was started with it.
+        if os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
+            return False
         if self._certify or self._cert_probe is not None:
             return False
+        if self._pack_cache is None or self._pack_cache.key != ops.kernels._points_key(X):
+            return False  # the fp16x3 planes are (re)built eagerly, outside any capture
         return not distributed or comm._native() is not None
 
     def _centroid_step_graph(self, X: torch.Tensor, C: torch.Tensor, comm, distributed: bool):
