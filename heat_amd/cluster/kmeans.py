@@ -86,7 +86,7 @@ class KMeans(_KCluster):
             return False
         if self._certify or self._cert_probe is not None:
             return False
-        if self._pack_cache is None or self._pack_cache.key != ops.kernels._points_key(X):
+        if self.precision == "fast" and (self._pack_cache is None or self._pack_cache.key != ops.kernels._points_key(X)):
             return False  # the fp16x3 planes are (re)built eagerly, outside any capture
         return not distributed or comm._native() is not None
 

@@ -133,25 +133,28 @@ def test_kmeans_graph_replay_matches_eager(gpu):
     import sys
 
     code = """
-import torch, heat_amd as ht
+import os, torch, heat_amd as ht
 ht.use_device("gpu")
 ht.random.seed(5)
 x = ht.random.randn(200_000, 64, split=0)
-res = []
-for mode in ("0", "1"):
-    import os
-    os.environ["HEAT_KMEANS_GRAPH"] = mode
-    km = ht.cluster.KMeans(n_clusters=256, init="random", max_iter=1, tol=None, random_state=1)
-    km._certify = False
-    for _ in range(6):
-        km.step(x)
+X = x.larray
+os.environ["HEAT_KMEANS_GRAPH"] = "1"
+km = ht.cluster.KMeans(n_clusters=256, init="random", max_iter=1, tol=None, random_state=1)
+km.step(x)   # packs the points (and re-arms the certified probe): always eager
+km._certify, km._cert_probe = False, None
+worst = []
+for _ in range(5):
+    C = km.cluster_centers_.larray.clone()
+    eager, _ = km._centroid_step(X, C, x.comm, False)   # the same step, launched eagerly
+    eager = eager.clone()
+    km.step(x)   # replayed from the graph
     torch.cuda.synchronize()
-    res.append(km.cluster_centers_.larray.clone())
-    assert (getattr(km, "_graph", None) is not None) == (mode == "1")
-d = (res[0] - res[1]).abs()
-# eager sums use float atomics (order-dependent rounding), so a few labels may flip over 6 steps
-assert float(d.median()) < 1e-5 and float(d.max()) < 0.1, (float(d.median()), float(d.max()))
-print("OK")
+    d = (km.cluster_centers_.larray - eager).abs()
+    worst.append((float(d.median()), float(d.max())))
+assert getattr(km, "_graph", None) is not None
+# per step: identical labels, sums within float-atomic rounding
+assert all(m < 1e-5 and M < 1e-3 for m, M in worst), worst
+print("OK", worst)
 """
     env = dict(os.environ, DEBUG_CLR_GRAPH_PACKET_CAPTURE="0", HEAT_KMEANS_GRAPH="0")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
