@@ -26,5 +26,6 @@ from . import utils
 from . import models
 from . import profiling
 from . import datasets
+from . import testing
 
 profiling._auto_enable()
