@@ -44,14 +44,16 @@ class KMeans(_KCluster):
         else:
             labels = self._assign_labels(X, C)
             sums, counts = ops.kmeans_update(X, labels, k)
-        kf = sums.numel()
-        packed = torch.empty(kf + k, dtype=torch.float64, device=sums.device)
-        packed[:kf].copy_(sums.reshape(-1))
-        packed[kf:].copy_(counts)
         if distributed:
+            kf = sums.numel()
+            packed = torch.empty(kf + k, dtype=torch.float64, device=sums.device)
+            packed[:kf].copy_(sums.reshape(-1))
+            packed[kf:].copy_(counts)
             comm.Allreduce(MPI.IN_PLACE, packed, MPI.SUM)
-        # new centroids + squared shift in one launch (csrc/kmeans_finalize.hip)
-        newC, self._step_shift = ops.kmeans_finalize(packed, C)
+            # new centroids + squared shift in one launch (csrc/kmeans_finalize.hip)
+            newC, self._step_shift = ops.kmeans_finalize(packed, C)
+        else:   # no pack: the epilogue reads the update kernel's fp32 sums and counts directly
+            newC, self._step_shift = ops.kmeans_finalize(None, C, sums=sums, counts=counts)
         return newC, labels
 
     def _update_centroids(self, x: DNDarray, matching_centroids: DNDarray) -> DNDarray:

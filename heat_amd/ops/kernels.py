@@ -1253,19 +1253,45 @@ def unpack_blocks(flat: torch.Tensor, shape, axis: int, counts, out: Optional[to
     return out
 
 
-def kmeans_finalize(packed: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+_FIN_WS = {}
+
+
+def _finalize_ws(device: torch.device) -> torch.Tensor:
+    """Zeroed once per (device, stream): per-block partials + the self-resetting arrival counter of
+    ``km_finalize`` (two streams must not share one)."""
+    key = (device, stream_ptr(device))
+    ws = _FIN_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(lib().ha_km_finalize_workspace()), dtype=torch.uint8, device=device)
+        _FIN_WS[key] = ws
+    return ws
+
+
+def kmeans_finalize(packed: Optional[torch.Tensor], C: torch.Tensor, sums: Optional[torch.Tensor] = None,
+                    counts: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Lloyd epilogue (``csrc/kmeans_finalize.hip``): from ``packed = [sums (k*f) | counts (k)]``
-    (fp64) and the current centroids C (float32, k x f) return (new centroids, squared shift as a
-    0-d fp64 tensor); empty clusters keep their centroid. One launch on the GPU."""
+    (fp64; or fp32 ``sums`` [k, f] and ``counts`` [k] with ``packed=None``) and the current
+    centroids C (float32, k x f) return (new centroids, squared shift as a 0-d fp64 tensor); empty
+    clusters keep their centroid. One launch on the GPU."""
     k, f = C.shape
-    if packed.is_cuda and C.dtype == torch.float32 and use_native(C) and hasattr(lib(), "ha_km_finalize"):
-        pk = packed.contiguous()
+    dev_in = packed if packed is not None else sums
+    if dev_in.is_cuda and C.dtype == torch.float32 and use_native(C) and hasattr(lib(), "ha_km_finalize_f32"):
         Cc = C if C.stride(-1) == 1 else C.contiguous()
         newC = torch.empty((k, f), dtype=torch.float32, device=C.device)
         shift = torch.empty((), dtype=torch.float64, device=C.device)
-        check(lib().ha_km_finalize(_ptr(pk), k, f, _ptr(Cc), Cc.stride(0), _ptr(newC), _ptr(shift),
-                                   ctypes.c_void_p(stream_ptr(C.device))), "ha_km_finalize")
+        ws = _finalize_ws(C.device)
+        s = ctypes.c_void_p(stream_ptr(C.device))
+        if packed is not None:
+            pk = packed.contiguous()
+            check(lib().ha_km_finalize(_ptr(pk), k, f, _ptr(Cc), Cc.stride(0), _ptr(newC), _ptr(shift), _ptr(ws), s),
+                  "ha_km_finalize")
+        else:
+            sc, cc = sums.float().contiguous(), counts.float().contiguous()
+            check(lib().ha_km_finalize_f32(_ptr(sc), _ptr(cc), k, f, _ptr(Cc), Cc.stride(0), _ptr(newC), _ptr(shift),
+                                           _ptr(ws), s), "ha_km_finalize_f32")
         return newC, shift
+    if packed is None:
+        packed = torch.cat([sums.reshape(-1).double(), counts.double()])
     kf = k * f
     gs = packed[:kf].reshape(k, f)
     gc = packed[kf:]

@@ -211,6 +211,33 @@ def test_kmeans_update(n, k, f):
     assert torch.equal(counts.double(), rc)
 
 
+@pytest.mark.parametrize("k,f,packed", [(3, 5, True), (3, 5, False), (1024, 64, True), (1024, 64, False),
+                                         (5000, 100, False), (7, 1, True)])
+def test_kmeans_finalize(k, f, packed):
+    """Native Lloyd epilogue vs fp64 torch: means, empty clusters keep their centroid, squared shift
+    (the last-block reduction resets its arrival counter: three launches in a row agree)."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(k * f)
+    C = torch.randn(k, f, generator=g).to(dev)
+    sums = (torch.randn(k, f, generator=g) * 50).to(dev)
+    counts = torch.randint(0, 40, (k,), generator=g).float().to(dev)
+    counts[0] = 0.0
+    ref = torch.where(counts.double().unsqueeze(1) > 0, sums.double() / counts.double().clamp(min=1).unsqueeze(1),
+                      C.double())
+    ref_shift = float(((C.double() - ref.float().double()) ** 2).sum())
+    for _ in range(3):
+        if packed:
+            pk = torch.cat([sums.reshape(-1).double(), counts.double()])
+            newC, shift = ops.kmeans_finalize(pk, C)
+        else:
+            newC, shift = ops.kmeans_finalize(None, C, sums=sums, counts=counts)
+        assert torch.allclose(newC.double(), ref, rtol=1e-6, atol=1e-6)
+        assert torch.equal(newC[0], C[0])
+        assert abs(float(shift) - ref_shift) <= 1e-9 * max(1.0, ref_shift)
+
+
 @pytest.mark.parametrize("shape,axis", [((10_000_003,), None), ((1000, 999), None), ((1000, 999), 0),
                                         ((1000, 999), 1), ((3, 1000, 4), 1), ((513, 1024), 0), ((7, 5), 1)])
 def test_moments(shape, axis):
