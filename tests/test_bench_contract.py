@@ -1,0 +1,44 @@
+"""bench.py contract on CPU: launched like the driver's multi-GPU run (torch.distributed.run, 2
+gloo ranks, rendezvous on 127.0.0.1), rank 0 prints exactly ONE JSON line with the required keys and
+the whole-job aggregate."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_lines(out):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_two_ranks_one_json_line():
+    env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--n-per-gpu", "3000", "--exact-steps", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["scaling"] == "weak" and rec["higher_is_better"] is True
+    assert rec["config"]["global_batch"] == 6000 and rec["config"]["parallelism"] == "dp2"
+    assert rec["extra"]["world_size_seen_by_rccl"] == 2
+    # whole-job aggregate: 2 n k f flops per step over the max-over-ranks step time
+    flops = 2 * 6000 * 1024 * 64
+    assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= 1e-6 * rec["value"]
