@@ -219,9 +219,16 @@ __global__ __launch_bounds__(KU_BLOCK) void ku_hist(const int* __restrict__ lab,
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
   const int64_t r1 = r0 + rows_per_blk < n ? r0 + rows_per_blk : n;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += KU_BLOCK) {
-    const int l = lab[i];
-    if ((unsigned)l < (unsigned)k) atomicAdd(&h[l], 1);
+  for (int64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += 4 * KU_BLOCK) {
+    int l[4];  // 4 label loads in flight per thread
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + (int64_t)u * KU_BLOCK;
+      l[u] = i < r1 ? lab[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((unsigned)l[u] < (unsigned)k) atomicAdd(&h[l[u]], 1);
   }
   __syncthreads();
   for (int e = threadIdx.x; e < k; e += KU_BLOCK) hist[(int64_t)blockIdx.x * k + e] = h[e];
@@ -289,9 +296,22 @@ __global__ __launch_bounds__(KU_BLOCK) void ku_scatter(const int* __restrict__ l
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
   const int64_t r1 = r0 + rows_per_blk < n ? r0 + rows_per_blk : n;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += KU_BLOCK) {
-    const int l = lab[i];
-    if ((unsigned)l < (unsigned)k) order[atomicAdd(&h[l], 1)] = (int)i;
+  // 4 rows per thread in flight: the label loads, then the (independent) LDS slot claims, then the
+  // stores, instead of one load -> atomic -> store chain per row
+  constexpr int U = 4;
+  for (int64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += U * KU_BLOCK) {
+    int l[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * KU_BLOCK;
+      l[u] = i < r1 ? lab[i] : -1;
+    }
+    int pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) pos[u] = (unsigned)l[u] < (unsigned)k ? atomicAdd(&h[l[u]], 1) : -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (pos[u] >= 0) order[pos[u]] = (int)(i0 + (int64_t)u * KU_BLOCK);
   }
 }
 
