@@ -1275,7 +1275,8 @@ def kmeans_finalize(packed: Optional[torch.Tensor], C: torch.Tensor, sums: Optio
     clusters keep their centroid. One launch on the GPU."""
     k, f = C.shape
     dev_in = packed if packed is not None else sums
-    if dev_in.is_cuda and C.dtype == torch.float32 and use_native(C) and hasattr(lib(), "ha_km_finalize_f32"):
+    if dev_in.is_cuda and C.dtype == torch.float32 and k * f < 2 ** 31 and use_native(C) and \
+            hasattr(lib(), "ha_km_finalize_f32"):
         Cc = C if C.stride(-1) == 1 else C.contiguous()
         newC = torch.empty((k, f), dtype=torch.float32, device=C.device)
         shift = torch.empty((), dtype=torch.float64, device=C.device)
