@@ -1,6 +1,8 @@
 """Singular value decomposition (the reference ships an empty placeholder, ``linalg/svd.py``).
 
-``svd`` here is a convenience: tall-skinny split-0 matrices use TSQR + a small local SVD of R."""
+``svd`` here is a convenience: tall-skinny split-0 matrices use TSQR + a small local SVD of R (U
+stays split 0), wide split-1 matrices the same on the transpose (V split 0); other layouts gather
+the matrix and run one local SVD."""
 from __future__ import annotations
 
 import torch
@@ -20,6 +22,16 @@ def svd(a: DNDarray, full_matrices: bool = False, compute_uv: bool = True):
         raise ValueError("svd requires a 2-D DNDarray")
     if full_matrices:
         raise NotImplementedError("full_matrices=True is not supported")
+    if a.is_distributed() and a.split == 1 and a.gshape[1] > a.gshape[0]:
+        # wide, split along the long axis: A^T is tall-skinny split 0 (a local transpose), and
+        # A^T = U' S V'^T gives A = V' S U'^T - no gather of A
+        from .basics import transpose
+
+        res = svd(transpose(a), full_matrices=False, compute_uv=compute_uv)
+        if not compute_uv:
+            return res
+        u2, s2, v2 = res
+        return v2, s2, u2
     if a.is_distributed() and a.split == 0 and a.gshape[0] >= a.gshape[1]:
         q, r = qr(a)
         rt = r._gathered() if r.is_distributed() else r.larray

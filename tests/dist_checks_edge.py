@@ -429,3 +429,28 @@ def check_qr_split1_panels():
             assert np.all(np.diag(rn) >= 0)
             _, r_only = ht.linalg.qr(ht.array(a, split=1), mode="reduced", calc_q=False)
             assert np.allclose(r_only.numpy(), rn, atol=1e-10)
+
+
+def check_svd_layouts():
+    """svd: tall split 0 (TSQR + SVD of R), wide split 1 (the same on the transpose), gathered
+    otherwise; singular values vs NumPy, U S V^T reconstructs A, U and V orthonormal."""
+    rng = np.random.default_rng(5)
+    for shp, split in [((40, 6), 0), ((6, 40), 1), ((40, 6), None), ((12, 9), 1), ((9, 12), 0)]:
+        a_np = rng.standard_normal(shp)
+        a = ht.array(a_np, split=split)
+        s_only = ht.linalg.svd(a, compute_uv=False)
+        np.testing.assert_allclose(s_only.numpy(), np.linalg.svd(a_np, compute_uv=False), rtol=1e-10, atol=1e-10)
+        u, s, v = ht.linalg.svd(a)
+        un, sn, vn = u.numpy(), s.numpy(), v.numpy()
+        r = min(shp)
+        assert un.shape == (shp[0], r) and vn.shape == (shp[1], r) and sn.shape == (r,)
+        np.testing.assert_allclose(sn, np.linalg.svd(a_np, compute_uv=False), rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose((un * sn) @ vn.T, a_np, rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(un.T @ un, np.eye(r), atol=1e-9)
+        np.testing.assert_allclose(vn.T @ vn, np.eye(r), atol=1e-9)
+    raises_ok = False
+    try:
+        ht.linalg.svd(ht.zeros((2, 3, 4)))
+    except ValueError:
+        raises_ok = True
+    assert raises_ok
