@@ -80,10 +80,11 @@ class KMeans(_KCluster):
         if os.environ.get("HEAT_KMEANS_GRAPH", "0") != "1" or not X.is_cuda:
             return False
         # Measured on MI355X / ROCm 7 (tools/microbench/graph_debug2.py): with the runtime's graph
-        # packet capture (the default), the second and later replays read stale data written by
-        # earlier nodes (update sums off, centroids diverge to 1e27); with
-        # DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 replays are exact. The variable is read at HIP init, so
-        # graph mode is only taken when the process was started with it.
+        # packet capture (the default), replays of a step containing a 256 KB memset node went wrong
+        # from the second replay (centroids diverged to 1e27); with
+        # DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 they were exact. The update kernels no longer memset
+        # (profiles/kmeans_graph_replay_r02.md), but graph mode stays restricted to processes
+        # started with that variable (read at HIP init): it is correct there and not faster.
         if os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
             return False
         if self._certify or self._cert_probe is not None:

@@ -213,8 +213,12 @@ constexpr int KU_CHUNK = 2048;     // sorted positions per gather workgroup
 constexpr int KU_RU = 8;           // rows in flight per gather thread
 
 __global__ __launch_bounds__(KU_BLOCK) void ku_hist(const int* __restrict__ lab, int64_t n, int k,
-                                                    int64_t rows_per_blk, int* __restrict__ hist) {
+                                                    int64_t rows_per_blk, int* __restrict__ hist,
+                                                    float* __restrict__ sums, int64_t nsums) {
   extern __shared__ int h[];
+  // zero the sums the gather pass accumulates into (instead of a separate memset launch)
+  for (int64_t e = (int64_t)blockIdx.x * KU_BLOCK + threadIdx.x; e < nsums; e += (int64_t)gridDim.x * KU_BLOCK)
+    sums[e] = 0.f;
   for (int e = threadIdx.x; e < k; e += KU_BLOCK) h[e] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
@@ -536,8 +540,8 @@ HA_EXPORT int ha_km_update(const float* X, int64_t n, int f, int64_t ldx, const 
   (void)num_cus;
   hipStream_t s = (hipStream_t)stream;
   if (ha_km_update_workspace(n, k, f, num_cus) < 0) return HA_UNSUPPORTED;
-  hipMemsetAsync(sums, 0, sizeof(float) * (size_t)k * f, s);
   if (n <= 0) {
+    hipMemsetAsync(sums, 0, sizeof(float) * (size_t)k * f, s);
     hipMemsetAsync(counts, 0, sizeof(float) * (size_t)k, s);
     return ha_launch_status();
   }
@@ -552,7 +556,8 @@ HA_EXPORT int ha_km_update(const float* X, int64_t n, int f, int64_t ldx, const 
     hipFuncSetAttribute((const void*)ku_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncSetAttribute((const void*)ku_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   }
-  hipLaunchKernelGGL(ku_hist, dim3((unsigned)nblk), dim3(KU_BLOCK), lds, s, labels, n, k, rows, hist);
+  hipLaunchKernelGGL(ku_hist, dim3((unsigned)nblk), dim3(KU_BLOCK), lds, s, labels, n, k, rows, hist, sums,
+                     (int64_t)k * f);
   hipLaunchKernelGGL(ku_scan_blk, dim3((k + 255) / 256), dim3(256), 0, s, hist, (int)nblk, k, total);
   hipLaunchKernelGGL(ku_scan_tot, dim3(1), dim3(1024), 0, s, total, k, cstart, counts);
   hipLaunchKernelGGL(ku_scatter, dim3((unsigned)nblk), dim3(KU_BLOCK), lds, s, labels, n, k, rows, hist, cstart,
