@@ -111,6 +111,7 @@ def main():
             dte = comm.allreduce(dte, ht.MPI.MAX) if comm.size > 1 else dte
             extra["exact_ms_per_step"] = dte / args.exact_steps * 1e3
             extra["exact_gflops_fp32"] = flops / (extra["exact_ms_per_step"] * 1e-3) / 1e9
+        extra.update(validate_kmeans(km, x, comm, k))
         if args.with_reference:
             extra["reference_impl_ms"] = reference_iteration(x, km, k)
             extra["speedup_vs_reference_impl"] = extra["reference_impl_ms"] / ms
@@ -145,6 +146,7 @@ def main():
                "global_batch": n, "seq_len": f, "parallelism": "dp{}".format(n_gpus)}
         extra["flop_convention"] = "2*n*n*f (the distance GEMM of the quadratic expansion)"
         extra["distances_per_s"] = n * n / (ms * 1e-3)
+        extra.update(validate_cdist(x, comm))
         scaling = "strong"
     else:
         args.n_per_gpu = args.n_per_gpu or 1_000_000_000
@@ -162,6 +164,7 @@ def main():
         ms = rank_times(comm, dt, args.steps, extra)
         value = 2 * n * 4 / (ms * 1e-3) / 1e9
         metric, unit = "moments_GB_per_s", "GB/s"
+        extra.update(validate_moments(x, m, v, comm))
         cfg = {"model": "mean+var float32 split=0", "global_batch": n, "seq_len": 1,
                "parallelism": "dp{}".format(n_gpus)}
     if args.workload == "kmeans" and args.precision == "fast":
@@ -172,6 +175,99 @@ def main():
                "vs_baseline": None, "dtype": "fp32", "data": "synthetic (device Threefry normal samples)",
                "config": cfg, "extra": extra}
         print(json.dumps(out), flush=True)
+
+
+def validate_kmeans(km, x, comm, k: int) -> dict:
+    """Self-check of the distributed step, outside the timed region: one more Lloyd step, then
+    (1) its centroids recomputed in fp64 from its labels (index_add over the local points + one
+    all-reduce) against the kernel path's centroids, (2) the all-reduced cluster counts summing to
+    n, (3) a centroid checksum identical on every rank (MAX == MIN over the ranks), and (4) the
+    time of the packed (k*f + k) fp64 all-reduce alone."""
+    import heat_amd as ht
+
+    X = x.larray
+    c_prev = km.cluster_centers_.larray.clone()
+    km.step(x)
+    lab = km._last_labels.reshape(-1).long()
+    c_new = km.cluster_centers_.larray
+    f = X.shape[1]
+    packed = torch.zeros(k * f + k, dtype=torch.float64, device=X.device)
+    sums = packed[: k * f].view(k, f)
+    sums.index_add_(0, lab, X.double())
+    packed[k * f:].index_add_(0, lab, torch.ones_like(lab, dtype=torch.float64))
+    if comm.size > 1:
+        comm.Allreduce(ht.MPI.IN_PLACE, packed, ht.MPI.SUM)
+    counts = packed[k * f:]
+    ref = torch.where(counts.unsqueeze(1) > 0, sums / counts.clamp(min=1).unsqueeze(1), c_prev.double())
+    scale = float(ref.abs().max()) or 1.0
+    err = float((c_new.double() - ref).abs().max()) / scale
+    chk = float((c_new.double() * torch.arange(1, c_new.numel() + 1, device=X.device,
+                                                dtype=torch.float64).view_as(c_new)).sum())
+    hi = comm.allreduce(chk, ht.MPI.MAX) if comm.size > 1 else chk
+    lo = comm.allreduce(chk, ht.MPI.MIN) if comm.size > 1 else chk
+    buf = torch.ones(k * f + k, dtype=torch.float64, device=X.device)
+    reps = 20
+    for _ in range(3):
+        comm.Allreduce(ht.MPI.IN_PLACE, buf, ht.MPI.SUM)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    comm.Barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        comm.Allreduce(ht.MPI.IN_PLACE, buf, ht.MPI.SUM)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / reps * 1e6
+    us = comm.allreduce(us, ht.MPI.MAX) if comm.size > 1 else us
+    return {"centroids_agree": hi == lo, "count_sum_ok": int(round(float(counts.sum()))) == x.gshape[0],
+            "centroid_max_rel_err_vs_fp64": err, "allreduce_us": us,
+            "allreduce_bytes": buf.numel() * buf.element_size()}
+
+
+def validate_moments(x, m, v, comm) -> dict:
+    """Global mean / variance of the timed calls against an fp64 recompute (chunked sums over the
+    local block + all-reduce), outside the timed region."""
+    import heat_amd as ht
+
+    X = x.larray.reshape(-1)
+    step = 1 << 27
+    s = torch.zeros(2, dtype=torch.float64, device=X.device)
+    for i in range(0, X.numel(), step):
+        s[0] += X[i: i + step].sum(dtype=torch.float64)
+    if comm.size > 1:
+        comm.Allreduce(ht.MPI.IN_PLACE, s, ht.MPI.SUM)
+    n = x.gnumel
+    mu = s[0] / n
+    for i in range(0, X.numel(), step):
+        s[1] += ((X[i: i + step].double() - mu) ** 2).sum()
+    q = s[1:].clone()
+    if comm.size > 1:
+        comm.Allreduce(ht.MPI.IN_PLACE, q, ht.MPI.SUM)
+    var = float(q[0]) / n
+    return {"mean_abs_err_vs_fp64": abs(float(m.item()) - float(mu)),
+            "var_rel_err_vs_fp64": abs(float(v.item()) - var) / max(abs(var), 1e-300)}
+
+
+def validate_cdist(x, comm) -> dict:
+    """Distances of a 4096-row sample (through ht.spatial.cdist, the same kernels) against fp64:
+    the error of the SQUARED distances relative to |x|^2 + |y|^2 (the quadratic expansion's
+    cancellation scale; near-zero distances have no relative accuracy in any fp32 expansion)."""
+    import heat_amd as ht
+
+    sub = x[:4096]
+    d = ht.spatial.cdist(sub, sub, quadratic_expansion=True).larray
+    loc = sub.resplit_(None).larray if sub.is_distributed() else sub.larray
+    L = loc.double()
+    ref = torch.cdist(L, L)
+    nrm = (L * L).sum(1)
+    rows = d.shape[0]
+    off = 0 if not x.is_distributed() else sum(comm.allgather(rows)[: comm.rank])
+    err = 0.0
+    if rows:
+        scale = nrm[off: off + rows].unsqueeze(1) + nrm.unsqueeze(0)
+        err = float(((d.double() ** 2 - ref[off: off + rows] ** 2).abs() / scale).max())
+    err = comm.allreduce(err, ht.MPI.MAX) if comm.size > 1 else err
+    return {"sample_max_sq_err_rel_vs_fp64": err}
 
 
 def rccl_world_size(comm) -> int:

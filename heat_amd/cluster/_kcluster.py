@@ -95,6 +95,10 @@ class _KCluster(ClusteringMixin, BaseEstimator):
 
     @property
     def inertia_(self) -> float:
+        # step() with tol=None keeps the shift as a device scalar (no host sync per step); the
+        # property hands out the float the reference returns
+        if self._inertia is not None and not isinstance(self._inertia, float):
+            self._inertia = float(self._inertia)
         return self._inertia
 
     @property

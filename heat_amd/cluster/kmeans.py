@@ -91,7 +91,13 @@ class KMeans(_KCluster):
             return False
         if self.precision == "fast" and (self._pack_cache is None or self._pack_cache.key != ops.kernels._points_key(X)):
             return False  # the fp16x3 planes are (re)built eagerly, outside any capture
-        return not distributed or comm._native() is not None
+        if not distributed:
+            return True
+        # a captured IPC all-reduce would freeze its host-side epoch and slot parity into the graph:
+        # every replay would pass its barriers on flags of earlier replays (wrong sums)
+        from ..parallel import ipc
+
+        return not ipc.enabled() and comm._native() is not None
 
     def _centroid_step_graph(self, X: torch.Tensor, C: torch.Tensor, comm, distributed: bool):
         """The Lloyd step replayed from a captured HIP graph: ONE launch per iteration instead of
@@ -117,9 +123,10 @@ class KMeans(_KCluster):
         c_in.copy_(C)
         g.replay()
         self._step_shift = shift.clone()
-        return c_out.clone(), labels
+        # the graph's buffers are overwritten by the next replay: hand out copies
+        return c_out.clone(), labels.clone()
 
-    def step(self, x: DNDarray) -> float:
+    def step(self, x: DNDarray) -> Union[float, torch.Tensor]:
         """One Lloyd iteration on the current centers (initialising them on first use); returns
         the squared centroid shift (a float, or a 0-d device tensor when ``tol`` is None). The
         building block of :meth:`fit`, exposed for streaming use and benchmarking."""

@@ -534,8 +534,9 @@ def save_netcdf(data: DNDarray, path: str, variable: str, mode: str = "w", dimen
                 try:
                     with nc.Dataset(path, "r+") as handle:
                         var = handle[variable]
-                        target = np.empty(0)  # shape probe of the addressed region
-                        full = _file_region(var.shape, key, data.gshape)
+                        dims = var.dimensions
+                        record = bool(dims) and handle.dimensions[dims[0]].isunlimited()
+                        full = _file_region(var.shape, key, data.gshape, record=record)
                         var[_sub_region(full, data, lsl)] = local
                 except Exception as e:
                     exc = e

@@ -16,7 +16,8 @@ from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
-           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "householder_qr",
+           "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "h3_planes", "H3Planes",
+           "gemm_h3_planes", "householder_qr",
            "householder_factor", "householder_apply", "householder_block",
            "radix_sort_supported", "sort_rows"]
 
@@ -874,20 +875,25 @@ def _gemm_operand(t: torch.Tensor, contig_dim: int):
     return t, t.stride(0) if contig_dim == 1 else t.stride(1), contig_dim == 0
 
 
-_GEMM_BK = int(os.environ.get("HEAT_GEMM_VARIANT", "4"))  # exact GEMM block: 2 = 128x128, 4 = 128x256
+_GEMM_BK = int(os.environ.get("HEAT_GEMM_VARIANT", "4"))  # 128-tile exact GEMM block: 2 = 128x128, 4 = 128x256
+_HA_UNSUPPORTED = 2
 
 
 def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
-             accumulate: bool = False) -> torch.Tensor:
-    """Exact fp32 ``a @ b`` on the f32-input matrix cores (``csrc/gemm_mfma.hip``): fp32 products
-    and accumulation in k order like any fp32 GEMM, every operand layout (row-/column-major views
-    such as ``x.T @ x``) without a copy, 64-bit offsets (no 4 GB operand limit). ``out``: a
-    row-major fp32 [M, N] view (e.g. a row block of a larger result); ``accumulate`` adds into it."""
+             accumulate: bool = False, alpha: float = 1.0) -> torch.Tensor:
+    """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on the f32-input matrix cores:
+    fp32 products and accumulation in k order like any fp32 GEMM, every operand layout
+    (row-/column-major views such as ``x.T @ x``) without a copy, 64-bit offsets (no 4 GB operand
+    limit). The 256 x 256-tile pipelined kernel (``csrc/gemm_tiled.hip: gemm_f32t``) takes
+    16-byte-aligned operands whose contiguous extents are multiples of 4; anything else runs on
+    the 128-tile kernel (``csrc/gemm_mfma.hip``). ``out``: a row-major fp32 [M, N] view (e.g. a
+    row block of a larger result)."""
     if not (a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32 \
             or a.dim() != 2 or b.dim() != 2:
+        res = alpha * (a @ b) if alpha != 1.0 else a @ b
         if out is None:
-            return a @ b
-        return out.add_(a @ b) if accumulate else torch.mm(a, b, out=out)
+            return res
+        return out.add_(res) if accumulate else out.copy_(res)
     M, K = a.shape
     N = b.shape[1]
     if b.shape[0] != K:
@@ -903,37 +909,104 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
         return out if accumulate else out.zero_()
     A, lda, a_km = _gemm_operand(a, 1)      # row-major: k contiguous; k-major: m contiguous
     B, ldb, b_nm = _gemm_operand(b, 1)      # k-major: n contiguous; n-major: k contiguous
-    check(lib().ha_gemm_f32(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, out.stride(0) if M > 1 else N,
-                            int(a_km), int(b_nm), int(accumulate), _GEMM_BK, ctypes.c_void_p(stream_ptr(a.device))),
-          "ha_gemm_f32")
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(a.device))
+    ldc = out.stride(0) if M > 1 else N
+    rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(not b_nm),
+                        float(alpha), int(accumulate), st)
+    if rc == _HA_UNSUPPORTED:
+        if alpha != 1.0:
+            tmp = gemm_f32(a, b)
+            return out.add_(tmp, alpha=alpha) if accumulate else torch.mul(tmp, alpha, out=out)
+        rc = L.ha_gemm_f32(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(b_nm),
+                           int(accumulate), _GEMM_BK, st)
+    check(rc, "ha_gemm_f32")
     return out
 
 
-def _h3_rows(X: torch.Tensor, Kp: int):
-    """fp16 hi/lo planes [R, Kp] (zero tail) + int32 row exponents of a row-major fp32 matrix X
-    [R, K], and the device non-finite flag."""
-    R, K = X.shape
-    if K % 4 != 0 or X.stride(1) != 1 or X.stride(0) % 4 != 0 or X.data_ptr() % 16 != 0:
-        X = F.pad(X.contiguous(), (0, Kp - K)) if K % 4 else X.contiguous()
-        K = X.shape[1]
-    hi = torch.empty((R, Kp), dtype=torch.float16, device=X.device)
-    lo = torch.empty((R, Kp), dtype=torch.float16, device=X.device)
-    if Kp > K:
-        hi[:, K:].zero_()
-        lo[:, K:].zero_()
-    ex = torch.empty(R, dtype=torch.int32, device=X.device)
-    flag = torch.zeros(1, dtype=torch.int32, device=X.device)
-    check(lib().ha_split3_rows(_ptr(X), R, K, X.stride(0), _ptr(hi), _ptr(None), _ptr(lo), Kp, _ptr(ex), _ptr(flag),
-                               ctypes.c_void_p(stream_ptr(X.device))), "ha_split3_rows")
-    return hi, lo, ex, flag
+class H3Planes(NamedTuple):
+    """fp16 hi/lo planes of one GEMM operand in the K8-panel layout [Kp/8][Rp][8] (rows = the
+    operand's non-contracted dimension, padded to 256; K padded to 16; zero padding), int32
+    power-of-two row exponents [Rp], and the device inf/nan flag."""
+    hi: torch.Tensor
+    lo: torch.Tensor
+    ex: torch.Tensor
+    flag: torch.Tensor
+    rows: int
+    Rp: int
+    Kp: int
 
 
-def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """fp32 ``a @ b`` by the FUSED fp16x3 MFMA kernel (``csrc/gemm_mfma.hip: gemm_h3``): row
-    scaled hi/lo planes of ``a`` and of ``b^T``, one kernel forming hi.hi + hi.lo + lo.hi with fp32
-    accumulation and the exact power-of-two unscale in its epilogue. Accuracy of an fp32 GEMM
-    (see :func:`gemm_f16x3`). Returns None for non-finite operands (the caller falls back; the
+def h3_planes(x: torch.Tensor, contract_dim: int) -> H3Planes:
+    """Split a 2-D fp32 GEMM operand for :func:`gemm_h3`: ``contract_dim`` is the dimension summed
+    over (1 for the left operand A[M, K], 0 for the right operand B[K, N]); the other dimension
+    gets one power-of-two scale per index (``csrc/gemm_tiled.hip: tg_split_rows / tg_split_cols``:
+    one read of x, fully coalesced plane writes)."""
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(x.device))
+    rows_dim = 1 - contract_dim
+    R, K = x.shape[rows_dim], x.shape[contract_dim]
+    Rp, Kp = max(256, (R + 255) // 256 * 256), max(16, (K + 15) // 16 * 16)
+    hi = torch.empty((Kp // 8, Rp, 8), dtype=torch.float16, device=x.device)
+    lo = torch.empty_like(hi)
+    ex = torch.empty(Rp, dtype=torch.int32, device=x.device)
+    flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+    # physical layout: rows of the operand contiguous along k ("rows" split) or along rows ("cols")
+    if x.stride(contract_dim) == 1 and x.stride(rows_dim) >= max(1, K):
+        P = x if contract_dim == 1 else x.t()           # [R][K], unit stride along K
+        check(L.ha_h3_split_rows(_ptr(P), R, K, P.stride(0), Rp, Kp, _ptr(hi), _ptr(lo), _ptr(ex), _ptr(flag), st),
+              "ha_h3_split_rows")
+    else:
+        P = x.t() if contract_dim == 1 else x           # [K][R], unit stride along R
+        if P.stride(1) != 1 or P.stride(0) < max(1, R):
+            P = P.contiguous()
+        mx = torch.empty(R, dtype=torch.float32, device=x.device)
+        check(L.ha_split_absmax(_ptr(P), K, R, P.stride(0), 1, _ptr(mx), _ptr(flag), st), "ha_split_absmax")
+        check(L.ha_h3_split_cols(_ptr(P), K, R, P.stride(0), Rp, Kp, _ptr(mx), _ptr(hi), _ptr(lo), _ptr(ex), st),
+              "ha_h3_split_cols")
+    return H3Planes(hi, lo, ex, flag, R, Rp, Kp)
+
+
+def gemm_h3_planes(pa: H3Planes, pb: H3Planes, out: torch.Tensor, alpha: float = 1.0, accumulate: bool = False):
+    """``out (+)= alpha * A @ B`` from pre-split operands (see :func:`h3_planes`)."""
+    if pa.Kp != pb.Kp:
+        raise ValueError("gemm_h3_planes: contraction lengths differ")
+    M, N = pa.rows, pb.rows
+    check(lib().ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(out),
+                            M, N, pa.Kp, pa.Rp, pb.Rp, out.stride(0) if M > 1 else N, float(alpha), int(accumulate),
+                            ctypes.c_void_p(stream_ptr(out.device))), "ha_gemm_h3t")
+    return out
+
+
+def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
+            accumulate: bool = False) -> Optional[torch.Tensor]:
+    """fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) by the fused fp16x3 MFMA kernel
+    (``csrc/gemm_tiled.hip: gemm_h3t``): power-of-two scaled fp16 hi/lo planes of both operands,
+    one 256 x 256-tile kernel forming hi.hi + hi.lo + lo.hi with fp32 accumulation and the exact
+    unscale in its epilogue. Accuracy of an fp32 GEMM (errors <= ~2^-21 |a||b| per product).
+    ``x.T @ x`` splits x once. Returns None for non-finite operands (the caller falls back; the
     check is one host sync)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.zeros((M, N), dtype=torch.float32, device=a.device) if accumulate else \
+            torch.empty((M, N), dtype=torch.float32, device=a.device)
+    elif out.shape != (M, N) or out.dtype != torch.float32 or (N > 1 and out.stride(1) != 1):
+        raise ValueError("gemm_h3: out must be a row-major float32 [M, N] tensor")
+    if M == 0 or N == 0:
+        return out
+    if K == 0:
+        return out if accumulate else out.zero_()
+    pa = h3_planes(a, 1)
+    pb = pa if _is_gram(a, b) else h3_planes(b, 0)
+    if int((pa.flag + pb.flag).item()) != 0:
+        return None
+    return gemm_h3_planes(pa, pb, out, alpha, accumulate)
+
+
+def gemm_h3_v1(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """The round-2 128 x 128-tile fused fp16x3 kernel (``csrc/gemm_mfma.hip: gemm_h3``), kept for
+    the A/B benchmark (``tools/microbench/gemm_bench.py``)."""
     M, K = a.shape
     N = b.shape[1]
     Kp = (K + 31) // 32 * 32
@@ -948,6 +1021,38 @@ def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     check(lib().ha_gemm_h3(_ptr(ahi), _ptr(alo), _ptr(bhi), _ptr(blo), _ptr(ea), _ptr(eb), _ptr(out), M, N, Kp,
                            out.stride(0) if M > 1 else N, ctypes.c_void_p(stream_ptr(a.device))), "ha_gemm_h3")
     return out
+
+
+def gemm_f32_v1(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The round-2 128-tile exact fp32 kernel (``csrc/gemm_mfma.hip: gemm_f32``), for A/B benches."""
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    A, lda, a_km = _gemm_operand(a, 1)
+    B, ldb, b_nm = _gemm_operand(b, 1)
+    check(lib().ha_gemm_f32(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, out.stride(0) if M > 1 else N,
+                            int(a_km), int(b_nm), 0, _GEMM_BK, ctypes.c_void_p(stream_ptr(a.device))), "ha_gemm_f32")
+    return out
+
+
+def _h3_rows(X: torch.Tensor, Kp: int):
+    """fp16 hi/lo planes [R, Kp] (zero tail) + int32 row exponents of a row-major fp32 matrix X
+    [R, K], and the device non-finite flag (the round-2 kernel's row-major plane layout)."""
+    R, K = X.shape
+    if K % 4 != 0 or X.stride(1) != 1 or X.stride(0) % 4 != 0 or X.data_ptr() % 16 != 0:
+        X = F.pad(X.contiguous(), (0, Kp - K)) if K % 4 else X.contiguous()
+        K = X.shape[1]
+    hi = torch.empty((R, Kp), dtype=torch.float16, device=X.device)
+    lo = torch.empty((R, Kp), dtype=torch.float16, device=X.device)
+    if Kp > K:
+        hi[:, K:].zero_()
+        lo[:, K:].zero_()
+    ex = torch.empty(R, dtype=torch.int32, device=X.device)
+    flag = torch.zeros(1, dtype=torch.int32, device=X.device)
+    check(lib().ha_split3_rows(_ptr(X), R, K, X.stride(0), _ptr(hi), _ptr(None), _ptr(lo), Kp, _ptr(ex), _ptr(flag),
+                               ctypes.c_void_p(stream_ptr(X.device))), "ha_split3_rows")
+    return hi, lo, ex, flag
 
 
 # --------------------------------------------------------------------------------------------- Householder QR

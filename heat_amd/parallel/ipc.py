@@ -153,6 +153,10 @@ class IpcAllreduce:
         counts_bytes = [int(c) for c in counts_bytes]
         if any(c % 4 or c > self.capacity for c in counts_bytes) or not t.is_contiguous() or not t.is_cuda:
             return None
+        if sum(counts_bytes) == 0:
+            # nothing to move and no kernel: the epoch must not advance, since the two-slot reuse
+            # argument needs a barrier between consecutive epochs
+            return torch.empty(0, dtype=torch.uint8, device=t.device)
         self._poll()
         self.epoch += 1
         words = [c // 4 for c in counts_bytes]
@@ -176,6 +180,8 @@ class IpcAllreduce:
         call's own output is NaN-poisoned, so a silent wrong sum is impossible either way."""
         if not self.supports(t):
             raise ValueError("tensor not supported by the IPC all-reduce")
+        if t.numel() == 0:
+            return t  # no kernel launches for an empty payload: keep the epoch (see allgather)
         self._poll()
         self.epoch += 1
         es = t.element_size()

@@ -204,3 +204,25 @@ def test_save_netcdf_exception():
     raises(TypeError, ht.save_netcdf, data, p, "data", dimension_names=1)
     raises(ValueError, ht.save_netcdf, data, p, "data", dimension_names=["a", "b"])
     raises(ValueError, ht.save_netcdf, data, p, "data", mode="x")
+
+
+def test_remove_folder():
+    """The reference's (commented-out) clean-up check ``test_io.py:624-629``: after saving into a
+    scratch folder every rank can see the file, and once all ranks passed a barrier rank 0 removes
+    the folder, which then no longer exists for anyone."""
+    comm = ht.MPI_WORLD
+    base = os.path.join(tempfile.gettempdir(), "heat_amd_rmdir_{}".format(os.environ.get("MASTER_PORT", os.getpid())))
+    if comm.rank == 0:
+        os.makedirs(base, exist_ok=True)
+    comm.Barrier()
+    path = os.path.join(base, "x.csv")
+    ht.save_csv(ht.arange(12, dtype=ht.float32, split=0).reshape((4, 3)), path) if hasattr(ht, "save_csv") else \
+        ht.save(ht.arange(12, dtype=ht.float32, split=0).reshape((4, 3)), path)
+    comm.Barrier()
+    assert os.path.exists(path)
+    comm.Barrier()
+    if comm.rank == 0:
+        os.remove(path)
+        os.rmdir(base)
+    comm.Barrier()
+    assert not os.path.exists(base)

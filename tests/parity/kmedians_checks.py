@@ -5,5 +5,32 @@ import heat_amd as ht
 
 from ._ml import kcluster_suite
 
-(test_clusterer, test_get_and_set_params, test_fit_iris_unsplit, test_exceptions,
- test_spherical_clusters) = kcluster_suite(ht.cluster.KMedians, {"n_clusters": 8, "init": "random", "max_iter": 300, "tol": 1e-4, "random_state": None})
+_SUITE = kcluster_suite(ht.cluster.KMedians, {"n_clusters": 8, "init": "random", "max_iter": 300, "tol": 1e-4, "random_state": None})
+_REF = "heat/cluster/tests/test_kmedians.py"
+
+
+def test_clusterer():
+    """KMedians is a clusterer and not a classifier/regressor (reference ``test_kmedians.py``)."""
+    _SUITE[0]()
+
+
+def test_get_and_set_params():
+    """Default parameters, set_params round trip (reference ``test_kmedians.py``)."""
+    _SUITE[1]()
+
+
+def test_fit_iris_unsplit():
+    """Iris fits with both initialisations, unsplit and split 0: centres of the right shape, labels
+    in range, fitted clusters covering the data (reference ``test_kmedians.py``)."""
+    _SUITE[2]()
+
+
+def test_exceptions():
+    """Split-1 input and bad initial centres raise (reference ``test_kmedians.py``)."""
+    _SUITE[3]()
+
+
+def test_spherical_clusters():
+    """Four well-separated spherical clusters (float32 / float64 / int32) are recovered: every
+    centre within one cluster radius of the truth (reference ``test_kmedians.py``)."""
+    _SUITE[4]()

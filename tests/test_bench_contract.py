@@ -24,10 +24,14 @@ def _json_lines(out):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-def test_bench_two_ranks_one_json_line():
+import pytest
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_multi_rank_one_json_line(ranks):
     env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks), "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(ranks), "--steps", "2", "--warmup", "1",
            "--n-per-gpu", "3000", "--exact-steps", "0"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -35,10 +39,33 @@ def test_bench_two_ranks_one_json_line():
     assert len(lines) == 1, r.stdout
     rec = lines[0]
     assert KEYS <= set(rec)
-    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["n_gpus"] == ranks and rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["scaling"] == "weak" and rec["higher_is_better"] is True
-    assert rec["config"]["global_batch"] == 6000 and rec["config"]["parallelism"] == "dp2"
-    assert rec["extra"]["world_size_seen_by_rccl"] == 2
+    assert rec["config"]["global_batch"] == 3000 * ranks and rec["config"]["parallelism"] == "dp%d" % ranks
+    assert rec["extra"]["world_size_seen_by_rccl"] == ranks
+    # self-validation of the distributed step (outside the timed region)
+    assert rec["extra"]["centroids_agree"] is True
+    assert rec["extra"]["count_sum_ok"] is True
+    assert rec["extra"]["centroid_max_rel_err_vs_fp64"] < 1e-5
+    assert rec["extra"]["allreduce_us"] > 0
     # whole-job aggregate: 2 n k f flops per step over the max-over-ranks step time
-    flops = 2 * 6000 * 1024 * 64
+    flops = 2 * 3000 * ranks * 1024 * 64
     assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= 1e-6 * rec["value"]
+
+
+@pytest.mark.parametrize("workload", ["moments", "cdist"])
+def test_bench_secondary_workloads_validate(workload):
+    env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    extra_args = ["--n-per-gpu", "100000"] if workload == "moments" else ["--rows", "6000", "--f", "8"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--workload", workload] + extra_args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    ex = lines[0]["extra"]
+    if workload == "moments":
+        assert ex["mean_abs_err_vs_fp64"] < 1e-5 and ex["var_rel_err_vs_fp64"] < 1e-5
+    else:
+        assert ex["sample_max_sq_err_rel_vs_fp64"] < 1e-5

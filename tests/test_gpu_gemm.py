@@ -95,3 +95,75 @@ def test_gemm_h3_fused(m, k, n, scale):
     # layouts: a column-major view and a k-contiguous b
     c2 = ops.gemm_h3(a.t().contiguous().t(), b.t().contiguous().t())
     assert torch.equal(c, c2)
+
+
+# ----------------------------------------------------------------- 256-tile kernels (gemm_tiled.hip)
+@pytest.mark.parametrize("m,k,n", [(256, 16, 256), (300, 260, 516), (1000, 33, 4), (4, 4, 4), (513, 1024, 257),
+                                   (2048, 20, 300), (8, 4096, 1200)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+def test_gemm_f32t_layouts_tails(m, k, n, layout):
+    """Exact 256-tile kernel: every layout, K tails (K % 16 != 0 is zeroed in LDS), clamped edge
+    rows / columns, against fp64 with the fp32-GEMM bound."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + 5 * k + 11 * n)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    c = ops.gemm_f32(A, B)
+    ref = a.double() @ b.double()
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
+
+
+def test_gemm_f32t_exact_integers_and_alpha_beta():
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(3)
+    a = torch.randint(-8, 9, (600, 272), generator=g).float().to(dev)
+    b = torch.randint(-8, 9, (272, 520), generator=g).float().to(dev)
+    ref = (a.double() @ b.double()).float()
+    assert torch.equal(ops.gemm_f32(a, b), ref)
+    c = torch.full((600, 520), 3.0, device=dev)
+    ops.gemm_f32(a, b, out=c, accumulate=True, alpha=-1.0)
+    assert torch.equal(c, 3.0 - ref)
+
+
+@pytest.mark.parametrize("m,k,n", [(256, 16, 256), (300, 260, 516), (1000, 33, 5), (1, 7, 1), (513, 1024, 257),
+                                   (4099, 130, 65)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+def test_gemm_h3t_layouts(m, k, n, layout):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + 3 * k + 7 * n + len(layout))
+    a = (torch.randn(m, k, generator=g) * torch.logspace(-5, 5, m).unsqueeze(1)).to(dev)
+    b = (torch.randn(k, n, generator=g) * torch.logspace(3, -3, n).unsqueeze(0)).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    c = ops.gemm_h3(A, B)
+    ref = a.double() @ b.double()
+    bound = 8 * k * 2.0 ** -24 * (a.abs().double() @ b.abs().double()) + 1e-300
+    assert torch.all((c.double() - ref).abs() <= bound), ((c.double() - ref).abs() / bound).max()
+
+
+def test_gemm_h3t_gram_alpha_accumulate_and_nonfinite():
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(5000, 300, generator=g).to(dev)
+    gram = ops.gemm_h3(x.t(), x)
+    ref = x.double().t() @ x.double()
+    bound = 8 * 5000 * 2.0 ** -24 * (x.abs().double().t() @ x.abs().double())
+    assert torch.all((gram.double() - ref).abs() <= bound)
+    c = torch.ones(5000, 300, device=dev)
+    ops.gemm_h3(x, gram, out=c, alpha=-0.5, accumulate=True)
+    r2 = 1 - 0.5 * (x.double() @ gram.double())
+    b2 = 8 * 300 * 2.0 ** -24 * 0.5 * (x.abs().double() @ gram.abs().double()) + 1e-6
+    assert torch.all((c.double() - r2).abs() <= b2)
+    y = x.clone()
+    y[3, 4] = float("inf")
+    assert ops.gemm_h3(y, gram) is None
