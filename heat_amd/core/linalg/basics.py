@@ -8,7 +8,9 @@ pipeline and full-size all-reduces:
 
 * ``0 x None``, ``None x 1``: local GEMM, no communication;
 * ``0 x 0``, ``0 x 1``, ``1 x 1``: ONE all-gather of the replicated operand's panels (all 7 xGMI
-  links in parallel), then ONE local GEMM on hipBLASLt (fp32 runs on the f32 MFMA path);
+  links in parallel), then ONE local GEMM - fp32 on the hand-written 256 x 256-tile MFMA kernels
+  (``ops/csrc/gemm_tiled.hip``: exact f32 MFMA, or the fused fp16x3 kernel when the float32
+  matmul precision is "high"), other dtypes on torch;
 * ``1 x None``, ``None x 0``, ``1 x 0`` (contraction axis split): local partial GEMM + ONE
   reduce-scatter straight into the split output (half the traffic of an all-reduce and no
   replicated M x N result).
@@ -94,26 +96,57 @@ def _reduce_scatter(partial: torch.Tensor, comm, axis: int) -> torch.Tensor:
 
 # Largest operand handed to one BLAS call on the device. rocBLAS/hipBLASLt kernels address their
 # operands through 32-bit buffer descriptors, so a single GEMM on a >4 GB operand (a 1.25e6 x 4096
-# fp32 shard is 20 GB on a 288 GB MI355X) faults; larger products are split into blocks.
+# fp32 shard is 20 GB on a 288 GB MI355X) faults; larger library products are split into blocks.
+# The hand-written kernels (fp32 on every path below) use 64-bit offsets and take any size.
 _BLAS_MAX_BYTES = int(os.environ.get("HEAT_BLAS_MAX_BYTES", str(1 << 31)))
 _CHUNK_ON_HOST = False  # tests: exercise the blocking on CPU tensors too
 
-
-_SPLIT_MIN_WORK = 1 << 30  # m*n*k below which the fp32 GEMM is used regardless of precision
+# "native" (default): fp32 device GEMMs on the hand-written MFMA kernels (ops/csrc/gemm_tiled.hip);
+# "blas": torch.matmul / the tripled-K library split (A/B comparisons)
+_GEMM_BACKEND = os.environ.get("HEAT_GEMM_BACKEND", "native")
 
 
 def _split_gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
-    """fp32 device GEMMs go to the fp16x3 split GEMM (``ops.gemm_f16x3``: fp32-GEMM accuracy on
-    the FP16 matrix cores, ~2.7x faster) when torch's float32 matmul precision is "high" or
-    "medium" (``torch.set_float32_matmul_precision``; both allow TF32/bf16-class products, the split
-    is more accurate than either). The default "highest" keeps the library fp32 GEMM."""
+    """fp32 device GEMMs run as the fused fp16x3 split GEMM (fp32-GEMM accuracy on the FP16 matrix
+    cores, ~2.3x faster) when torch's float32 matmul precision is "high" or "medium"
+    (``torch.set_float32_matmul_precision``; both allow TF32/bf16-class products, the split is more
+    accurate than either). The default "highest" keeps exact fp32 products (f32 MFMA)."""
     return (a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
-            and torch.get_float32_matmul_precision() != "highest"
-            and a.shape[0] * a.shape[1] * b.shape[1] >= _SPLIT_MIN_WORK)
+            and torch.get_float32_matmul_precision() != "highest")
+
+
+def _native_fp32(a: torch.Tensor, b: torch.Tensor) -> bool:
+    if _GEMM_BACKEND != "native" or not (a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32):
+        return False
+    from ... import ops
+
+    return ops.use_native(a)
+
+
+def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
+          accumulate: bool = False) -> torch.Tensor:
+    """``alpha * a @ b`` (``+ out`` when ``accumulate``) for 2-D operands: device fp32 on the
+    hand-written MFMA kernels - the fused fp16x3 kernel when the float32 matmul precision allows it,
+    else the exact f32-MFMA kernel (both 256 x 256 tiles, any operand layout, 64-bit offsets, so no
+    blocking); other dtypes / host tensors on torch (blocked below the library's operand limit)."""
+    if _native_fp32(a, b):
+        from ... import ops
+
+        if _split_gemm_ok(a, b):
+            r = ops.gemm_h3(a, b, out=out, alpha=alpha, accumulate=accumulate)
+            if r is not None:
+                return r
+        return ops.gemm_f32(a, b, out=out, accumulate=accumulate, alpha=alpha)
+    r = _mm_blocked(a, b)
+    if alpha != 1.0:
+        r = r * alpha
+    if out is None:
+        return r
+    return out.add_(r) if accumulate else out.copy_(r)
 
 
 def _leaf_mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    if a.dim() == 2 and b.dim() == 2 and _split_gemm_ok(a, b):
+    if a.dim() == 2 and b.dim() == 2 and _split_gemm_ok(a, b) and _GEMM_BACKEND != "native":
         from ... import ops
 
         return ops.gemm_f16x3(a, b)
@@ -121,8 +154,16 @@ def _leaf_mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``a @ b`` with every BLAS operand below ``_BLAS_MAX_BYTES`` (blocks along the largest of
-    m, k, n; contraction blocks accumulate with addmm)."""
+    """``a @ b``: device fp32 matrices on the hand-written kernels (:func:`fgemm`), everything else
+    through :func:`_mm_blocked`."""
+    if a.dim() == 2 and b.dim() == 2 and _native_fp32(a, b):
+        return fgemm(a, b)
+    return _mm_blocked(a, b)
+
+
+def _mm_blocked(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b`` with every library operand below ``_BLAS_MAX_BYTES`` (blocks along the largest of
+    m, k, n; contraction blocks accumulate)."""
     if a.dim() != 2 or b.dim() != 2 or not (a.is_cuda or _CHUNK_ON_HOST):
         return _leaf_mm(a, b)
     m, k = a.shape
@@ -133,25 +174,19 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return _leaf_mm(a, b)
     if k >= m and k >= n and k > 1:
         step = max(1, lim // (max(m, n, 1) * es))
-        out = _mm(a[:, :step], b[:step])
+        out = _mm_blocked(a[:, :step], b[:step])
         for k0 in range(step, k, step):
-            out += _mm(a[:, k0: k0 + step], b[k0: k0 + step])
+            out += _mm_blocked(a[:, k0: k0 + step], b[k0: k0 + step])
         return out
     out = torch.empty((m, n), dtype=torch.result_type(a, b), device=a.device)
     if m >= n:
         step = max(1, lim // (max(k, n) * es))
-        direct = _split_gemm_ok(a[:step], b) and max(k, n) * es * step <= lim
         for r0 in range(0, m, step):
-            if direct and a[r0: r0 + step].shape[0] * k * n >= _SPLIT_MIN_WORK:
-                from ... import ops
-
-                ops.gemm_f16x3(a[r0: r0 + step], b, out=out[r0: r0 + step])
-            else:
-                out[r0: r0 + step] = _mm(a[r0: r0 + step], b)
+            out[r0: r0 + step] = _mm_blocked(a[r0: r0 + step], b)
     else:
         step = max(1, lim // (max(k, m) * es))
         for c0 in range(0, n, step):
-            out[:, c0: c0 + step] = _mm(a, b[:, c0: c0 + step])
+            out[:, c0: c0 + step] = _mm_blocked(a, b[:, c0: c0 + step])
     return out
 
 

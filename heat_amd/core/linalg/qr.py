@@ -244,8 +244,77 @@ def _cholqr(local: torch.Tensor, comm, calc_q: bool, distributed: bool):
     return None
 
 
+def _cholqr_native(A: torch.Tensor, comm, calc_q: bool, distributed: bool):
+    """CholeskyQR2 of a device fp32 block entirely on the hand-written kernels: the Gram matrices
+    and both Q products on the 256-tile MFMA GEMMs (``ops/csrc/gemm_tiled.hip``, exact f32 or fused
+    fp16x3 by the float32 matmul precision), the fp64 Cholesky and triangular inverse on
+    ``ops/csrc/linalg64.hip`` (no rocSOLVER / rocBLAS). One n x n all-reduce per pass; one host
+    sync per pass for the breakdown / conditioning decision."""
+    from ... import ops
+    from .basics import fgemm
+
+    dt = A.dtype
+
+    def allreduce(g: torch.Tensor) -> torch.Tensor:
+        if distributed:
+            from ..communication import MPI
+
+            comm.Allreduce(MPI.IN_PLACE, g, MPI.SUM)
+        return g
+
+    def factor(G: torch.Tensor, first: bool):
+        R, info = ops.cholesky_upper(G.double())
+        Rinv = ops.tri_inv_upper(R)
+        ok = int(info.item()) == 0 and bool(torch.isfinite(Rinv).all())
+        if ok and first:
+            ok = _cond_estimate_inv(R, Rinv) <= 1e3  # CholeskyQR2 with an fp32 Gram: cond(A) <~ 1e3
+        if distributed:
+            ok = comm.allreduce(int(ok)) == comm.size
+        return (R, Rinv) if ok else (None, None)
+
+    R1, Ri1 = factor(allreduce(fgemm(A.T, A)), True)
+    if R1 is None:
+        return None
+    Q1 = fgemm(A, Ri1.to(dt))
+    R2, Ri2 = factor(allreduce(fgemm(Q1.T, Q1)), False)
+    if R2 is None:
+        return None
+    R = ops.gemm64(R2, R1).to(dt)
+    if not calc_q:
+        return None, R
+    Q = fgemm(Q1, Ri2.to(dt))
+    return Q, R
+
+
+def _cond_estimate_inv(R: torch.Tensor, Rinv: torch.Tensor, iters: int = 12) -> float:
+    """2-norm condition number estimate ||R|| ||R^-1|| by power iteration on R^T R and
+    R^-T R^-1 (fp64 matrix-vector products on ``ops.gemm64``; deterministic start vector)."""
+    from ... import ops
+
+    n = R.shape[0]
+    if n == 0:
+        return 1.0
+    g = torch.Generator(device="cpu").manual_seed(12345)
+    x0 = (torch.rand(n, 1, generator=g, dtype=torch.float64) + 0.5).to(R.device)
+    res = []
+    for M in (R, Rinv):
+        x = x0 / x0.norm()
+        s = 0.0
+        for _ in range(iters):
+            y = ops.gemm64(M.T, ops.gemm64(M, x))
+            s = float(y.norm())
+            if not 0.0 < s < float("inf"):
+                return float("inf")
+            x = y / s
+        res.append(s)
+    return (res[0] * res[1]) ** 0.5
+
+
 def _cholqr_attempt(local: torch.Tensor, comm, calc_q: bool, distributed: bool, precise: bool):
-    from .basics import _mm
+    from .basics import _mm, _native_fp32
+
+    if not precise and _native_fp32(local, local):
+        return _cholqr_native(local, comm, calc_q, distributed)
 
     m_r, n = local.shape
     dt = local.dtype

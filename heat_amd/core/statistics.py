@@ -31,11 +31,13 @@ __all__ = ["argmax", "argmin", "average", "bincount", "cov", "histc", "histogram
 # ---------------------------------------------------------------------------------------------
 # moments engine
 # ---------------------------------------------------------------------------------------------
-def _moments(x: DNDarray, axis):
+def _moments(x: DNDarray, axis, final=None, ddof: int = 0):
     """Global (count, mean, M2) along ``axis`` as local torch tensors plus result metadata.
 
-    Returns (n, mean, m2, gshape, split, balanced) where the tensors are this rank's block of the
-    result (replicated when the split axis is reduced)."""
+    Returns (res, gshape, split, balanced) where ``res`` is this rank's block of the result
+    (replicated when the split axis is reduced): the (n, mean, M2) triple, or with ``final`` in
+    ('mean', 'var', 'std') the value itself. Without a cross-rank merge that is ONE fused kernel
+    launch on the device (``ops.moments``)."""
     axis = sanitize_axis(x.gshape, axis)
     if isinstance(axis, tuple):
         if len(axis) == 1:
@@ -55,28 +57,51 @@ def _moments(x: DNDarray, axis):
             if x.split is not None:
                 new_split = keep.index(x.split) if x.split in keep else len(keep)
             t = reshape(t, newshape, new_split=new_split)
-            return _moments(t, len(keep))
+            return _moments(t, len(keep), final, ddof)
     t = x.larray
+    merge = x.is_distributed() and (axis is None or axis == x.split)
     if axis is None:
-        n, mu, m2 = ops.moments(t, None)
-        if x.is_distributed():
-            n, mu, m2 = _allmerge(x.comm, n, mu, m2)
-        return n, mu, m2, (), None, True
-    gshape = tuple(s for i, s in enumerate(x.gshape) if i != axis)
+        gshape, split, bal = (), None, True
+    else:
+        gshape = tuple(s for i, s in enumerate(x.gshape) if i != axis)
+        split, bal = None, True
+        if not merge and x.split is not None and x.split != axis:
+            split = x.split if x.split < axis else x.split - 1
+            bal = x.balanced
+    if not merge:
+        return ops.moments(t, axis, final, ddof), gshape, split, bal
     n, mu, m2 = ops.moments(t, axis)
-    if x.is_distributed() and axis == x.split:
-        n, mu, m2 = _allmerge(x.comm, n, mu, m2)
-        return n, mu, m2, gshape, None, True
-    split = None
-    if x.split is not None and x.split != axis:
-        split = x.split if x.split < axis else x.split - 1
-    return n, mu, m2, gshape, split, x.balanced if split is not None else True
+    n, mu, m2 = _allmerge(x.comm, n, mu, m2)
+    if final is None:
+        return (n, mu, m2), gshape, split, bal
+    if final == "mean":
+        return mu, gshape, split, bal
+    v = m2 / (n - ddof)
+    return (v.sqrt() if final == "std" else v), gshape, split, bal
+
+
+# outputs up to this many elements are merged from an all-gather of every rank's triples (one
+# collective, latency-bound); larger ones by two all-reduces (3 x out instead of p x 3 x out)
+_ALLGATHER_MERGE_MAX = 4096
 
 
 def _allmerge(comm, n, mu, m2):
-    packed = torch.stack([n.reshape(-1), mu.reshape(-1), m2.reshape(-1)])  # [3, out]
-    allp = comm.allgather_tensor(packed.unsqueeze(0).contiguous(), 0)       # [p, 3, out]
-    N, MU, M2 = ops.merge_moments(allp[:, 0], allp[:, 1], allp[:, 2], 0)
+    """Chan merge of every rank's (n, mean, M2) partials (fp64). Small outputs: ONE all-gather of
+    the packed triples and a fixed-order merge. Large outputs: all-reduce [n, n mean] -> global
+    mean, then all-reduce the M2 contributions around it (m2_r + n_r (mean_r - mean)^2) - exact
+    Chan algebra, no cancellation, traffic independent of the number of ranks."""
+    if n.numel() <= _ALLGATHER_MERGE_MAX:
+        packed = torch.stack([n.reshape(-1), mu.reshape(-1), m2.reshape(-1)])  # [3, out]
+        allp = comm.allgather_tensor(packed.unsqueeze(0).contiguous(), 0)       # [p, 3, out]
+        N, MU, M2 = ops.merge_moments(allp[:, 0], allp[:, 1], allp[:, 2], 0)
+        return N.reshape(n.shape), MU.reshape(mu.shape), M2.reshape(m2.shape)
+    s = torch.stack([n.reshape(-1), (n * mu).reshape(-1)])
+    comm.Allreduce(MPI.IN_PLACE, s, MPI.SUM)
+    N = s[0]
+    MU = s[1] / torch.where(N > 0, N, torch.ones_like(N))
+    d = mu.reshape(-1) - MU
+    M2 = m2.reshape(-1) + n.reshape(-1) * d * d
+    comm.Allreduce(MPI.IN_PLACE, M2, MPI.SUM)
     return N.reshape(n.shape), MU.reshape(mu.shape), M2.reshape(m2.shape)
 
 
@@ -127,7 +152,7 @@ def mean(x: DNDarray, axis=None) -> DNDarray:
         s = arithmetics.sum(x, axis=axis)
         cnt = x.gnumel / max(1, s.gnumel)
         return s / cnt
-    n, mu, m2, gshape, split, bal = _moments(x, axis)
+    mu, gshape, split, bal = _moments(x, axis, "mean")
     return _wrap(x, mu, gshape, split, bal, _result_dtype(x))
 
 
@@ -144,16 +169,13 @@ def var(x: DNDarray, axis=None, ddof: int = 0, **kwargs) -> DNDarray:
     if ddof > 1:
         raise NotImplementedError("only ddof 0 and 1 are supported, got {}".format(ddof))
     axis = _moment_axis(x, axis)
-    n, mu, m2, gshape, split, bal = _moments(x, axis)
-    v = m2 / (n - ddof)
+    v, gshape, split, bal = _moments(x, axis, kwargs.pop("_final", "var"), ddof)
     return _wrap(x, v, gshape, split, bal, _result_dtype(x))
 
 
 def std(x: DNDarray, axis=None, ddof: int = 0, **kwargs) -> DNDarray:
-    """Standard deviation (square root of :func:`var`)."""
-    v = var(x, axis, ddof, **kwargs)
-    v.larray.sqrt_()
-    return v
+    """Standard deviation (square root of :func:`var`, fused into the same kernel)."""
+    return var(x, axis, ddof, _final="std", **kwargs)
 
 
 def _central_moment_sums(x: DNDarray, axis, powers=(2, 3, 4)):

@@ -24,7 +24,7 @@ _lib = None
 _lock = threading.Lock()
 _load_error = None
 
-c_void_p, c_int, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+c_void_p, c_int, c_int64, c_double = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
 
 _SIGNATURES = {
     "ha_km_workspace_floats": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
@@ -33,8 +33,10 @@ _SIGNATURES = {
     "ha_km_update_workspace": (c_int64, [c_int64, c_int, c_int, c_int]),
     "ha_km_update": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                              c_int, c_void_p]),
-    "ha_moments_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
-    "ha_moments_cols": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
+    "ha_moments_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_int, c_double,
+                                c_void_p, c_void_p]),
+    "ha_moments_cols": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_int, c_double,
+                                c_void_p, c_void_p]),
 }
 
 

@@ -29,6 +29,8 @@
 //     then re-read from that XCD's L2.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
@@ -50,11 +52,15 @@ __device__ __forceinline__ void tg_dma16(const void* src, unsigned char* dst) {
 
 // wait until at most N of this wave's vector-memory ops are outstanding (its DMA of the stage
 // about to be read has landed), retire LDS ops, then the workgroup barrier
+// (sched_barrier(0) on both sides: register-only MFMAs would otherwise migrate across the
+// asm statement, which only orders memory operations)
 template <int N>
 __device__ __forceinline__ void tg_wait_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 __device__ __forceinline__ void tg_wait_stage(int64_t t, int64_t nk) {
@@ -170,22 +176,43 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
   };
 
   const int64_t nk = Kp / TK;
-  // one stage: issue the DMA of t+3, the first accumulator row, wait for stage t+1 + barrier,
-  // then read stage t+1's fragments under the remaining three rows of MFMAs
+  // Steady-state stage (t + 3 < nk, no branches, so the scheduler sees one region per half): the
+  // DMA of stage t+3 issued between the first accumulator row's MFMAs, the counted wait for stage
+  // t+1 + barrier, then stage t+1's 16 fragment reads spread between the other 36 MFMAs. Every
+  // DMA / ds_read issues in the shadow of a 32-cycle MFMA instead of in front of the first one.
+  auto step_full = [&](int64_t t, const H3Frag& Fc, H3Frag& Fn) {
+    stage(t + 3);
+    mma_row(Fc, 0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (LDS-DMA)
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    tg_wait_barrier<16>();
+    load(Fn, t + 1);
+    mma_row(Fc, 1);
+    mma_row(Fc, 2);
+    mma_row(Fc, 3);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // general stage (the last three): DMA / wait only for stages that exist
   auto step = [&](int64_t t, const H3Frag& Fc, H3Frag& Fn) {
     if (t + 3 < nk) stage(t + 3);
-    __builtin_amdgcn_s_setprio(1);
     mma_row(Fc, 0);
-    __builtin_amdgcn_s_setprio(0);
     if (t + 1 < nk) {
       tg_wait_stage(t + 1, nk);
       load(Fn, t + 1);
     }
-    __builtin_amdgcn_s_setprio(1);
     mma_row(Fc, 1);
     mma_row(Fc, 2);
     mma_row(Fc, 3);
-    __builtin_amdgcn_s_setprio(0);
   };
 
   H3Frag F0, F1;
@@ -195,11 +222,20 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
     load(F0, 0);
   }
   int64_t t = 0;
-  for (; t + 2 <= nk; t += 2) {
-    step(t, F0, F1);
-    step(t + 1, F1, F0);
+  for (; t + 4 < nk; t += 2) {
+    step_full(t, F0, F1);
+    step_full(t + 1, F1, F0);
   }
-  if (t < nk) step(t, F0, F1);
+  if (t < nk) {
+    step(t, F0, F1);
+    if (t + 1 < nk) {
+      step(t + 1, F1, F0);
+      if (t + 2 < nk) {
+        step(t + 2, F0, F1);
+        if (t + 3 < nk) step(t + 3, F1, F0);
+      }
+    }
+  }
 
   // epilogue: the tile's 2 x 256 exponents through LDS (the stage buffers are free once every
   // wave passed this barrier), then C row = m0 + wm 128 + 32 i + (g & 3) + 8 (g >> 2) + 4 h,
@@ -215,24 +251,39 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
 // ------------------------------------------------------------------------------------------ f32
 // AK: A k-major ([K][M], m contiguous) - else row-major ([M][K], k contiguous).
 // BK_: B k-major ([K][N], n contiguous) - else n-major ([N][K], k contiguous).
-struct F32Frag {
+// MI16: v_mfma_f32_16x16x4_f32 (8 x 8 accumulators of 16 x 16 per wave; lane group g = lane >> 4
+// holds k = 4 g + s at step s) - else v_mfma_f32_32x32x2_f32 (4 x 4 of 32 x 32; lane half h holds
+// k = 8 h + s). Same FLOP per clock; the chip holds a different clock on each shape.
+constexpr int F32_KP = 1040;                 // k-row pitch of a k-major image (16 B pad: no 2-way conflict)
+constexpr int F32_OP = 16 * F32_KP;          // bytes per operand per stage
+constexpr int F32_STAGE = 2 * F32_OP;        // 33280
+static_assert(TNBUF * F32_STAGE <= 160 * 1024, "LDS");
+
+template <bool MI16>
+struct F32Frag;
+template <>
+struct F32Frag<false> {
   float a[4][8], b[4][8];
 };
+template <>
+struct F32Frag<true> {
+  floatx4 a[8], b[8];
+};
 
-template <bool AK, bool BK_>
+template <bool AK, bool BK_, bool MI16>
 __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * TSTAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * F32_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t nbn = (N + TB - 1) / TB, nbm = (M + TB - 1) / TB;
   const int64_t bid = tg_xcd_remap(blockIdx.x, nbm * nbn);
   const int64_t m0 = (bid / nbn) * TB, n0 = (bid % nbn) * TB;
   const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5, r = lane & 31;
 
-  // staging: waves 0, 1 move A (16 KB: 16 pieces), waves 2, 3 move B. Piece q (0..15) of an
-  // operand: row-major image -> k-chunk q >> 2, rows 64 (q & 3) + lane; k-major -> k-row q.
+  // staging: waves 0, 1 move A (16 pieces of 1 KB), waves 2, 3 move B. Piece q (0..15) of an
+  // operand: row-major image -> k-chunk q >> 2, rows 64 (q & 3) + lane (at q KB); k-major -> k-row q
+  // (at q F32_KP).
   const bool isA = wave < 2;
   const bool km = isA ? AK : BK_;
   const float* P = isA ? A : B;
@@ -247,7 +298,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
   int64_t coloff = rbase + 4 * lane;  // k-major images: 4 consecutive rows (columns of memory)
   coloff = coloff + 4 <= rows ? coloff : rows - 4;
   auto stage = [&](int64_t t) {
-    unsigned char* dst = smem + (t & (TNBUF - 1)) * TSTAGE + (isA ? 0 : 16384);
+    unsigned char* dst = smem + (t & (TNBUF - 1)) * F32_STAGE + (isA ? 0 : F32_OP);
     const int64_t k0 = t * TK;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -255,7 +306,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
       if (km) {
         int64_t k = k0 + q;
         k = k < K ? k : K - 1;
-        tg_dma16(P + k * ld + coloff, dst + q * 1024);
+        tg_dma16(P + k * ld + coloff, dst + q * F32_KP);
       } else {
         int64_t k = k0 + 4 * (q >> 2);
         k = k + 4 <= K ? k : K - 4;
@@ -263,68 +314,127 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
       }
     }
   };
+  // steady-state staging (a whole in-range stage: no clamping, no branches) - the pointer of piece q
+  // is lb[q & 3] + a uniform offset (q & 3 == i & 3 since 8 half has no low bits)
+  const float* lb[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) lb[g] = P + (km ? coloff : rowoff[g]);
+  // koff(q) = (k0 + q qa) lmul + (q >> 2) qb: k-major (1, ld, 0), row-major (0, 1, 4) - arithmetic on
+  // wave-uniform integers, so A and B waves run the same branch-free code
+  const int dstride = km ? F32_KP : 1024, qa = km ? 1 : 0, qb = km ? 0 : 4;
+  const int64_t lmul = km ? ld : 1;
+  const int opoff = isA ? 0 : F32_OP;
+  auto stage_full = [&](int64_t t) {
+    unsigned char* dst = smem + (t & (TNBUF - 1)) * F32_STAGE + opoff;
+    const int64_t k0 = t * TK;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = 8 * half + i;
+      tg_dma16(lb[i & 3] + ((k0 + q * qa) * lmul + (q >> 2) * qb), dst + q * dstride);
+    }
+  };
   // zero the k >= K entries of this wave's pieces of the last stage (after its own DMA landed)
   auto zero_tail = [&](int64_t t) {
-    unsigned char* dst = smem + (t & (TNBUF - 1)) * TSTAGE + (isA ? 0 : 16384);
+    unsigned char* dst = smem + (t & (TNBUF - 1)) * F32_STAGE + (isA ? 0 : F32_OP);
     const int64_t k0 = t * TK;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int q = 8 * half + i;
       if (km) {
-        if (k0 + q >= K) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
+        if (k0 + q >= K) *reinterpret_cast<floatx4*>(dst + q * F32_KP + lane * 16) = (floatx4)(0.f);
       } else {
-        const int64_t k = k0 + 4 * (q >> 2);
-        if (k >= K) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
+        if (k0 + 4 * (q >> 2) >= K) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
       }
     }
   };
 
-  // fragments: lane (r, h), MFMA step s <-> k = 8 h + s
-  auto load = [&](F32Frag& F, int64_t t) {
-    const unsigned char* b = smem + (t & (TNBUF - 1)) * TSTAGE;
+  auto load = [&](F32Frag<MI16>& F, int64_t t) {
+    const unsigned char* b = smem + (t & (TNBUF - 1)) * F32_STAGE;
+    if constexpr (MI16) {
+      // lane (r16 = lane & 15, g = lane >> 4): rows of block i, k = 4 g + s
+      const int r16 = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ra = wm * 128 + i * 32 + r, cb = wn * 128 + i * 32 + r;
-      if (AK) {
+      for (int i = 0; i < 8; ++i) {
+        const int ra = wm * 128 + i * 16 + r16, cb = wn * 128 + i * 16 + r16;
+        if (AK) {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) F.a[i][s] = *reinterpret_cast<const float*>(b + (8 * h + s) * 1024 + ra * 4);
-      } else {
-        const floatx4 x0 = *reinterpret_cast<const floatx4*>(b + ((2 * h) * 256 + ra) * 16);
-        const floatx4 x1 = *reinterpret_cast<const floatx4*>(b + ((2 * h + 1) * 256 + ra) * 16);
+          for (int s = 0; s < 4; ++s) F.a[i][s] = *reinterpret_cast<const float*>(b + (4 * g + s) * F32_KP + ra * 4);
+        } else {
+          F.a[i] = *reinterpret_cast<const floatx4*>(b + (g * 256 + ra) * 16);
+        }
+        if (BK_) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          F.a[i][s] = x0[s];
-          F.a[i][4 + s] = x1[s];
+          for (int s = 0; s < 4; ++s)
+            F.b[i][s] = *reinterpret_cast<const float*>(b + F32_OP + (4 * g + s) * F32_KP + cb * 4);
+        } else {
+          F.b[i] = *reinterpret_cast<const floatx4*>(b + F32_OP + (g * 256 + cb) * 16);
         }
       }
-      if (BK_) {
+    } else {
+      // lane (r, h): rows of block i, k = 8 h + s
+      const int h = lane >> 5, r = lane & 31;
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
-          F.b[i][s] = *reinterpret_cast<const float*>(b + 16384 + (8 * h + s) * 1024 + cb * 4);
-      } else {
-        const floatx4 y0 = *reinterpret_cast<const floatx4*>(b + 16384 + ((2 * h) * 256 + cb) * 16);
-        const floatx4 y1 = *reinterpret_cast<const floatx4*>(b + 16384 + ((2 * h + 1) * 256 + cb) * 16);
+      for (int i = 0; i < 4; ++i) {
+        const int ra = wm * 128 + i * 32 + r, cb = wn * 128 + i * 32 + r;
+        if (AK) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          F.b[i][s] = y0[s];
-          F.b[i][4 + s] = y1[s];
+          for (int s = 0; s < 8; ++s) F.a[i][s] = *reinterpret_cast<const float*>(b + (8 * h + s) * F32_KP + ra * 4);
+        } else {
+          const floatx4 x0 = *reinterpret_cast<const floatx4*>(b + ((2 * h) * 256 + ra) * 16);
+          const floatx4 x1 = *reinterpret_cast<const floatx4*>(b + ((2 * h + 1) * 256 + ra) * 16);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            F.a[i][s] = x0[s];
+            F.a[i][4 + s] = x1[s];
+          }
+        }
+        if (BK_) {
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            F.b[i][s] = *reinterpret_cast<const float*>(b + F32_OP + (8 * h + s) * F32_KP + cb * 4);
+        } else {
+          const floatx4 y0 = *reinterpret_cast<const floatx4*>(b + F32_OP + ((2 * h) * 256 + cb) * 16);
+          const floatx4 y1 = *reinterpret_cast<const floatx4*>(b + F32_OP + ((2 * h + 1) * 256 + cb) * 16);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            F.b[i][s] = y0[s];
+            F.b[i][4 + s] = y1[s];
+          }
         }
       }
     }
   };
 
+  // accumulators: MI16 8 x 8 of floatx4, else 4 x 4 of floatx16 (256 registers either way)
   floatx16 acc[4][4];
+  floatx4 acc16[8][8];
+  if constexpr (MI16) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (floatx16)(0.f);
+      for (int j = 0; j < 8; ++j) acc16[i][j] = (floatx4)(0.f);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (floatx16)(0.f);
+  }
 
-  auto mma_row = [&](const F32Frag& F, int i) {
+  // part p of a stage's MFMAs (p = 0: before the barrier, 1..3 after)
+  auto mma_part = [&](const F32Frag<MI16>& F, int p) {
+    if constexpr (MI16) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[i][s], F.b[j][s], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 8; ++j)
+          acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.a[i][p], F.b[j][p], acc16[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[p][s], F.b[j][s], acc[p][j], 0, 0, 0);
+    }
   };
 
   const int64_t nk = (K + TK - 1) / TK;
@@ -338,32 +448,91 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
     }
     tg_wait_stage(t, nk);
   };
-  auto step = [&](int64_t t, const F32Frag& Fc, F32Frag& Fn) {
+  // steady state (t + 3 < nk and stage t + 1 is not the zero-padded tail): branch-free, DMA and
+  // fragment reads interleaved with the MFMAs (see gemm_h3t)
+  auto step_full = [&](int64_t t, const F32Frag<MI16>& Fc, F32Frag<MI16>& Fn) {
+    stage_full(t + 3);
+    mma_part(Fc, 0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, MI16 ? 8 : 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+    }
+    tg_wait_barrier<16>();
+    load(Fn, t + 1);
+    mma_part(Fc, 1);
+    mma_part(Fc, 2);
+    mma_part(Fc, 3);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, MI16 ? 6 : 3, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto step = [&](int64_t t, const F32Frag<MI16>& Fc, F32Frag<MI16>& Fn) {
     if (t + 3 < nk) stage(t + 3);
-    mma_row(Fc, 0);
+    mma_part(Fc, 0);
     if (t + 1 < nk) {
       ready(t + 1);
       load(Fn, t + 1);
     }
-    mma_row(Fc, 1);
-    mma_row(Fc, 2);
-    mma_row(Fc, 3);
+    mma_part(Fc, 1);
+    mma_part(Fc, 2);
+    mma_part(Fc, 3);
   };
 
-  F32Frag F0, F1;
+  F32Frag<MI16> F0, F1;
   for (int64_t t = 0; t < 3 && t < nk; ++t) stage(t);
   if (nk > 0) {
     ready(0);
     load(F0, 0);
   }
   int64_t t = 0;
-  for (; t + 2 <= nk; t += 2) {
-    step(t, F0, F1);
-    step(t + 1, F1, F0);
+  for (; t + 4 < nk; t += 2) {
+    step_full(t, F0, F1);
+    step_full(t + 1, F1, F0);
   }
-  if (t < nk) step(t, F0, F1);
+  if (t < nk) {
+    step(t, F0, F1);
+    if (t + 1 < nk) {
+      step(t + 1, F1, F0);
+      if (t + 2 < nk) {
+        step(t + 2, F0, F1);
+        if (t + 3 < nk) step(t + 3, F1, F0);
+      }
+    }
+  }
 
-  tg_store_tile(acc, C, M, N, ldc, m0, n0, wm, wn, h, r, alpha, beta, nullptr);
+  if constexpr (MI16) {
+    // 16 x 16 C/D map: column = lane & 15, row = 4 (lane >> 4) + reg
+    const bool full = m0 + TB <= M && n0 + TB <= N;
+    const int r16 = lane & 15, g4 = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t rb = m0 + wm * 128 + i * 16 + g4;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t gn = n0 + wn * 128 + j * 16 + r16;
+        const bool colok = full || gn < N;
+        float* cb = C + rb * ldc + gn;
+        float cv[4];
+        if (beta) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) cv[g] = (colok && (full || rb + g < M)) ? cb[g * ldc] : 0.f;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v = alpha * acc16[i][j][g];
+          if (beta) v += cv[g];
+          if (colok && (full || rb + g < M)) cb[g * ldc] = v;
+        }
+      }
+      asm volatile("" ::: "memory");
+    }
+  } else {
+    tg_store_tile(acc, C, M, N, ldc, m0, n0, wm, wn, lane >> 5, lane & 31, alpha, beta, nullptr);
+  }
 }
 
 // ------------------------------------------------------------------------ h3 operand splitting
@@ -512,8 +681,14 @@ int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, 
                 int64_t ldc, float alpha, int beta, hipStream_t s) {
   const int64_t nwg = ((M + TB - 1) / TB) * ((N + TB - 1) / TB);
   if (nwg > 0x7FFFFFFF) return HA_UNSUPPORTED;
-  hipLaunchKernelGGL((gemm_f32t<AK, BK_>), dim3((unsigned)nwg), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc,
-                     alpha, beta);
+  // HEAT_GEMM_F32_SHAPE=16 selects the 16x16x4 MFMA shape (A/B benchmarking)
+  static const int shape = getenv("HEAT_GEMM_F32_SHAPE") ? atoi(getenv("HEAT_GEMM_F32_SHAPE")) : 32;
+  if (shape == 16)
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, true>), dim3((unsigned)nwg), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb,
+                       ldc, alpha, beta);
+  else
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false>), dim3((unsigned)nwg), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb,
+                       ldc, alpha, beta);
   return ha_launch_status();
 }
 

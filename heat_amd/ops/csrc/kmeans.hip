@@ -463,6 +463,166 @@ __global__ __launch_bounds__(256) void ku_gather4(const float* __restrict__ X, i
   }
 }
 
+// ---------------------------------------------------------------- deterministic update (default)
+// The update above is fast but its float atomics (and the atomic slot claims of ku_scatter) make
+// the sums depend on timing. The deterministic pipeline keeps its shape and removes every
+// order-dependent step:
+//   * ku_scatter_det: block b covers the same rows as its ku_hist histogram; its W waves each own a
+//     contiguous sub-range (per-wave counts + a prefix over waves in LDS), and each 64-row batch is
+//     placed by a bitonic sort of (label, lane) keys across the wave - positions inside a cluster
+//     segment follow row order, whatever the scheduling;
+//   * ku_gather_det: the sorted positions are cut into ranges of KU_RANGE; a (range, column-group)
+//     thread sums its range sequentially and writes the partial of every (cluster, range) segment it
+//     touches to its own slot P[cluster + range] (cluster + range is unique along the monotone
+//     walk) - no atomics;
+//   * ku_reduce_det: sums[c] = the cluster's range partials added in range order (fp64).
+constexpr int KU_RANGE = 256;
+constexpr int KU_RD = 8;  // rows in flight per gather thread
+
+__global__ __launch_bounds__(1024) void ku_scatter_det(const int* __restrict__ lab, int64_t n, int k,
+                                                       int64_t rows_per_blk, int W, const int* __restrict__ hist,
+                                                       const int* __restrict__ cstart, int* __restrict__ order) {
+  extern __shared__ int cnt[];  // [W][k]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  const int64_t r1 = r0 + rows_per_blk < n ? r0 + rows_per_blk : n;
+  const int64_t sub = (r1 - r0 + W - 1) / W;
+  const int64_t s0 = r0 + w * sub < r1 ? r0 + w * sub : r1;
+  const int64_t s1 = s0 + sub < r1 ? s0 + sub : r1;
+  for (int e = tid; e < W * k; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int64_t i = s0 + lane; i < s1; i += 64) {
+    const int l = lab[i];
+    if ((unsigned)l < (unsigned)k) atomicAdd(&cnt[w * k + l], 1);  // integer counts: order-free
+  }
+  __syncthreads();
+  for (int c = tid; c < k; c += blockDim.x) {
+    int run = cstart[c] + hist[(int64_t)blockIdx.x * k + c];
+    for (int v = 0; v < W; ++v) {
+      const int t = cnt[v * k + c];
+      cnt[v * k + c] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+  int* my = cnt + w * k;
+  const unsigned long long below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= lane
+  for (int64_t b0 = s0; b0 < s1; b0 += 64) {
+    const int64_t i = b0 + lane;
+    const int l = i < s1 ? lab[i] : -1;
+    int key = (unsigned)l < (unsigned)k ? (l << 6) | lane : 0x7FFFFFFF;
+    // bitonic sort of the 64 keys across the wave (ascending by label, then lane)
+#pragma unroll
+    for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        const int other = __shfl_xor(key, j, 64);
+        const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
+        key = (lower == up) ? min(key, other) : max(key, other);
+      }
+    }
+    const bool valid = key != 0x7FFFFFFF;
+    const int sl = key >> 6;
+    const int prev = __shfl_up(key, 1, 64);
+    const bool start = valid && (lane == 0 || (prev >> 6) != sl);
+    const unsigned long long starts = __ballot(start);
+    const int mys = 63 - __clzll(starts & below);
+    const unsigned long long after = starts & ~below;
+    // a run ends at the next start or at the first invalid key (invalid keys sort last); the
+    // ballot runs with the whole wave active (inside the branch it would see only the starts)
+    const int nvalid = __popcll(__ballot(valid));
+    int base = 0;
+    if (start) {
+      const int end = after ? __ffsll((long long)after) - 1 : nvalid;
+      base = my[sl];
+      my[sl] = base + (end - lane);
+    }
+    const int b = __shfl(base, mys < 0 ? 0 : mys, 64);
+    if (valid) order[b + (lane - mys)] = (int)(b0 + (key & 63));
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void ku_gather_det(const float* __restrict__ X, int f, int64_t ldx,
+                                                     const int* __restrict__ order, const int* __restrict__ cstart,
+                                                     int k, float* __restrict__ P) {
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int64_t nvalid = cstart[k];
+  const int64_t rg = (int64_t)blockIdx.x * 16 + rl;
+  const int64_t p0 = rg * KU_RANGE;
+  if (p0 >= nvalid) return;
+  const int64_t p1 = p0 + KU_RANGE < nvalid ? p0 + KU_RANGE : nvalid;
+  const int c0 = ku_cluster_of(cstart, k, p0);
+  for (int cb = 0; cb < f; cb += 64) {
+    const int col = cb + 4 * cg;
+    if (col >= f) break;
+    int cur = c0;
+    int64_t nb = cstart[cur + 1];
+    floatx4 acc = (floatx4)(0.f);
+    auto flush = [&]() {
+      float* d = P + ((int64_t)cur + rg) * f + col;
+      if (VEC) {
+        *reinterpret_cast<floatx4*>(d) = acc;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (col + q < f) d[q] = acc[q];
+      }
+      acc = (floatx4)(0.f);
+    };
+    auto row = [&](int idx) {
+      const float* src = X + (int64_t)idx * ldx + col;
+      if (VEC) return *reinterpret_cast<const floatx4*>(src);
+      floatx4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = col + q < f ? src[q] : 0.f;
+      return v;
+    };
+    int64_t q = p0;
+    for (; q + KU_RD <= p1; q += KU_RD) {
+      int idx[KU_RD];
+      floatx4 v[KU_RD];
+#pragma unroll
+      for (int u = 0; u < KU_RD; ++u) idx[u] = order[q + u];
+#pragma unroll
+      for (int u = 0; u < KU_RD; ++u) v[u] = row(idx[u]);
+#pragma unroll
+      for (int u = 0; u < KU_RD; ++u) {
+        while (q + u >= nb) {
+          flush();
+          ++cur;
+          nb = cstart[cur + 1];
+        }
+        acc += v[u];
+      }
+    }
+    for (; q < p1; ++q) {
+      const floatx4 v = row(order[q]);
+      while (q >= nb) {
+        flush();
+        ++cur;
+        nb = cstart[cur + 1];
+      }
+      acc += v;
+    }
+    flush();
+  }
+}
+
+__global__ __launch_bounds__(256) void ku_reduce_det(const float* __restrict__ P, const int* __restrict__ cstart,
+                                                     int k, int f, float* __restrict__ sums) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)k * f) return;
+  const int c = (int)(e / f), j = (int)(e % f);
+  const int64_t a = cstart[c], b = cstart[c + 1];
+  double s = 0.0;
+  if (b > a) {
+    const int64_t rlo = a / KU_RANGE, rhi = (b - 1) / KU_RANGE;
+    for (int64_t r = rlo; r <= rhi; ++r) s += (double)P[((int64_t)c + r) * f + j];
+  }
+  sums[e] = (float)s;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -524,14 +684,20 @@ static void ku_grid(int64_t n, int64_t* nblk, int64_t* rows_per_blk) {
   *rows_per_blk = rows;
 }
 
-// int32 scratch ha_km_update needs (-1: unsupported k).
+// int32 scratch ha_km_update needs (-1: unsupported k): the order array, histograms, totals and
+// segment starts, plus the deterministic gather's (k + ranges) x f float partials.
 HA_EXPORT int64_t ha_km_update_workspace(int64_t n, int k, int f, int num_cus) {
-  (void)f;
   (void)num_cus;
   if (k <= 0 || (int64_t)k * 4 > 150 * 1024 || n >= (int64_t)1 << 31) return -1;
   int64_t nblk, rows;
   ku_grid(n, &nblk, &rows);
-  return n + nblk * k + k + (k + 1);
+  const int64_t nranges = (n + KU_RANGE - 1) / KU_RANGE;
+  return n + nblk * k + k + (k + 1) + 4 + (k + nranges) * (int64_t)f;
+}
+
+static bool ku_deterministic() {
+  static const bool d = [] { const char* e = getenv("HEAT_KU_DETERMINISTIC"); return !e || atoi(e) != 0; }();
+  return d;
 }
 
 // sums [k][f] and counts [k] are written completely.
@@ -560,6 +726,29 @@ HA_EXPORT int ha_km_update(const float* X, int64_t n, int f, int64_t ldx, const 
                      (int64_t)k * f);
   hipLaunchKernelGGL(ku_scan_blk, dim3((k + 255) / 256), dim3(256), 0, s, hist, (int)nblk, k, total);
   hipLaunchKernelGGL(ku_scan_tot, dim3(1), dim3(1024), 0, s, total, k, cstart, counts);
+  if (ku_deterministic()) {
+    // waves per scatter block: their per-wave counts ([W][k] ints) must fit in LDS
+    int W = 16;
+    while (W > 1 && (size_t)W * k * sizeof(int) > 128 * 1024) W >>= 1;
+    const size_t lds_det = (size_t)W * k * sizeof(int);
+    if (lds_det > 64 * 1024)
+      hipFuncSetAttribute((const void*)ku_scatter_det, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_det);
+    hipLaunchKernelGGL(ku_scatter_det, dim3((unsigned)nblk), dim3(64 * W), lds_det, s, labels, n, k, rows, W, hist,
+                       cstart, order);
+    // partials after cstart[k + 1] (16-byte aligned)
+    int64_t off = (int64_t)((cstart + k + 1) - workspace);
+    off = (off + 3) & ~(int64_t)3;
+    float* P = reinterpret_cast<float*>(workspace + off);
+    const int64_t nranges = (n + KU_RANGE - 1) / KU_RANGE;
+    const unsigned gblk = (unsigned)((nranges + 15) / 16);
+    if (f % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0)
+      hipLaunchKernelGGL(ku_gather_det<true>, dim3(gblk), dim3(256), 0, s, X, f, ldx, order, cstart, k, P);
+    else
+      hipLaunchKernelGGL(ku_gather_det<false>, dim3(gblk), dim3(256), 0, s, X, f, ldx, order, cstart, k, P);
+    hipLaunchKernelGGL(ku_reduce_det, dim3((unsigned)(((int64_t)k * f + 255) / 256)), dim3(256), 0, s, P, cstart, k,
+                       f, sums);
+    return ha_launch_status();
+  }
   hipLaunchKernelGGL(ku_scatter, dim3((unsigned)nblk), dim3(KU_BLOCK), lds, s, labels, n, k, rows, hist, cstart,
                      order);
   static const bool g4 = [] { const char* e = getenv("HEAT_KU_GATHER4"); return !e || atoi(e) != 0; }();

@@ -53,9 +53,51 @@ __device__ __forceinline__ Trip wave_merge(Trip t) {
   return t;
 }
 
+// Final outputs of a reduction (the fused epilogue, K6): kind 0 = the (n, mean, M2) triple in
+// fp64 (input of a cross-rank merge), 1 = mean, 2 = var = M2 / (n - ddof), 3 = std, as fp32.
+__device__ __forceinline__ void mom_emit(const Trip& t, int kind, double ddof, void* out, int64_t i) {
+  if (kind == 0) {
+    double* o = reinterpret_cast<double*>(out) + i * 3;
+    o[0] = t.n;
+    o[1] = t.mean;
+    o[2] = t.m2;
+    return;
+  }
+  double v = t.mean;
+  if (kind >= 2) {
+    v = t.m2 / (t.n - ddof);
+    if (kind == 3) v = sqrt(v);
+  }
+  reinterpret_cast<float*>(out)[i] = (float)v;
+}
+
+// Publish this block's partial (already stored by thread 0) and take a ticket on the per-output
+// arrival counter; true in every thread of the block that arrived last. Agent-scope release before
+// the ticket, acquire (L1 invalidate) in the last block before it reads the other partials; the
+// last block resets the counter for the next launch on this workspace.
+__device__ __forceinline__ bool mom_last_arrival(unsigned* __restrict__ cnt, unsigned expected) {
+  __shared__ bool last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool l = atomicAdd(cnt, 1u) == expected - 1;
+    if (l) {
+      __threadfence();
+      *cnt = 0u;
+    }
+    last = l;
+  }
+  __syncthreads();
+  return last;
+}
+
+__device__ __forceinline__ Trip mom_load(const double* p) { return Trip{p[0], p[1], p[2]}; }
+
 // rows: x[r * ld + i], i in [0, len).  Grid.x = nrows * nchunks; part[(r*nchunks + c)*3 + {0,1,2}]
 __global__ __launch_bounds__(256) void mom_rows(const float* __restrict__ x, int64_t nrows, int64_t len,
-                                                int64_t ld, int nchunks, double* __restrict__ part) {
+                                                int64_t ld, int nchunks, double* __restrict__ part,
+                                                void* __restrict__ out, int kind, double ddof,
+                                                unsigned* __restrict__ arrive) {
   const int64_t g = blockIdx.x;
   const int64_t r = g / nchunks;
   const int c = (int)(g % nchunks);
@@ -131,10 +173,32 @@ __global__ __launch_bounds__(256) void mom_rows(const float* __restrict__ x, int
   if (tid == 0) {
     Trip acc = {sh[0][0], sh[0][1], sh[0][2]};
     for (int k = 1; k < 4; ++k) acc = chan(acc, Trip{sh[k][0], sh[k][1], sh[k][2]});
-    double* o = part + g * 3;
-    o[0] = acc.n;
-    o[1] = acc.mean;
-    o[2] = acc.m2;
+    if (out != nullptr && nchunks == 1) {
+      mom_emit(acc, kind, ddof, out, r);
+    } else {
+      double* o = part + g * 3;
+      o[0] = acc.n;
+      o[1] = acc.mean;
+      o[2] = acc.m2;
+    }
+  }
+  if (out == nullptr || nchunks == 1) return;
+  // fused epilogue: the last of the row's nchunks blocks merges their partials in chunk order
+  if (!mom_last_arrival(arrive + r, (unsigned)nchunks)) return;
+  Trip m = {0.0, 0.0, 0.0};
+  for (int q = tid; q < nchunks; q += 256) m = chan(m, mom_load(part + (r * nchunks + q) * 3));
+  m = wave_merge(m);
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    sh[w][0] = m.n;
+    sh[w][1] = m.mean;
+    sh[w][2] = m.m2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    Trip acc = {sh[0][0], sh[0][1], sh[0][2]};
+    for (int k = 1; k < 4; ++k) acc = chan(acc, Trip{sh[k][0], sh[k][1], sh[k][2]});
+    mom_emit(acc, kind, ddof, out, r);
   }
 }
 
@@ -142,7 +206,8 @@ __global__ __launch_bounds__(256) void mom_rows(const float* __restrict__ x, int
 // the shift K = row[0], so the shifted sums are plain wave sums (no per-lane Chan merges, which
 // made the block-per-row kernel ~4x slower than HBM on 1e6 x 1000 inputs).
 __global__ __launch_bounds__(256) void mom_rows_wave(const float* __restrict__ x, int64_t nrows, int64_t len,
-                                                     int64_t ld, double* __restrict__ part) {
+                                                     int64_t ld, double* __restrict__ part, void* __restrict__ out,
+                                                     int kind, double ddof) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= nrows) return;
@@ -191,9 +256,13 @@ __global__ __launch_bounds__(256) void mom_rows_wave(const float* __restrict__ x
   s2 = ha_wave_sum(s2);
   if (lane == 0) {
     const Trip t = trip_from_shifted((double)len, K, s1, s2);
-    part[r * 3 + 0] = t.n;
-    part[r * 3 + 1] = t.mean;
-    part[r * 3 + 2] = t.m2;
+    if (out != nullptr) {
+      mom_emit(t, kind, ddof, out, r);
+    } else {
+      part[r * 3 + 0] = t.n;
+      part[r * 3 + 1] = t.mean;
+      part[r * 3 + 2] = t.m2;
+    }
   }
 }
 
@@ -201,13 +270,15 @@ __global__ __launch_bounds__(256) void mom_rows_wave(const float* __restrict__ x
 // columns; grid = (ceil(ncols / (256*VEC)), nchunks).  part[(c*ncols + col)*3 + {0,1,2}]
 template <int VEC>
 __global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int64_t len, int64_t ncols,
-                                                int64_t ld, int nchunks, double* __restrict__ part) {
+                                                int64_t ld, int nchunks, double* __restrict__ part,
+                                                void* __restrict__ out, int kind, double ddof,
+                                                unsigned* __restrict__ cnt) {
   const int64_t col0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
   const int c = blockIdx.y;
   const int64_t per = (len + nchunks - 1) / nchunks;
   const int64_t r0 = (int64_t)c * per;
   const int64_t r1 = r0 + per < len ? r0 + per : len;
-  if (col0 >= ncols) return;
+  if (col0 < ncols) {
   float K[VEC], s1[VEC], s2[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
@@ -280,47 +351,74 @@ __global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int
     const int64_t col = col0 + e;
     if (col < ncols) {
       const Trip t = trip_from_shifted(n, K[e], s1[e], s2[e]);
-      double* o = part + ((int64_t)c * ncols + col) * 3;
-      o[0] = t.n;
-      o[1] = t.mean;
-      o[2] = t.m2;
+      if (out != nullptr && nchunks == 1) {
+        mom_emit(t, kind, ddof, out, col);
+      } else {
+        double* o = part + ((int64_t)c * ncols + col) * 3;
+        o[0] = t.n;
+        o[1] = t.mean;
+        o[2] = t.m2;
+      }
+    }
+  }
+  }
+  if (out == nullptr || nchunks == 1) return;
+  // every thread's partial is stored: retire them before the block's release + ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // fused epilogue: the last of the column block's nchunks blocks merges them in chunk order
+  if (!mom_last_arrival(cnt + blockIdx.x, (unsigned)nchunks)) return;
+  if (col0 >= ncols) return;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int64_t col = col0 + e;
+    if (col < ncols) {
+      Trip t = {0.0, 0.0, 0.0};
+      for (int q = 0; q < nchunks; ++q) t = chan(t, mom_load(part + ((int64_t)q * ncols + col) * 3));
+      mom_emit(t, kind, ddof, out, col);
     }
   }
 }
 
 }  // namespace
 
+// (n, mean, M2) of each row x[r * ld + i], i < len. out == null: per-chunk partial triples into
+// part[(r nchunks + c) 3 + {0, 1, 2}]; else the final value per row (kind: 0 triple fp64, 1 mean,
+// 2 var, 3 std as fp32) into out - chunks merged by the row's last block (cnt: nrows zeroed
+// counters, reset by the kernel).
 HA_EXPORT int ha_moments_rows(const float* x, int64_t nrows, int64_t len, int64_t ld, int nchunks, double* part,
-                              void* stream) {
+                              void* out, int kind, double ddof, unsigned* cnt, void* stream) {
   if (nrows <= 0) return HA_OK;
-  if (nchunks < 1) return HA_BAD_ARG;
+  if (nchunks < 1 || (out != nullptr && nchunks > 1 && cnt == nullptr)) return HA_BAD_ARG;
   if (nchunks == 1 && len > 0 && len <= 16384) {
     const int64_t blocks = (nrows + 3) / 4;
     if (blocks > 0x7fffffffLL) return HA_UNSUPPORTED;
     hipLaunchKernelGGL(mom_rows_wave, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, nrows, len, ld,
-                       part);
+                       part, out, kind, ddof);
     return ha_launch_status();
   }
   const int64_t grid = nrows * nchunks;
   if (grid > 0x7fffffffLL) return HA_UNSUPPORTED;
   hipLaunchKernelGGL(mom_rows, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, x, nrows, len, ld, nchunks,
-                     part);
+                     part, out, kind, ddof, cnt);
   return ha_launch_status();
 }
 
+// (n, mean, M2) of each column x[i * ld + col], i < len; out / kind / cnt as ha_moments_rows (cnt:
+// one counter per block of 256 * VEC columns, i.e. ceil(ncols / 256) suffice).
 HA_EXPORT int ha_moments_cols(const float* x, int64_t len, int64_t ncols, int64_t ld, int nchunks, double* part,
-                              void* stream) {
+                              void* out, int kind, double ddof, unsigned* cnt, void* stream) {
   if (ncols <= 0) return HA_OK;
-  if (nchunks < 1 || nchunks > 65535) return HA_BAD_ARG;
+  if (nchunks < 1 || nchunks > 65535 || (out != nullptr && nchunks > 1 && cnt == nullptr)) return HA_BAD_ARG;
   const bool vec = (ncols % 4 == 0) && (ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
   if (vec) {
     const int64_t gx = (ncols / 4 + 255) / 256;
     hipLaunchKernelGGL(mom_cols<4>, dim3((unsigned)gx, nchunks), dim3(256), 0, (hipStream_t)stream, x, len, ncols,
-                       ld, nchunks, part);
+                       ld, nchunks, part, out, kind, ddof, cnt);
   } else {
     const int64_t gx = (ncols + 255) / 256;
     hipLaunchKernelGGL(mom_cols<1>, dim3((unsigned)gx, nchunks), dim3(256), 0, (hipStream_t)stream, x, len, ncols,
-                       ld, nchunks, part);
+                       ld, nchunks, part, out, kind, ddof, cnt);
   }
   return ha_launch_status();
 }

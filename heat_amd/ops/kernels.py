@@ -17,7 +17,7 @@ from . import check, lib, stream_ptr, use_native
 __all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "h3_planes", "H3Planes",
-           "gemm_h3_planes", "householder_qr",
+           "gemm_h3_planes", "gemm64", "cholesky_upper", "tri_inv_upper", "householder_qr",
            "householder_factor", "householder_apply", "householder_block",
            "radix_sort_supported", "sort_rows"]
 
@@ -301,10 +301,38 @@ def merge_moments(n: torch.Tensor, mean: torch.Tensor, m2: torch.Tensor, dim: in
     return N, mu, M2
 
 
-def _moments_native(x: torch.Tensor, axis):
+_MOM_KINDS = {None: 0, "mean": 1, "var": 2, "std": 3}
+_MOM_COUNTERS = {}
+
+
+def _mom_counters(device, n: int) -> torch.Tensor:
+    """Zeroed arrival counters of the fused moments epilogue (the kernels reset what they use)."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    c = _MOM_COUNTERS.get(key)
+    if c is None or c.numel() < n:
+        c = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+        _MOM_COUNTERS[key] = c
+    return c
+
+
+def _moments_native(x: torch.Tensor, axis, final=None, ddof: int = 0):
+    """One launch (``csrc/moments.hip``): per-chunk partials merged by each output's last block.
+    final None: (N, mean, M2) fp64 triples; 'mean' / 'var' / 'std': the fp32 result itself."""
     L = lib()
     s = ctypes.c_void_p(stream_ptr(x.device))
     ncu = num_cus(x.device)
+    kind = _MOM_KINDS[final]
+
+    def out_for(shape):
+        if kind == 0:
+            return torch.empty(tuple(shape) + (3,), dtype=torch.float64, device=x.device)
+        return torch.empty(tuple(shape), dtype=torch.float32, device=x.device)
+
+    def finish(out, shape):
+        if kind:
+            return out
+        return out[..., 0], out[..., 1], out[..., 2]
+
     if axis is None:
         flat = x.reshape(-1)
         if not flat.is_contiguous():
@@ -312,10 +340,10 @@ def _moments_native(x: torch.Tensor, axis):
         numel = flat.numel()
         nchunks = max(1, min(8 * ncu, (numel + 16383) // 16384))
         part = torch.empty((1, nchunks, 3), dtype=torch.float64, device=x.device)
-        check(L.ha_moments_rows(_ptr(flat), 1, numel, numel, nchunks, _ptr(part), s), "ha_moments_rows")
-        N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 1)
-        return N.reshape(()), mu.reshape(()), M2.reshape(())
-    nd = x.dim()
+        out = out_for(())
+        check(L.ha_moments_rows(_ptr(flat), 1, numel, numel, nchunks, _ptr(part), _ptr(out), kind, float(ddof),
+                                _ptr(_mom_counters(x.device, 1)), s), "ha_moments_rows")
+        return finish(out, ())
     if not x.is_contiguous():
         x = x.contiguous()
     shape = list(x.shape)
@@ -331,48 +359,58 @@ def _moments_native(x: torch.Tensor, axis):
         nrows = outer
         nchunks = max(1, min((2 * 8 * ncu + nrows - 1) // max(nrows, 1), (red + 4095) // 4096))
         part = torch.empty((nrows, nchunks, 3), dtype=torch.float64, device=x.device)
-        check(L.ha_moments_rows(_ptr(x), nrows, red, red, nchunks, _ptr(part), s), "ha_moments_rows")
-        if nchunks == 1:
-            N, mu, M2 = part[:, 0, 0], part[:, 0, 1], part[:, 0, 2]
-        else:
-            N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 1)
-    elif outer == 1:
+        out = out_for(out_shape)
+        check(L.ha_moments_rows(_ptr(x), nrows, red, red, nchunks, _ptr(part), _ptr(out), kind, float(ddof),
+                                _ptr(_mom_counters(x.device, nrows) if nchunks > 1 else None), s), "ha_moments_rows")
+        return finish(out, out_shape)
+    if outer == 1:
         ncols = inner
         col_blocks = max(1, (ncols + 1023) // 1024)
         # row chunks: ~2 workgroups per CU, 8 rows in flight per thread (1e6 x 1000, axis 0: 8 per
-        # CU 0.91 ms, 4 0.81 ms, 2 0.76 ms = 5.3 TB/s; fewer partials for the fp64 merge too)
+        # CU 0.91 ms, 4 0.81 ms, 2 0.76 ms = 5.3 TB/s; fewer partials for the merge too)
         cpc = int(os.environ.get("HEAT_MOM_COL_CHUNKS_PER_CU", "2"))
         nchunks = max(1, min(65535, (cpc * ncu + col_blocks - 1) // col_blocks, (red + 63) // 64))
         part = torch.empty((nchunks, ncols, 3), dtype=torch.float64, device=x.device)
-        check(L.ha_moments_cols(_ptr(x), red, ncols, ncols, nchunks, _ptr(part), s), "ha_moments_cols")
-        N, mu, M2 = merge_moments(part[..., 0], part[..., 1], part[..., 2], 0)
-    else:
-        y = x.movedim(axis, -1).contiguous()
-        return _moments_native(y, y.dim() - 1)
-    return N.reshape(out_shape), mu.reshape(out_shape), M2.reshape(out_shape)
+        out = out_for(out_shape)
+        check(L.ha_moments_cols(_ptr(x), red, ncols, ncols, nchunks, _ptr(part), _ptr(out), kind, float(ddof),
+                                _ptr(_mom_counters(x.device, (ncols + 255) // 256)), s), "ha_moments_cols")
+        return finish(out, out_shape)
+    y = x.movedim(axis, -1).contiguous()
+    return _moments_native(y, y.dim() - 1, final, ddof)
 
 
-def moments(x: torch.Tensor, axis: Optional[int] = None):
-    """(count, mean, M2) over ``axis`` (None = all) as float64 tensors.
+def moments(x: torch.Tensor, axis: Optional[int] = None, final: Optional[str] = None, ddof: int = 0):
+    """(count, mean, M2) over ``axis`` (None = all) as float64 tensors; with ``final`` in
+    ('mean', 'var', 'std') the float32 result itself (variance with ``ddof``).
 
-    Device fp32 tensors: one HBM pass with 16-byte loads (``moments.hip``)."""
+    Device fp32 tensors: ONE kernel launch - one HBM pass with 16-byte loads and the chunk merge
+    fused into each output's last block (``moments.hip``)."""
     if use_native(x) and x.dtype == torch.float32 and x.numel() > 0:
-        return _moments_native(x, axis)
+        return _moments_native(x, axis, final, ddof)
     xd = x.double() if not x.is_complex() else x
     if axis is None:
         n = torch.tensor(float(x.numel()), dtype=torch.float64, device=x.device)
         if x.numel() == 0:
             z = torch.tensor(0.0, dtype=torch.float64, device=x.device)
-            return n, z, z.clone()
-        var, mean = torch.var_mean(xd, correction=0)
-        return n, mean, var * n
-    n = torch.full([s for i, s in enumerate(x.shape) if i != axis], float(x.shape[axis]), dtype=torch.float64,
-                   device=x.device)
-    if x.shape[axis] == 0:
-        z = torch.zeros_like(n)
-        return n, z, z.clone()
-    var, mean = torch.var_mean(xd, dim=axis, correction=0)
-    return n, mean, var * n
+            n, mean, m2 = n, z, z.clone()
+        else:
+            var, mean = torch.var_mean(xd, correction=0)
+            m2 = var * n
+    else:
+        n = torch.full([s for i, s in enumerate(x.shape) if i != axis], float(x.shape[axis]), dtype=torch.float64,
+                       device=x.device)
+        if x.shape[axis] == 0:
+            z = torch.zeros_like(n)
+            mean, m2 = z, z.clone()
+        else:
+            var, mean = torch.var_mean(xd, dim=axis, correction=0)
+            m2 = var * n
+    if final is None:
+        return n, mean, m2
+    if final == "mean":
+        return mean
+    v = m2 / (n - ddof)
+    return v.sqrt() if final == "std" else v
 
 
 # --------------------------------------------------------------------------------------------- cdist
@@ -1053,6 +1091,72 @@ def _h3_rows(X: torch.Tensor, Kp: int):
     check(lib().ha_split3_rows(_ptr(X), R, K, X.stride(0), _ptr(hi), _ptr(None), _ptr(lo), Kp, _ptr(ex), _ptr(flag),
                                ctypes.c_void_p(stream_ptr(X.device))), "ha_split3_rows")
     return hi, lo, ex, flag
+
+
+# --------------------------------------------------------------------------------------------- fp64 factor kernels
+def _native64(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.float64 and use_native(t)
+
+
+def gemm64(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
+           beta: float = 0.0, upper: bool = False) -> torch.Tensor:
+    """fp64 ``out = beta * out + alpha * a @ b`` on the fp64 matrix cores (``csrc/linalg64.hip:
+    gemm64``, v_mfma_f64_16x16x4_f64); any row-/column-major operand views. ``upper``: only the
+    entries on or above the diagonal of ``out`` are written. Host tensors: torch."""
+    M, K = a.shape
+    N = b.shape[1]
+    if not _native64(a) or b.dtype != torch.float64:
+        res = alpha * (a @ b)
+        if out is None:
+            out = torch.zeros((M, N), dtype=a.dtype, device=a.device)
+        full = res + beta * out if beta != 0.0 else res
+        if upper:
+            mask = torch.ones((M, N), dtype=torch.bool, device=a.device).triu()
+            out.copy_(torch.where(mask, full, out))
+        else:
+            out.copy_(full)
+        return out
+    if out is None:
+        out = torch.zeros((M, N), dtype=torch.float64, device=a.device)
+    A, lda, a_km = _gemm_operand(a, 1)
+    B, ldb, b_nm = _gemm_operand(b, 1)
+    check(lib().ha_gemm64(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, out.stride(0) if M > 1 else N, int(a_km),
+                          int(not b_nm), int(upper), 1, 0, 0, 0, float(alpha), float(beta),
+                          ctypes.c_void_p(stream_ptr(a.device))), "ha_gemm64")
+    return out
+
+
+def cholesky_upper(g: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Upper Cholesky factor R (G = R^T R) of a symmetric positive definite fp64 matrix and a
+    device int32 ``info`` (0, or 1 + the first failing column). Device tensors: the blocked
+    kernels of ``csrc/linalg64.hip`` (chol_diag / chol_panel / gemm64 trailing update) - no
+    rocSOLVER. Host: torch.linalg.cholesky_ex."""
+    if not _native64(g):
+        r, info = torch.linalg.cholesky_ex(g, upper=True)
+        return r, info.to(torch.int32).reshape(1)
+    n = g.shape[0]
+    R = g.contiguous().clone()
+    info = torch.zeros(1, dtype=torch.int32, device=g.device)
+    if n:
+        check(lib().ha_chol_upper64(_ptr(R), n, R.stride(0), _ptr(info), ctypes.c_void_p(stream_ptr(g.device))),
+              "ha_chol_upper64")
+    return R.triu_(), info
+
+
+def tri_inv_upper(r: torch.Tensor) -> torch.Tensor:
+    """Inverse of an upper-triangular fp64 matrix (``csrc/linalg64.hip``: 64 x 64 diagonal blocks
+    inverted directly, off-diagonal blocks by recursive doubling on gemm64). Host: a triangular
+    solve against the identity."""
+    n = r.shape[0]
+    if not _native64(r):
+        return torch.linalg.solve_triangular(r, torch.eye(n, dtype=r.dtype, device=r.device), upper=True)
+    R = r.contiguous()
+    X = torch.empty((n, n), dtype=torch.float64, device=r.device)
+    W = torch.empty((n, n), dtype=torch.float64, device=r.device)
+    if n:
+        check(lib().ha_trtri_upper64(_ptr(R), n, R.stride(0), _ptr(X), n, _ptr(W),
+                                     ctypes.c_void_p(stream_ptr(r.device))), "ha_trtri_upper64")
+    return X
 
 
 # --------------------------------------------------------------------------------------------- Householder QR

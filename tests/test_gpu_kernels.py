@@ -211,6 +211,52 @@ def test_kmeans_update(n, k, f):
     assert torch.equal(counts.double(), rc)
 
 
+@pytest.mark.parametrize("n,k,f,skew", [(1_000_000, 1024, 64, False), (300_000, 64, 64, True), (70_001, 5, 17, True),
+                                         (200_000, 3000, 8, False), (12345, 33, 100, False)])
+def test_kmeans_update_deterministic(n, k, f, skew):
+    """The default update is order-independent: repeated calls (different scheduling each time) give
+    bit-identical sums, which match an fp64 reference to fp32 rounding. Skewed labels (a few huge
+    clusters spanning many gather ranges, empty clusters) exercise the segment walk."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + k)
+    X = torch.randn(n, f, generator=g).to(dev)
+    if skew:
+        lab = (torch.randn(n, generator=g).abs() * k / 6).long().clamp(max=k - 1)
+        lab[lab == 1] = 0          # an empty cluster
+    else:
+        lab = torch.randint(0, k, (n,), generator=g)
+    lab = lab.to(dev).to(torch.int32)
+    sums, counts = ops.kmeans_update(X, lab, k)
+    for _ in range(3):
+        s2, c2 = ops.kmeans_update(X, lab, k)
+        assert torch.equal(s2, sums) and torch.equal(c2, counts)
+    ref = torch.zeros(k, f, dtype=torch.float64, device=dev).index_add_(0, lab.long(), X.double())
+    rc = torch.bincount(lab.long(), minlength=k).double()
+    assert torch.equal(counts.double(), rc)
+    bound = 1e-6 * torch.zeros(k, f, dtype=torch.float64, device=dev).index_add_(0, lab.long(), X.double().abs()) \
+        + 1e-6
+    assert torch.all((sums.double() - ref).abs() <= 4 * bound), ((sums.double() - ref).abs() / bound).max()
+
+
+def test_kmeans_fit_bit_reproducible():
+    """Two fits with the same seed give bit-identical centroids and labels (deterministic update)."""
+    import heat_amd as ht
+
+    _dev()
+    ht.use_device("gpu")
+    ht.random.seed(5)
+    x = ht.random.randn(400_000, 32, split=0)
+    out = []
+    for _ in range(2):
+        km = ht.cluster.KMeans(n_clusters=256, init="random", max_iter=8, tol=None, random_state=11)
+        km.fit(x)
+        out.append((km.cluster_centers_.larray.clone(), km.labels_.larray.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize("k,f,packed", [(3, 5, True), (3, 5, False), (1024, 64, True), (1024, 64, False),
                                          (5000, 100, False), (7, 1, True)])
 def test_kmeans_finalize(k, f, packed):
@@ -254,6 +300,37 @@ def test_moments(shape, axis):
         rv, rm = torch.var_mean(xd, dim=axis, correction=0)
     assert torch.allclose(mu, rm, rtol=1e-6, atol=1e-5)
     assert torch.allclose(m2 / n, rv, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape,axis", [((3_000_000,), None), ((1000, 5000), None), ((300, 70001), 1),
+                                        ((70001, 300), 0), ((200_000, 3), 0), ((5, 1_000_001), 1),
+                                        ((64, 50, 33), 1), ((1000, 1001), 0), ((1000, 1001), 1)])
+@pytest.mark.parametrize("final", ["mean", "var", "std"])
+def test_moments_fused_final(shape, axis, final):
+    """ONE launch per call: the per-chunk partials are merged by each output's last-arriving block
+    (fixed chunk order, so repeated calls are bit-identical) and the fp32 result written directly."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(sum(shape) + (axis or 0))
+    x = (torch.randn(*shape, generator=g) * 3 + 100).to(dev)
+    ddof = 1 if final != "mean" else 0
+    r = ops.moments(x, axis, final, ddof)
+    assert r.dtype == torch.float32
+    xd = x.double()
+    if axis is None:
+        rv, rm = torch.var_mean(xd, correction=ddof)
+    else:
+        rv, rm = torch.var_mean(xd, dim=axis, correction=ddof)
+    ref = {"mean": rm, "var": rv, "std": rv.sqrt()}[final]
+    assert r.shape == ref.shape
+    assert torch.allclose(r.double(), ref, rtol=2e-6, atol=1e-6), (r.double() - ref).abs().max()
+    for _ in range(3):
+        assert torch.equal(ops.moments(x, axis, final, ddof), r)
+    # the triples path agrees with the fused one
+    n, mu, m2 = ops.moments(x, axis)
+    if final == "mean":
+        assert torch.equal(mu.float(), r)
 
 
 @pytest.mark.parametrize("exact", [False, True])

@@ -54,3 +54,91 @@ def test_ht_qr_ill_conditioned_uses_householder(gpu):
     assert (qt.T @ qt - torch.eye(200, dtype=torch.float64, device=qt.device)).abs().max().item() < 1e-5
     rec = (qt @ r.larray.double() - A.larray.double()).abs().max().item()
     assert rec < 1e-5 * A.larray.abs().max().item()
+
+
+# ------------------------------------------------------------ fp64 factor kernels (csrc/linalg64.hip)
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 200, 1000, 4096])
+def test_cholesky_upper_device(n):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(n)
+    a = torch.randn(n + 7, n, generator=g, dtype=torch.float64)
+    G = (a.T @ a).to(dev)
+    R, info = ops.cholesky_upper(G)
+    assert int(info.item()) == 0
+    assert torch.equal(R, torch.triu(R)) and bool((torch.diagonal(R) > 0).all())
+    rel = ((R.T @ R - G).abs().max() / G.abs().max()).item()
+    assert rel < 1e-13 * max(1, n // 64), rel
+    ref = torch.linalg.cholesky(G.cpu(), upper=True)
+    assert torch.allclose(R.cpu(), ref, rtol=1e-9, atol=1e-9 * ref.abs().max().item())
+
+
+def test_cholesky_upper_reports_breakdown():
+    from heat_amd import ops
+
+    dev = _dev()
+    G = torch.eye(300, dtype=torch.float64)
+    G[150, 150] = -1.0
+    _, info = ops.cholesky_upper(G.to(dev))
+    assert int(info.item()) == 151
+
+
+@pytest.mark.parametrize("n", [1, 64, 100, 129, 513, 1000, 4096])
+def test_tri_inv_upper_device(n):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(3 * n)
+    R = torch.triu(torch.randn(n, n, generator=g, dtype=torch.float64)) + 4 * torch.eye(n, dtype=torch.float64)
+    R = R.to(dev)
+    X = ops.tri_inv_upper(R)
+    assert torch.equal(X, torch.triu(X))
+    err = (X @ R - torch.eye(n, dtype=torch.float64, device=dev)).abs().max().item()
+    assert err < 1e-12 * max(1, n // 16), err
+
+
+@pytest.mark.parametrize("m,k,n", [(64, 64, 64), (100, 37, 300), (1000, 64, 1000), (3, 5, 7)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+def test_gemm64_layouts_upper(m, k, n, layout):
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + k + n)
+    a = torch.randn(m, k, generator=g, dtype=torch.float64)
+    b = torch.randn(k, n, generator=g, dtype=torch.float64)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    c0 = torch.randn(m, n, generator=g, dtype=torch.float64)
+    c = c0.clone().to(dev)
+    ops.gemm64(A.to(dev), B.to(dev), out=c, alpha=-2.0, beta=0.5)
+    ref = 0.5 * c0 - 2.0 * (a @ b)
+    assert torch.allclose(c.cpu(), ref, rtol=1e-12, atol=1e-12 * k)
+    cu = c0.clone().to(dev)
+    ops.gemm64(A.to(dev), B.to(dev), out=cu, upper=True)
+    mask = torch.ones(m, n, dtype=torch.bool).triu()
+    assert torch.allclose(cu.cpu(), torch.where(mask, a @ b, c0), rtol=1e-12, atol=1e-12 * k)
+
+
+@pytest.mark.parametrize("precision", ["highest", "high"])
+@pytest.mark.parametrize("m,n", [(100_000, 256), (20_000, 300), (4096, 64)])
+def test_cholqr_native_path(m, n, precision):
+    """Device fp32 CholeskyQR2 on the hand-written kernels (gemm_tiled + linalg64): orthogonal Q,
+    Q R = A to fp32-GEMM accuracy, R upper with a non-negative diagonal."""
+    import heat_amd as ht
+
+    dev = _dev()
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(precision)
+    try:
+        a = _ill(m, n, 50.0, m + n, torch.float32)
+        x = ht.array(a.to(dev), split=None)
+        q, r = ht.linalg.qr(x, mode="reduced")
+        Q, R = q.larray.double(), r.larray.double()
+        orth = (Q.T @ Q - torch.eye(n, dtype=torch.float64, device=dev)).abs().max().item()
+        assert orth < 1e-5, orth
+        rec = (Q @ R - a.to(dev).double()).abs().max().item() / a.abs().max().item()
+        assert rec < 1e-5, rec
+        assert torch.equal(R, torch.triu(R)) and bool((torch.diagonal(R) >= 0).all())
+    finally:
+        torch.set_float32_matmul_precision(old)
