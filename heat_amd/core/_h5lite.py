@@ -6,9 +6,11 @@ Reading covers what h5py (default settings) and the netCDF-4 library write for p
 arrays: superblock v0-v3, object headers v1 and v2 ("OHDR"/"OCHK" continuation blocks), groups
 as symbol tables (v1 B-tree + SNOD + local heap) or compact link messages, dataspace v1/v2,
 fixed-point / IEEE float datatypes, and layouts contiguous, compact and chunked (v1 B-tree chunk
-index, or a v4 single-chunk index) without filters. Datasets are returned as lazy
-:class:`H5Dataset` objects whose slices read only the addressed rows (``numpy.memmap`` over
-contiguous storage), so every rank of a split load touches just its own byte range.
+index, or a v4 single-chunk index), chunks optionally filtered by deflate (gzip), shuffle and
+fletcher32 (the filters h5py's ``compression="gzip"``, ``shuffle=True``, ``fletcher32=True`` write).
+Datasets are returned as lazy :class:`H5Dataset` objects whose slices read only the addressed
+rows (``numpy.memmap`` over contiguous storage; for chunked storage only the chunks the slice
+touches are read and decompressed), so every rank of a split load touches just its own byte range.
 
 Writing produces an HDF5 file that h5py/HDF5 tools read: superblock v0, a root group with a
 symbol table sized for many datasets, v1 object headers, contiguous storage. A dataset is
@@ -20,11 +22,13 @@ from __future__ import annotations
 
 import os
 import struct
+import zlib
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
-__all__ = ["is_hdf5", "open_file", "H5File", "H5Dataset", "create_file", "create_dataset", "open_for_write"]
+__all__ = ["is_hdf5", "open_file", "H5File", "H5Dataset", "create_file", "create_dataset", "open_for_write",
+           "create_chunked_dataset", "append_chunks", "finish_chunked", "chunk_filters", "encode_chunk"]
 
 _SIG = b"\x89HDF\r\n\x1a\n"
 _UNDEF = 0xFFFFFFFFFFFFFFFF
@@ -65,28 +69,97 @@ class H5Dataset:
             return np.memmap(self.path, dtype=self.dtype, mode="r", offset=self._layout["address"], shape=self.shape)
         if kind == "compact":
             return np.frombuffer(self._layout["data"], dtype=self.dtype).reshape(self.shape)
-        return self._read_chunked()
+        return self._read_region(tuple(0 for _ in self.shape), self.shape)
 
-    def _read_chunked(self) -> np.ndarray:
-        out = np.zeros(self.shape, self.dtype)
+    def _decode(self, raw: bytes, mask: int) -> bytes:
+        """Undo the filter pipeline (reverse order; filter i skipped where bit i of the chunk's
+        mask is set)."""
+        filters = self._layout.get("filters") or []
+        for i in range(len(filters) - 1, -1, -1):
+            if mask >> i & 1:
+                continue
+            fid, cd = filters[i]
+            if fid == 1:      # deflate
+                raw = zlib.decompress(raw)
+            elif fid == 2:    # shuffle: byte planes back into elements
+                es = cd[0] if cd else self.dtype.itemsize
+                n = len(raw) // es
+                body = np.frombuffer(raw, np.uint8, n * es).reshape(es, n).T.tobytes()
+                raw = body + raw[n * es:]
+            elif fid == 3:    # fletcher32: trailing 4-byte checksum
+                raw = raw[:-4]
+            else:
+                raise NotImplementedError("HDF5 filter {} needs h5py".format(fid))
+        return raw
+
+    def _read_region(self, start, stop) -> np.ndarray:
+        """The box [start, stop) of a chunked dataset, reading (and decoding) only the chunks that
+        intersect it."""
+        out = np.zeros(tuple(b - a for a, b in zip(start, stop)), self.dtype)
+        if out.size == 0:
+            return out
         cdims = self._layout["chunk"]
+        nel = int(np.prod(cdims))
         with open(self.path, "rb") as f:
             for offs, addr, size, mask in self._layout["chunks"](f):
-                if mask:
-                    raise NotImplementedError("filtered (compressed) HDF5 chunks need h5py")
+                lo = [max(o, a) for o, a in zip(offs, start)]
+                hi = [min(o + c, s, b) for o, c, s, b in zip(offs, cdims, self.shape, stop)]
+                if any(h <= l for l, h in zip(lo, hi)):
+                    continue
                 f.seek(addr)
-                raw = np.frombuffer(f.read(size), dtype=self.dtype)
-                blk = raw[: int(np.prod(cdims))].reshape(cdims)
-                sl = tuple(slice(o, min(o + c, s)) for o, c, s in zip(offs, cdims, self.shape))
-                out[sl] = blk[tuple(slice(0, x.stop - x.start) for x in sl)]
+                raw = f.read(size)
+                if self._layout.get("filters"):
+                    raw = self._decode(raw, mask)
+                blk = np.frombuffer(raw, dtype=self.dtype, count=nel).reshape(cdims)
+                src = tuple(slice(l - o, h - o) for l, h, o in zip(lo, hi, offs))
+                dst = tuple(slice(l - a, h - a) for l, h, a in zip(lo, hi, start))
+                out[dst] = blk[src]
         return out
 
     def __getitem__(self, key) -> np.ndarray:
+        if self._layout["kind"] == "chunked":
+            box = _basic_box(key, self.shape)
+            if box is not None:
+                start, stop, post = box
+                return np.array(self._read_region(start, stop)[post])
         return np.array(self._contiguous()[key])
 
     def __array__(self, dtype=None):
         a = np.array(self._contiguous())
         return a.astype(dtype) if dtype is not None else a
+
+
+def _basic_box(key, shape):
+    """(start, stop, post-index) of a basic NumPy key made of ints, unit-step slices and at most
+    one Ellipsis; None for anything else (fancy / strided keys read the whole array)."""
+    if not isinstance(key, tuple):
+        key = (key,)
+    if sum(k is Ellipsis for k in key) > 1:
+        return None
+    if Ellipsis in key:
+        i = key.index(Ellipsis)
+        key = key[:i] + (slice(None),) * (len(shape) - len(key) + 1) + key[i + 1:]
+    key = key + (slice(None),) * (len(shape) - len(key))
+    if len(key) != len(shape):
+        return None
+    start, stop, post = [], [], []
+    for k, n in zip(key, shape):
+        if isinstance(k, (int, np.integer)) and not isinstance(k, bool):
+            k = int(k) + (n if k < 0 else 0)
+            if not 0 <= k < n:
+                return None
+            start.append(k)
+            stop.append(k + 1)
+            post.append(0)
+        elif isinstance(k, slice) and k.step in (None, 1):
+            a, b, _ = k.indices(n)
+            b = max(a, b)
+            start.append(a)
+            stop.append(b)
+            post.append(slice(None))
+        else:
+            return None
+    return start, stop, tuple(post)
 
 
 class _Reader:
@@ -264,6 +337,7 @@ class _Reader:
     # ------------------------------------------------------------ datasets
     def dataset(self, addr: int) -> Optional[H5Dataset]:
         shape = dtype = layout = None
+        filters = []
         attrs = {}
         for t, data in self.messages(addr):
             if t == 0x01:
@@ -273,13 +347,9 @@ class _Reader:
             elif t == 0x08:
                 layout = self._layout(data)
             elif t == 0x0B:
-                nf = data[1]
-                if nf:
-                    layout = {"kind": "filtered"}
+                filters = self._filters(data)
         if shape is None or dtype is None or layout is None:
             return None
-        if layout["kind"] == "filtered":
-            raise NotImplementedError("filtered (compressed) HDF5 datasets need h5py")
         if layout["kind"] == "chunked-btree":
             btree, cd = layout["btree"], layout["chunk"]
             rd = self
@@ -292,7 +362,39 @@ class _Reader:
             cd, addr_, size_, mask_ = layout["chunk"], layout["address"], layout["size"], layout["mask"]
             layout = {"kind": "chunked", "chunk": cd,
                       "chunks": lambda f, _a=addr_, _s=size_, _m=mask_, _n=len(cd): [((0,) * _n, _a, _s, _m)]}
+        if filters:
+            if layout["kind"] != "chunked":
+                raise NotImplementedError("filters on non-chunked HDF5 storage")
+            for fid, _ in filters:
+                if fid not in (1, 2, 3):
+                    raise NotImplementedError("HDF5 filter {} needs h5py".format(fid))
+            layout["filters"] = filters
         return H5Dataset(self.path, shape, dtype, layout, attrs)
+
+    @staticmethod
+    def _filters(d: bytes) -> List[Tuple[int, List[int]]]:
+        """Filter pipeline message (0x000B) v1 / v2 -> [(filter id, client data)] in pipeline order."""
+        ver, nf = d[0], d[1]
+        p = 8 if ver == 1 else 2
+        out = []
+        for _ in range(nf):
+            fid = int.from_bytes(d[p: p + 2], "little")
+            p += 2
+            nlen = 0
+            if ver == 1 or fid >= 256:
+                nlen = int.from_bytes(d[p: p + 2], "little")
+                p += 2
+            p += 2  # flags
+            ncd = int.from_bytes(d[p: p + 2], "little")
+            p += 2
+            if nlen:
+                p += nlen + ((-nlen) % 8 if ver == 1 else 0)
+            cd = [int.from_bytes(d[p + 4 * i: p + 4 * i + 4], "little") for i in range(ncd)]
+            p += 4 * ncd
+            if ver == 1 and ncd % 2:
+                p += 4
+            out.append((fid, cd))
+        return out
 
     def _dataspace(self, d: bytes) -> Tuple[int, ...]:
         ver, ndim, flags = d[0], d[1], d[2]
@@ -510,78 +612,275 @@ def create_file(path: str) -> None:
         f.write(bytes(buf))
 
 
+def _add_object(f, name: str, build) -> int:
+    """Insert ``name`` into the root symbol table of an open file made by :func:`create_file`;
+    ``build(oh_addr)`` returns (object header bytes, end of the object's data). Returns the
+    object header address."""
+    L = _root_layout()
+    f.seek(0, os.SEEK_END)
+    eof = f.tell()
+    f.seek(L["snod"] + 6)
+    nsym = struct.unpack("<H", f.read(2))[0]
+    if nsym >= 2 * _LEAF_K:
+        raise NotImplementedError("more than {} datasets in one file".format(2 * _LEAF_K))
+    f.seek(L["heap"] + 16)
+    free_off = struct.unpack("<Q", f.read(8))[0]
+    raw = name.encode("utf-8") + b"\0"
+    need = len(raw) + ((-len(raw)) % 8)
+    if free_off == _UNDEF or free_off + need + 16 > _HEAP_SIZE:
+        raise NotImplementedError("dataset name heap of {} bytes is full".format(_HEAP_SIZE))
+    # entries must stay sorted by name: read them, insert, rewrite
+    ent_size = 2 * _SO + 24
+    f.seek(L["snod"] + 8)
+    ents = [f.read(ent_size) for _ in range(nsym)]
+    f.seek(L["heap_data"])
+    heap = f.read(_HEAP_SIZE)
+
+    def ename(e):
+        o = struct.unpack_from("<Q", e, 0)[0]
+        return heap[o: heap.index(b"\0", o)].decode("utf-8")
+
+    if any(ename(e) == name for e in ents):
+        raise ValueError("dataset {} exists".format(name))
+    oh_addr = eof + ((-eof) % 8)
+    oh, end = build(oh_addr)
+    f.seek(oh_addr)
+    f.write(oh)
+    f.truncate(max(end, oh_addr + len(oh)))
+    # name into the heap, free list moves on
+    f.seek(L["heap_data"] + free_off)
+    f.write(raw + b"\0" * ((-len(raw)) % 8))
+    new_free = free_off + need
+    f.seek(L["heap_data"] + new_free)
+    f.write(struct.pack("<QQ", 1, _HEAP_SIZE - new_free))
+    f.seek(L["heap"] + 16)
+    f.write(struct.pack("<Q", new_free))
+    heap = heap[:free_off] + raw + heap[free_off + len(raw):]
+    ents.append(struct.pack("<QQII", free_off, oh_addr, 0, 0) + b"\0" * 16)
+    ents.sort(key=ename)
+    f.seek(L["snod"] + 6)
+    f.write(struct.pack("<H", len(ents)))
+    f.write(b"".join(ents))
+    # B-tree key1 = heap offset of the largest name in the node
+    f.seek(L["btree"] + 8 + 2 * _SO + 2 * 8)
+    f.write(struct.pack("<Q", struct.unpack_from("<Q", ents[-1], 0)[0]))
+    _set_eof(f, max(end, oh_addr + len(oh)))
+    return oh_addr
+
+
+def _set_eof(f, end: int) -> None:
+    f.seek(8 + 16 + 16)
+    f.write(struct.pack("<Q", end))
+
+
+def _dspace(shape) -> bytes:
+    return struct.pack("<BBBB4x", 1, len(shape), 0, 0) + b"".join(struct.pack("<Q", int(s)) for s in shape)
+
+
 def create_dataset(path: str, name: str, shape: Tuple[int, ...], dtype) -> int:
     """Declare a contiguous dataset in a file made by :func:`create_file`; storage is allocated
     (zero-filled) at the end of the file. Returns the byte offset of the data."""
-    L = _root_layout()
     dt = np.dtype(dtype)
     if dt.kind == "b":
         dt = np.dtype("u1")
     nbytes = int(np.prod(shape)) * dt.itemsize
-    with open(path, "r+b") as f:
-        f.seek(0, os.SEEK_END)
-        eof = f.tell()
-        f.seek(L["snod"] + 6)
-        nsym = struct.unpack("<H", f.read(2))[0]
-        if nsym >= 2 * _LEAF_K:
-            raise NotImplementedError("more than {} datasets in one file".format(2 * _LEAF_K))
-        f.seek(L["heap"] + 16)
-        free_off = struct.unpack("<Q", f.read(8))[0]
-        raw = name.encode("utf-8") + b"\0"
-        need = len(raw) + ((-len(raw)) % 8)
-        if free_off == _UNDEF or free_off + need + 16 > _HEAP_SIZE:
-            raise NotImplementedError("dataset name heap of {} bytes is full".format(_HEAP_SIZE))
-        # entries must stay sorted by name: read them, insert, rewrite
-        ent_size = 2 * _SO + 24
-        f.seek(L["snod"] + 8)
-        ents = [f.read(ent_size) for _ in range(nsym)]
-        f.seek(L["heap_data"])
-        heap = f.read(_HEAP_SIZE)
+    fill = struct.pack("<BBBB", 2, 2, 2, 0)  # fill value message v2: write time never, undefined
+    res = {}
 
-        def ename(e):
-            o = struct.unpack_from("<Q", e, 0)[0]
-            return heap[o: heap.index(b"\0", o)].decode("utf-8")
-
-        if any(ename(e) == name for e in ents):
-            raise ValueError("dataset {} exists".format(name))
-        # object header of the dataset, data right after it (8-aligned)
-        oh_addr = eof + ((-eof) % 8)
-        ndim = len(shape)
-        dspace = struct.pack("<BBBB4x", 1, ndim, 0, 0) + b"".join(struct.pack("<Q", int(s)) for s in shape)
-        layout = struct.pack("<BBQQ", 3, 1, 0, nbytes)
-        fill = struct.pack("<BBBB", 2, 2, 2, 0)  # fill value message v2: write time never, undefined
-        msgs = [_msg(0x01, dspace), _msg(0x03, _dtype_msg(dt)), _msg(0x05, fill), _msg(0x08, layout)]
-        oh = _ohdr(msgs)
+    def build(oh_addr):
+        def msgs(addr):
+            return [_msg(0x01, _dspace(shape)), _msg(0x03, _dtype_msg(dt)), _msg(0x05, fill),
+                    _msg(0x08, struct.pack("<BBQQ", 3, 1, addr, nbytes))]
+        oh = _ohdr(msgs(0))
         data_addr = oh_addr + len(oh)
         data_addr += (-data_addr) % 64
-        layout = struct.pack("<BBQQ", 3, 1, data_addr, nbytes)
-        msgs[3] = _msg(0x08, layout)
+        res["data"] = data_addr
+        return _ohdr(msgs(data_addr)), data_addr + nbytes
+
+    with open(path, "r+b") as f:
+        _add_object(f, name, build)
+    return res["data"]
+
+
+# ---------------------------------------------------------------- chunked + filtered (compressed)
+_ISTORE_K = 32   # chunk B-tree node: 2K entries (the v0 superblock default)
+
+
+def _filter_msg(filters) -> bytes:
+    """Filter pipeline message v1 for [(id, client data)]."""
+    body = struct.pack("<BB6x", 1, len(filters))
+    for fid, cd in filters:
+        body += struct.pack("<HHHH", fid, 0, 0, len(cd)) + b"".join(struct.pack("<I", int(c)) for c in cd)
+        if len(cd) % 2:
+            body += b"\0" * 4
+    return body
+
+
+def chunk_filters(dtype, compression=None, compression_opts=None, shuffle=False, fletcher32=False):
+    """The filter pipeline h5py builds for ``create_dataset(compression=..., shuffle=...,
+    fletcher32=...)``: [(id, client data)] - shuffle, then deflate, then fletcher32."""
+    filters = []
+    dt = np.dtype(dtype)
+    if shuffle:
+        filters.append((2, [dt.itemsize]))
+    if compression is not None:
+        if compression not in ("gzip", 1, "deflate"):
+            raise NotImplementedError("compression {!r}: only gzip (deflate) without h5py".format(compression))
+        level = 4 if compression_opts is None else int(compression_opts)
+        if not 0 <= level <= 9:
+            raise ValueError("gzip compression level must be in [0, 9], got {}".format(level))
+        filters.append((1, [level]))
+    if fletcher32:
+        filters.append((3, []))
+    return filters
+
+
+def encode_chunk(block: np.ndarray, filters) -> bytes:
+    """Apply a filter pipeline to one chunk (C order, full chunk shape)."""
+    raw = np.ascontiguousarray(block).tobytes()
+    for fid, cd in filters:
+        if fid == 2:
+            es = cd[0]
+            n = len(raw) // es
+            raw = np.frombuffer(raw, np.uint8, n * es).reshape(n, es).T.tobytes() + raw[n * es:]
+        elif fid == 1:
+            raw = zlib.compress(raw, cd[0])
+        elif fid == 3:
+            raw = raw + struct.pack("<I", _fletcher32(raw))
+        else:
+            raise NotImplementedError("HDF5 filter {}".format(fid))
+    return raw
+
+
+def _fletcher32(data: bytes) -> int:
+    """HDF5's Fletcher-32 over 16-bit big-endian words (odd trailing byte padded)."""
+    if len(data) % 2:
+        data = data + b"\0"
+    w = np.frombuffer(data, dtype=">u2").astype(np.uint64)
+    s1 = s2 = 0
+    for i in range(0, len(w), 360):
+        blk = w[i: i + 360]
+        c1 = np.cumsum(blk) + s1
+        s2 = int((s2 + c1.sum()) % 65535)
+        s1 = int(c1[-1] % 65535)
+    return (s2 << 16) | s1
+
+
+def create_chunked_dataset(path: str, name: str, shape: Tuple[int, ...], dtype, chunks: Tuple[int, ...],
+                           filters) -> int:
+    """Declare a chunked (optionally filtered) dataset; returns its object header address. Its
+    chunks are appended by :func:`append_chunks` and indexed by :func:`finish_chunked`."""
+    dt = np.dtype(dtype)
+    if dt.kind == "b":
+        dt = np.dtype("u1")
+    if len(chunks) != len(shape) or any(c < 1 for c in chunks):
+        raise ValueError("chunks {} do not fit shape {}".format(chunks, shape))
+    fill = struct.pack("<BBBB", 2, 2, 2, 0)
+
+    def build(oh_addr):
+        layout = struct.pack("<BBBQ", 3, 2, len(shape) + 1, _UNDEF) + \
+            b"".join(struct.pack("<I", int(c)) for c in chunks) + struct.pack("<I", dt.itemsize)
+        msgs = [_msg(0x01, _dspace(shape)), _msg(0x03, _dtype_msg(dt)), _msg(0x05, fill)]
+        if filters:
+            msgs.append(_msg(0x0B, _filter_msg(filters)))
+        msgs.append(_msg(0x08, layout))
         oh = _ohdr(msgs)
-        f.seek(oh_addr)
-        f.write(oh)
-        f.truncate(data_addr + nbytes)
-        # name into the heap, free list moves on
-        f.seek(L["heap_data"] + free_off)
-        f.write(raw + b"\0" * ((-len(raw)) % 8))
-        new_free = free_off + need
-        f.seek(L["heap_data"] + new_free)
-        f.write(struct.pack("<QQ", 1, _HEAP_SIZE - new_free))
-        f.seek(L["heap"] + 16)
-        f.write(struct.pack("<Q", new_free))
-        heap = heap[:free_off] + raw + heap[free_off + len(raw):]
-        new_ent = struct.pack("<QQII", free_off, oh_addr, 0, 0) + b"\0" * 16
-        ents.append(new_ent)
-        ents.sort(key=ename)
-        f.seek(L["snod"] + 6)
-        f.write(struct.pack("<H", len(ents)))
-        f.write(b"".join(ents))
-        # B-tree key1 = heap offset of the largest name in the node
-        f.seek(L["btree"] + 8 + 2 * _SO + 2 * 8)
-        f.write(struct.pack("<Q", struct.unpack_from("<Q", ents[-1], 0)[0]))
-        # superblock end-of-file address
-        f.seek(8 + 16 + 16)
-        f.write(struct.pack("<Q", data_addr + nbytes))
-    return data_addr
+        return oh, oh_addr + len(oh)
+
+    with open(path, "r+b") as f:
+        return _add_object(f, name, build)
+
+
+def append_chunks(path: str, offset: int, blobs: List[bytes]) -> None:
+    """Write encoded chunks back to back at ``offset`` (every rank its own byte range)."""
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        pos = offset
+        for b in blobs:
+            os.pwrite(fd, b, pos)
+            pos += len(b)
+    finally:
+        os.close(fd)
+
+
+def finish_chunked(path: str, name: str, records, data_end: int) -> None:
+    """Index the chunks of a dataset declared by :func:`create_chunked_dataset`: ``records`` are
+    (chunk offsets, file address, stored size, filter mask) for every chunk; the v1 B-tree (2K
+    entries per node, as many levels as needed) goes at ``data_end`` and the layout message is
+    patched to point at its root."""
+    with open(path, "r+b") as f:
+        r = _Reader(path)
+        try:
+            oh_addr = _resolve_root(r, name)
+            lay_pos, ndim1 = _layout_msg_pos(r, oh_addr)
+        finally:
+            r.close()
+        recs = sorted(records, key=lambda x: tuple(x[0]))
+        nd = ndim1 - 1
+        cap = 2 * _ISTORE_K
+        keysz = 8 + 8 * ndim1
+        node_size = 8 + 2 * _SO + cap * _SO + (cap + 1) * keysz
+        pos = data_end + ((-data_end) % 8)
+
+        def key(size, mask, offs):
+            return struct.pack("<II", size, mask) + b"".join(struct.pack("<Q", int(o)) for o in offs) + \
+                struct.pack("<Q", 0)
+
+        # chunk dims for the right-bound key
+        f.seek(lay_pos + 3 + 8)
+        cdims = struct.unpack("<" + "I" * nd, f.read(4 * nd))
+        entries = [(key(sz, m, offs), addr, tuple(int(o) + c for o, c in zip(offs, cdims)))
+                   for offs, addr, sz, m in recs]
+        level = 0
+        while True:
+            groups = [entries[i: i + cap] for i in range(0, len(entries), cap)] or [[]]
+            addrs = [pos + i * node_size for i in range(len(groups))]
+            nxt = []
+            for gi, grp in enumerate(groups):
+                left = addrs[gi - 1] if gi > 0 else _UNDEF
+                right = addrs[gi + 1] if gi + 1 < len(groups) else _UNDEF
+                body = b"TREE" + struct.pack("<BBH", 1, level, len(grp)) + struct.pack("<QQ", left, right)
+                for k, child, _ in grp:
+                    body += k + struct.pack("<Q", child)
+                end_offs = grp[-1][2] if grp else (0,) * nd
+                body += key(0, 0, end_offs)
+                body += b"\0" * (node_size - len(body))
+                f.seek(addrs[gi])
+                f.write(body)
+                if grp:
+                    nxt.append((grp[0][0], addrs[gi], grp[-1][2]))
+            pos += len(groups) * node_size
+            if len(groups) == 1:
+                root = addrs[0]
+                break
+            entries = nxt
+            level += 1
+        f.seek(lay_pos + 3)
+        f.write(struct.pack("<Q", root))
+        _set_eof(f, pos)
+
+
+def _resolve_root(r: "_Reader", name: str) -> int:
+    addr = r.root
+    for part in [p for p in name.split("/") if p]:
+        kids = r.children(addr)
+        if part not in kids:
+            raise KeyError(name)
+        addr = kids[part]
+    return addr
+
+
+def _layout_msg_pos(r: "_Reader", oh_addr: int) -> Tuple[int, int]:
+    """File position of the body of the (v1 object header) layout message and its rank (+1)."""
+    ver, _, nmsg, _, hsize = struct.unpack("<BBHII", r._read(oh_addr, 12))
+    p = oh_addr + 16
+    for _ in range(nmsg):
+        t, size, _flags = struct.unpack("<HHB", r._read(p, 5))
+        if t == 0x08:
+            body = r._read(p + 8, size)
+            return p + 8, body[2]
+        p += 8 + size
+    raise KeyError("no layout message")
 
 
 def open_for_write(path: str, name: str) -> np.memmap:

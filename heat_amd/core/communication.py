@@ -546,6 +546,10 @@ class MPICommunication(Communication):
             counts = self.allgather_sizes(moved.shape[0])
         rest = tuple(moved.shape[1:])
         got = self._ipc_allgather(moved, counts) if len(counts) else None
+        if got is None and moved.is_cuda and len(counts) and self._native() is not None \
+                and moved.dtype in (torch.int8, torch.uint8, torch.bool, torch.int32, torch.int64, torch.float16,
+                                    torch.float32, torch.float64, torch.bfloat16):
+            got = self._native().allgatherv(moved, counts)  # grouped RCCL p2p on the current stream
         if got is not None:
             return _SD.StagedWork(None), (lambda: got.movedim(0, axis) if axis != 0 else got)
         mx = max(counts) if len(counts) else 0
@@ -565,6 +569,22 @@ class MPICommunication(Communication):
             return res.movedim(0, axis) if axis != 0 else res
 
         return work, fin
+
+    def reduce_scatter_tensor(self, out: torch.Tensor, inp: torch.Tensor, op: Op = None) -> torch.Tensor:
+        """``out`` = this rank's 1/size block (along dim 0) of the element-wise SUM (or ``op``) of
+        every rank's ``inp`` - the native stream-ordered RCCL reduce-scatter under
+        ``HEAT_COMM_NATIVE=1``, else torch's (host-staged for a gloo group)."""
+        op = MPI.SUM if op is None else op
+        self._trace("Reduce_scatter", inp)
+        if self.size == 1:
+            return out.copy_(inp)
+        opname = {MPI.SUM: "sum", MPI.PROD: "prod", MPI.MAX: "max", MPI.MIN: "min"}.get(op)
+        nc = self._native() if inp.is_cuda else None
+        if nc is not None and opname is not None and nc.supports(inp, opname) and inp.is_contiguous() \
+                and out.is_contiguous():
+            return nc.reduce_scatter(inp, out, opname)
+        _SD.reduce_scatter_tensor(out, inp, op=op.torch_op, group=self.group)
+        return out
 
     def allgather_tensor(self, t: torch.Tensor, axis: int = 0, counts: Optional[Sequence[int]] = None) -> torch.Tensor:
         """Return the concatenation of all ranks' tensors along ``axis`` (sizes may differ)."""

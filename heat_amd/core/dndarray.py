@@ -308,9 +308,23 @@ class DNDarray:
 
         from ..parallel import staging as _SD
 
-        ops, recv_prev, recv_next = [], None, None
         comm = self.comm
         wire = torch.uint8 if a.dtype == torch.bool else a.dtype
+        # xGMI peer path (HEAT_IPC_ALLREDUCE=1, node-local device job): every rank's [first; last]
+        # slices in ONE direct all-gather kernel - each rank reads its peers' slots over their own
+        # links - and the neighbours' slices are picked out (no per-neighbour RCCL send/recv)
+        got = None
+        if a.is_cuda and len(active) == p:
+            both = torch.cat([first, last], dim=s).to(wire).movedim(s, 0).contiguous()
+            got = comm._ipc_allgather(both, [2 * halo_size] * p)
+        if got is not None:
+            g = got.movedim(0, s) if s != 0 else got
+            prev_t = g.narrow(s, (2 * (rank - 1) + 1) * halo_size, halo_size) if prev_r is not None else None
+            next_t = g.narrow(s, 2 * (rank + 1) * halo_size, halo_size) if next_r is not None else None
+            self.__halo_prev = None if prev_t is None else prev_t.to(a.dtype).contiguous()
+            self.__halo_next = None if next_t is None else next_t.to(a.dtype).contiguous()
+            return
+        ops, recv_prev, recv_next = [], None, None
         if prev_r is not None:
             ops.append(dist.P2POp(dist.isend, first.to(wire).contiguous(), comm._g(prev_r), comm.group))
             recv_prev = torch.empty(shape, dtype=wire, device=a.device)

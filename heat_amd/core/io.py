@@ -250,6 +250,8 @@ def save_hdf5(data: DNDarray, path: str, dataset: str, mode: str = "w", **kwargs
     comm = data.comm
     np_dtype = np.dtype(torch.empty(0, dtype=data.larray.dtype).numpy().dtype)
     counts, displs = data.counts_displs() if data.is_distributed() else ((None,), (None,))
+    if h5py is None and any(kwargs.get(k) for k in ("compression", "chunks", "shuffle", "fletcher32")):
+        return _save_hdf5_chunked(data, path, dataset, mode, np_dtype, **kwargs)
     exc = None
     if comm.rank == 0:
         try:
@@ -281,6 +283,92 @@ def save_hdf5(data: DNDarray, path: str, dataset: str, mode: str = "w", **kwargs
         if counts[me]:
             _write_slab(path, dataset, tuple(sl), local)
         comm.Barrier()
+
+
+def _save_hdf5_chunked(data: DNDarray, path: str, dataset: str, mode: str, np_dtype, compression=None,
+                       compression_opts=None, chunks=None, shuffle=False, fletcher32=False, **unused) -> None:
+    """Chunked / compressed HDF5 without h5py (the reference passes these keywords to h5py's
+    ``create_dataset``, ``heat/core/io.py:185-197``). Chunks are a grid over the array; every rank
+    encodes (shuffle / deflate / fletcher32) the chunks whose first row along the split axis it
+    holds - the rows of a chunk that continue on the next ranks arrive in ONE exchange of the
+    ranks' leading rows - then the encoded sizes are all-gathered, every rank writes its chunks at
+    its own file offset in parallel, and rank 0 writes the chunk B-tree."""
+    comm = data.comm
+    if np_dtype == np.dtype("bool"):
+        np_dtype = np.dtype("u1")
+    gshape = tuple(int(s) for s in data.gshape)
+    nd = len(gshape)
+    split = data.split if data.is_distributed() else None
+    if chunks is None or chunks is True:
+        # ~1 MiB chunks: full extent in the trailing dimensions, rows along the first
+        row = int(np.prod(gshape[1:])) * np_dtype.itemsize if nd > 1 else np_dtype.itemsize
+        chunks = (max(1, min(gshape[0] if nd else 1, (1 << 20) // max(row, 1))),) + tuple(gshape[1:])
+    chunks = tuple(max(1, min(int(c), max(1, s))) for c, s in zip(chunks, gshape))
+    filters = _h5lite.chunk_filters(np_dtype, compression, compression_opts, shuffle, fletcher32)
+    local = np.ascontiguousarray(data.larray.cpu().numpy()).astype(np_dtype, copy=False)
+    exc = None
+    if comm.rank == 0:
+        try:
+            if mode == "w" or not os.path.exists(path):
+                _h5lite.create_file(path)
+            _h5lite.create_chunked_dataset(path, dataset, gshape, np_dtype, chunks, filters)
+        except Exception as e:  # propagated to every rank
+            exc = e
+    _exception_barrier(comm, exc)
+    if split is None:
+        lo, hi, mine = 0, (gshape[0] if nd else 1), comm.rank == 0
+        block = local
+        ax = 0
+    else:
+        counts, displs = data.counts_displs()
+        ax = split
+        lo, hi, mine = displs[comm.rank], displs[comm.rank] + counts[comm.rank], counts[comm.rank] > 0
+        block = local
+        # rows of my chunks that live on later ranks: every rank shares its leading rows (less than
+        # one chunk along the split axis), the owners take what they need
+        lead = np.take(local, np.arange(min(chunks[ax], local.shape[ax])), axis=ax)
+        leads = comm.allgather((displs[comm.rank], lead))
+        need_hi = min(gshape[ax], -(-hi // chunks[ax]) * chunks[ax]) if hi > lo else hi
+        extra = [blk for (d0, blk) in leads if hi <= d0 < need_hi and blk.shape[ax]]
+        if extra and mine:
+            block = np.concatenate([local] + extra, axis=ax)
+            block = np.take(block, np.arange(min(block.shape[ax], need_hi - lo)), axis=ax)
+    recs, blobs = [], []
+    if mine and nd:
+        c_ax = chunks[ax]
+        first = -(-lo // c_ax) * c_ax
+        grids = [range(0, gshape[d], chunks[d]) if d != ax else range(first, hi, c_ax) for d in range(nd)]
+        for offs in __import__("itertools").product(*grids):
+            sl = tuple(slice(o - (lo if d == ax else 0), o - (lo if d == ax else 0) + chunks[d])
+                       for d, o in enumerate(offs))
+            src = block[sl]
+            full = np.zeros(chunks, np_dtype)
+            full[tuple(slice(0, n) for n in src.shape)] = src
+            enc = _h5lite.encode_chunk(full, filters)
+            recs.append((offs, len(enc)))
+            blobs.append(enc)
+    elif mine:  # 0-d
+        enc = _h5lite.encode_chunk(np.asarray(local).reshape(()), filters)
+        recs.append(((), len(enc)))
+        blobs.append(enc)
+    sizes = comm.allgather(sum(len(b) for b in blobs))
+    base = comm.bcast(os.path.getsize(path) if comm.rank == 0 else None, root=0)
+    base += (-base) % 8
+    start = base + sum(sizes[: comm.rank])
+    if blobs:
+        _h5lite.append_chunks(path, start, blobs)
+    pos, mine_recs = start, []
+    for (offs, n) in recs:
+        mine_recs.append((offs, pos, n, 0))
+        pos += n
+    all_recs = comm.gather(mine_recs, root=0)
+    comm.Barrier()
+    if comm.rank == 0:
+        try:
+            _h5lite.finish_chunked(path, dataset, [r for rs in all_recs for r in rs], base + sum(sizes))
+        except Exception as e:
+            exc = e
+    _exception_barrier(comm, exc)
 
 
 def _write_slab(path: str, dataset: str, sl, local: np.ndarray) -> None:

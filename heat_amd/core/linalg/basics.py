@@ -89,7 +89,7 @@ def _reduce_scatter(partial: torch.Tensor, comm, axis: int) -> torch.Tensor:
     wire_in, wire_out = inp, out
     if inp.dtype == torch.bool:
         wire_in, wire_out = inp.to(torch.uint8), out.to(torch.uint8)
-    _SD.reduce_scatter_tensor(wire_out, wire_in, op=dist.ReduceOp.SUM, group=comm.group)
+    comm.reduce_scatter_tensor(wire_out, wire_in)  # native stream-ordered RCCL under HEAT_COMM_NATIVE=1
     res = wire_out[: counts[comm.rank]]
     return res.movedim(0, axis).contiguous()
 

@@ -120,6 +120,14 @@ HA_EXPORT int ha_comm_allgather(void* comm, const void* send, void* recv, int64_
   return r == 0 ? HA_OK : 100 + r;
 }
 
+// recv (recvcount elements) = this rank's block of the reduction of send (nranks x recvcount)
+HA_EXPORT int ha_comm_reducescatter(void* comm, const void* send, void* recv, int64_t recvcount, int dtype, int op,
+                                    void* stream) {
+  if (!g_rccl.handle || !comm || recvcount < 0) return HA_BAD_ARG;
+  const rcclResult r = g_rccl.ReduceScatter(send, recv, (size_t)recvcount, dtype, op, comm, (hipStream_t)stream);
+  return r == 0 ? HA_OK : 100 + r;
+}
+
 HA_EXPORT int ha_comm_broadcast(void* comm, void* buf, int64_t count, int dtype, int root, void* stream) {
   if (!g_rccl.handle || !comm || count < 0) return HA_BAD_ARG;
   const rcclResult r = g_rccl.Broadcast(buf, buf, (size_t)count, dtype, root, comm, (hipStream_t)stream);

@@ -5,8 +5,9 @@ Native stream-ordered RCCL communicator (``ops/csrc/comm.hip``).
 unique id travels over the existing process group) on the RCCL instance torch already loaded.
 Collectives run on the CALLER's current stream - ordered with the surrounding kernels, no
 ProcessGroupNCCL side-stream events, capturable in a HIP graph - and return immediately.
-``HEAT_COMM_NATIVE=1`` routes device SUM/MAX/MIN/PROD all-reduces, all-gathers and the byte
-exchanges of ``exchange_axis`` through it; the default stays torch's ProcessGroupNCCL. An
+``HEAT_COMM_NATIVE=1`` routes device SUM/MAX/MIN/PROD all-reduces, all-gathers (also of unequal
+blocks: a grouped send/receive, no padding), reduce-scatters and the byte exchanges of
+``exchange_axis`` through it; the default stays torch's ProcessGroupNCCL. An
 asynchronous RCCL error (peer failure) is polled with :meth:`check` (the heat watchdog calls it on
 every synchronising wait).
 """
@@ -93,6 +94,37 @@ class NativeComm:
         out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         check(self.L.ha_comm_allgather(self.handle, ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                        t.numel(), _DT[t.dtype], self._stream(t)), "ha_comm_allgather")
+        return out
+
+    def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """``out`` = this rank's block of the element-wise reduction of ``inp`` (size x out.numel()
+        elements, contiguous) on the current stream."""
+        from ..ops import check
+
+        assert inp.is_contiguous() and out.is_contiguous() and self.supports(inp, op)
+        assert inp.numel() == out.numel() * self.size and inp.dtype == out.dtype
+        check(self.L.ha_comm_reducescatter(self.handle, ctypes.c_void_p(inp.data_ptr()),
+                                           ctypes.c_void_p(out.data_ptr()), out.numel(), _DT[inp.dtype], _OPS[op],
+                                           self._stream(inp)), "ha_comm_reducescatter")
+        return out
+
+    def allgatherv(self, moved: torch.Tensor, counts: Sequence[int]) -> torch.Tensor:
+        """Concatenation along dim 0 of every rank's contiguous block (rank q holds counts[q]
+        rows): one RCCL group of sends of the local block to every peer and receives of theirs,
+        on the current stream (no padding to the largest block)."""
+        from ..ops import check
+
+        row = int(np.prod(moved.shape[1:])) * moved.element_size()
+        out = torch.empty((sum(counts),) + tuple(moved.shape[1:]), dtype=moved.dtype, device=moved.device)
+        own = counts[self.rank] * row
+        sb = np.full(self.size, own, dtype=np.int64)
+        so = np.zeros(self.size, dtype=np.int64)
+        rb = np.asarray([c * row for c in counts], dtype=np.int64)
+        ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.int64)
+        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        check(self.L.ha_comm_alltoallv(self.handle, self.size, self.rank, ctypes.c_void_p(moved.data_ptr()), p(sb),
+                                       p(so), ctypes.c_void_p(out.data_ptr()), p(rb), p(ro), self._stream(moved)),
+              "ha_comm_alltoallv")
         return out
 
     def broadcast_(self, t: torch.Tensor, root: int) -> torch.Tensor:

@@ -8,6 +8,7 @@ isend/irecv to the ring neighbours), so communication overlaps the compute of ``
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List
 
 import torch
@@ -16,16 +17,28 @@ import torch.distributed as dist
 from . import staging as _SD
 
 
-def ring_pass(block: torch.Tensor, fn: Callable[[torch.Tensor, int], None], comm, sizes: List[int] = None):
+def ring_mode() -> str:
+    """``HEAT_RING_MODE``: "ring" (default: two blocks in memory, one neighbour link per step) or
+    "direct" (every rank posts its block to all p - 1 peers at once - on a fully connected xGMI node
+    all 7 links of a GPU carry data concurrently - and the blocks are consumed in ring order as they
+    arrive; p blocks in memory)."""
+    return os.environ.get("HEAT_RING_MODE", "ring")
+
+
+def ring_pass(block: torch.Tensor, fn: Callable[[torch.Tensor, int], None], comm, sizes: List[int] = None,
+              mode: str = None):
     """Visit every rank's ``block`` in ring order (own first), overlapping transfer and compute.
 
-    ``sizes`` (optional) gives every rank's leading dimension when blocks are uneven."""
+    ``sizes`` (optional) gives every rank's leading dimension when blocks are uneven; ``mode``
+    overrides :func:`ring_mode`."""
     p, me = comm.size, comm.rank
     if p == 1:
         fn(block, me)
         return
     if sizes is None:
         sizes = comm.allgather_sizes(block.shape[0])
+    if (mode or ring_mode()) == "direct":
+        return _direct_pass(block, fn, comm, sizes)
     rest = tuple(block.shape[1:])
     cur = block.contiguous()
     src = me
@@ -45,3 +58,26 @@ def ring_pass(block: torch.Tensor, fn: Callable[[torch.Tensor, int], None], comm
         if recv is not None:
             cur = recv
             src = (src - 1) % p
+
+
+def _direct_pass(block: torch.Tensor, fn, comm, sizes: List[int]):
+    """All-peers variant of :func:`ring_pass`: one batched group of p - 1 sends of the local block
+    and p - 1 receives (pairwise order: step k sends to rank + k and receives from rank - k, so
+    every link is busy in both directions), then ``fn`` on the own block while the transfers run,
+    then on every received block in ring order."""
+    p, me = comm.size, comm.rank
+    rest = tuple(block.shape[1:])
+    cur = block.contiguous()
+    recvs, ops = {}, []
+    for k in range(1, p):
+        to, frm = (me + k) % p, (me - k) % p
+        recvs[frm] = torch.empty((sizes[frm],) + rest, dtype=cur.dtype, device=cur.device)
+        ops.append(dist.P2POp(dist.isend, cur, comm._g(to), comm.group))
+        ops.append(dist.P2POp(dist.irecv, recvs[frm], comm._g(frm), comm.group))
+    works = _SD.batch_isend_irecv(ops)
+    fn(cur, me)
+    for w in works:
+        w.wait()
+    for k in range(1, p):
+        src = (me - k) % p
+        fn(recvs.pop(src), src)

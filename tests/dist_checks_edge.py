@@ -408,6 +408,42 @@ def check_matmul_ring_streamed():
         basics._RING_MIN_BYTES = old
 
 
+def check_matmul_ring_direct():
+    """The all-peers ring mode (``HEAT_RING_MODE=direct``: every block posted to all p - 1 peers
+    at once) gives the same panel-streamed matmul and streamed cdist as the neighbour ring."""
+    import os
+
+    from heat_amd.core.linalg import basics
+
+    old, old_env = basics._RING_MIN_BYTES, os.environ.get("HEAT_RING_MODE")
+    basics._RING_MIN_BYTES = 0
+    os.environ["HEAT_RING_MODE"] = "direct"
+    try:
+        rng = np.random.default_rng(62)
+        for (m, k, n) in ((9, 7, 5), (17, 1, 6), (3, 4, 2)):
+            a = rng.standard_normal((m, k))
+            b = rng.standard_normal((k, n))
+            for sa in (0, 1):
+                for sb in (0, 1):
+                    C = ht.array(a, split=sa) @ ht.array(b, split=sb)
+                    assert np.allclose(C.numpy(), a @ b, rtol=1e-10, atol=1e-12), (m, k, n, sa, sb)
+        x = rng.standard_normal((23, 3)).astype(np.float32)
+        X = ht.array(x, split=0)
+        seen = []
+        ht.spatial.cdist_stream(X, X, lambda d, i, j: seen.append((i, j, d.shape)), tile=5)
+        rows = sum(s[0] for (i, j, s) in seen if j == 0)
+        assert rows == X.lshape[0]
+        d = ht.spatial.cdist(X, X)
+        ref = np.sqrt(((x[:, None, :] - x[None, :, :]) ** 2).sum(-1))
+        assert np.allclose(d.numpy(), ref, atol=1e-4)
+    finally:
+        basics._RING_MIN_BYTES = old
+        if old_env is None:
+            os.environ.pop("HEAT_RING_MODE", None)
+        else:
+            os.environ["HEAT_RING_MODE"] = old_env
+
+
 def check_qr_split1_panels():
     """Column-split QR keeps the column split (Householder panel factorisation by the owner,
     reflector broadcasts): orthogonal Q, A = QR, upper-triangular R, also for cond(A) = 1e10 and

@@ -191,3 +191,34 @@ def bench_ipc():
             print(json.dumps(res), flush=True)
     ar.check()
     ar.close()
+
+
+def check_ipc_halo():
+    """``DNDarray.get_halo`` takes the xGMI peer path under HEAT_IPC_ALLREDUCE=1: every rank's
+    boundary slices in one direct all-gather kernel; neighbours' slices match the data (split 0
+    and split 1, halo 1 and 3), and ``diff`` along the split axis agrees with numpy."""
+    assert os.environ.get("HEAT_IPC_ALLREDUCE") == "1"
+    comm = ht.MPI_WORLD
+    r, p = comm.rank, comm.size
+    a = np.arange(24 * 10, dtype=np.float32).reshape(24, 10)
+    for split in (0, 1):
+        x = ht.array(a, split=split, device="gpu")
+        assert x.larray.is_cuda
+        counts, displs = x.counts_displs()
+        for h in (1, 3):
+            x.get_halo(h)
+            if r > 0:
+                lo = displs[r] - h
+                ref = a[lo: displs[r]] if split == 0 else a[:, lo: displs[r]]
+                assert np.array_equal(x.halo_prev.cpu().numpy(), ref), (split, h)
+            else:
+                assert x.halo_prev is None
+            if r < p - 1:
+                hi = displs[r] + counts[r]
+                ref = a[hi: hi + h] if split == 0 else a[:, hi: hi + h]
+                assert np.array_equal(x.halo_next.cpu().numpy(), ref), (split, h)
+            else:
+                assert x.halo_next is None
+        assert np.allclose(ht.diff(x, axis=split).numpy(), np.diff(a, axis=split))
+    assert getattr(comm, "_ipc", None) is not None, "the IPC path was not taken"
+    assert comm._ipc.error() == 0

@@ -24,3 +24,9 @@ def test_ipc_timeout_is_loud(gpu):
 @pytest.mark.parametrize("nprocs", [2, 3])
 def test_ipc_allgather_two_shot(gpu, nprocs):
     run_distributed("tests.ipc_checks:check_ipc_allgather_and_two_shot", nprocs, timeout=110, keep_gpu=True)
+
+
+@pytest.mark.parametrize("nprocs", [2, 3])
+def test_ipc_halo(gpu, nprocs):
+    run_distributed("tests.ipc_checks:check_ipc_halo", nprocs, timeout=110, keep_gpu=True,
+                    env_extra={"HEAT_IPC_ALLREDUCE": "1"})
