@@ -64,10 +64,29 @@ class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
         k = self.n_neighbors
         if self.effective_metric_ is not None:
             distances = self.effective_metric_(x, self.x)
-            d = distances._gathered() if distances.split == 1 else distances.larray
-            _, idx = torch.topk(d, k, dim=1, largest=False)
-            ylab = self.y._gathered() if self.y.is_distributed() else self.y.larray
-            votes = ylab[idx.reshape(-1).to(ylab.device)].reshape(idx.shape[0], k, -1).sum(1)
+            if distances.split == 1 and distances.is_distributed():
+                # columns = training rows, split like the labels: local top-k of every rank's
+                # column block, ONE all-gather of the p x k candidates (distance + label vector),
+                # top-k of those - the query x train matrix is never gathered
+                d = distances.larray
+                kk = min(k, d.shape[1])
+                ylab = self.y.larray.to(torch.float32)
+                if kk:
+                    vals, idx = torch.topk(d, kk, dim=1, largest=False)
+                    cand_y = ylab[idx.reshape(-1).to(ylab.device)].reshape(d.shape[0], kk, -1)
+                else:
+                    vals = d.new_zeros((d.shape[0], 0))
+                    cand_y = ylab.new_zeros((d.shape[0], 0, ylab.shape[1]))
+                comm = distances.comm
+                all_v = comm.allgather_tensor(vals.to(torch.float64).contiguous(), 1)
+                all_y = comm.allgather_tensor(cand_y.contiguous(), 1)
+                _, sel = torch.topk(all_v, k, dim=1, largest=False)
+                votes = torch.gather(all_y, 1, sel.unsqueeze(-1).expand(-1, -1, all_y.shape[-1])).sum(1)
+            else:
+                d = distances.larray
+                _, idx = torch.topk(d, k, dim=1, largest=False)
+                ylab = self.y._gathered() if self.y.is_distributed() else self.y.larray
+                votes = ylab[idx.reshape(-1).to(ylab.device)].reshape(idx.shape[0], k, -1).sum(1)
             lab = torch.argmax(votes, dim=1)
             return DNDarray(lab, (x.gshape[0],), ht.int64, x.split if x.split == 0 else None, x.device, x.comm,
                             x.balanced)

@@ -69,9 +69,13 @@ class Spectral(ClusteringMixin, BaseEstimator):
         evals, idx = torch.sort(evals)
         evecs = evecs[:, idx].to(T.larray.dtype)
         eigenvalues = ht.array(evals.to(T.larray.dtype), device=L.device, comm=L.comm)
-        Vs = V if V.split is None else ht.resplit(V, None)
-        vec = Vs.larray @ evecs
-        eigenvectors = ht.array(vec, split=0 if x.split == 0 else None, device=L.device, comm=L.comm)
+        # V stays row-split: every rank forms its own rows of V @ evecs (n x m basis never gathered)
+        vec = V.larray @ evecs.to(V.larray.dtype)
+        if V.split == 0:
+            eigenvectors = ht.DNDarray(vec, (n, vec.shape[1]), ht.types.canonical_heat_type(vec.dtype), 0, L.device,
+                                       L.comm, V.balanced)
+        else:
+            eigenvectors = ht.array(vec, split=0 if x.split == 0 else None, device=L.device, comm=L.comm)
         return eigenvalues, eigenvectors
 
     def fit(self, x: DNDarray) -> "Spectral":

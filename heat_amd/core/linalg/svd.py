@@ -1,8 +1,8 @@
 """Singular value decomposition (the reference ships an empty placeholder, ``linalg/svd.py``).
 
-``svd`` here is a convenience: tall-skinny split-0 matrices use TSQR + a small local SVD of R (U
-stays split 0), wide split-1 matrices the same on the transpose (V split 0); other layouts gather
-the matrix and run one local SVD."""
+``svd`` here is a convenience: tall distributed matrices use TSQR + a small local SVD of R (U
+stays split 0; a column-split input is redistributed to rows first), wide ones the same on the
+transpose (V split 0). The matrix is never gathered; only the n x n factor R is replicated."""
 from __future__ import annotations
 
 import torch
@@ -22,9 +22,9 @@ def svd(a: DNDarray, full_matrices: bool = False, compute_uv: bool = True):
         raise ValueError("svd requires a 2-D DNDarray")
     if full_matrices:
         raise NotImplementedError("full_matrices=True is not supported")
-    if a.is_distributed() and a.split == 1 and a.gshape[1] > a.gshape[0]:
-        # wide, split along the long axis: A^T is tall-skinny split 0 (a local transpose), and
-        # A^T = U' S V'^T gives A = V' S U'^T - no gather of A
+    if a.is_distributed() and a.gshape[1] > a.gshape[0]:
+        # wide: A^T is tall (a local transpose; split 0 <-> 1), and A^T = U' S V'^T gives
+        # A = V' S U'^T - no gather of A
         from .basics import transpose
 
         res = svd(transpose(a), full_matrices=False, compute_uv=compute_uv)
@@ -32,8 +32,14 @@ def svd(a: DNDarray, full_matrices: bool = False, compute_uv: bool = True):
             return res
         u2, s2, v2 = res
         return v2, s2, u2
-    if a.is_distributed() and a.split == 0 and a.gshape[0] >= a.gshape[1]:
-        q, r = qr(a)
+    if a.is_distributed():
+        # tall: rows split (one redistribution when the columns were split), TSQR, a small local SVD
+        # of R, U = Q U_r
+        if a.split != 0:
+            from ..manipulations import resplit
+
+            a = resplit(a, 0)
+        q, r = qr(a, mode="reduced")
         rt = r._gathered() if r.is_distributed() else r.larray
         ur, s, vh = torch.linalg.svd(rt, full_matrices=False)
         S = DNDarray(s, tuple(s.shape), types.canonical_heat_type(s.dtype), None, a.device, a.comm, True)

@@ -768,10 +768,27 @@ def diag(a: DNDarray, offset: int = 0) -> DNDarray:
     if not a.is_distributed():
         res = torch.diag(a.larray, offset)
         return DNDarray(res, (n, n), a.dtype, a.split, a.device, a.comm, True)
-    full = a._gathered()
-    res = torch.diag(full, offset)
-    _, _, sl = a.comm.chunk((n, n), a.split)
-    return DNDarray(res[sl].contiguous(), (n, n), a.dtype, 0, a.device, a.comm, True)
+    # rank r builds its row block [R0, R1) of the n x n result; its diagonal entries are the
+    # contiguous range v[R0 - max(-offset, 0) ...] of the vector: ONE redistribution of the vector
+    # (O(local) memory), no gather
+    comm = a.comm
+    m = a.gshape[0]
+    counts = [comm.chunk((n, n), 0, rank=r)[1][0] for r in range(comm.size)]
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    sh = -offset if offset < 0 else 0   # row j holds v[j - sh]
+    need = [max(0, min(m, s0 + c - sh) - max(0, s0 - sh)) for s0, c in zip(starts, counts)]
+    v = a.copy()
+    target = torch.tensor(need, dtype=torch.int64).reshape(-1, 1)
+    v.redistribute_(lshape_map=v.create_lshape_map(), target_map=target)
+    R0, R1 = int(starts[comm.rank]), int(starts[comm.rank] + counts[comm.rank])
+    res = torch.zeros((R1 - R0, n), dtype=a.larray.dtype, device=a.larray.device)
+    vl = v.larray
+    if vl.numel():
+        j0 = max(R0, sh)                                    # first row with an entry
+        rows = torch.arange(j0 - R0, j0 - R0 + vl.shape[0], device=res.device)
+        cols = torch.arange(j0 + offset, j0 + offset + vl.shape[0], device=res.device)
+        res[rows, cols] = vl
+    return DNDarray(res, (n, n), a.dtype, 0, a.device, comm, True)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -900,13 +917,29 @@ def unique(a: DNDarray, sorted: bool = False, return_inverse: bool = False, axis
             return res, inv_arr
         return res
     axis = sanitize_axis(a.gshape, axis)
-    full = a._gathered() if a.is_distributed() else a.larray
-    uniq, inv = torch.unique(full, sorted=True, return_inverse=True, dim=axis)
+    if not a.is_distributed():
+        uniq, inv = torch.unique(a.larray, sorted=True, return_inverse=True, dim=axis)
+        res = DNDarray(uniq, tuple(uniq.shape), a.dtype, None, a.device, a.comm, True)
+        if return_inverse:
+            return res, DNDarray(inv, tuple(inv.shape), types.int64, None, a.device, a.comm, True)
+        return res
+    # slices along `axis` must be whole on one rank: split the array along `axis` (one
+    # redistribution when it is split elsewhere), unique the local slices, ONE all-gather of the
+    # local uniques (not of the array), and unique again; the inverse of the local slices comes
+    # from their position among the global uniques
+    src = a if a.split == axis else resplit(a, axis)
+    local_u = torch.unique(src.larray, sorted=True, dim=axis)
+    allu = a.comm.allgather_tensor(local_u, axis)
+    uniq = torch.unique(allu, sorted=True, dim=axis)
     res = DNDarray(uniq, tuple(uniq.shape), a.dtype, None, a.device, a.comm, True)
-    if a.split is not None and a.split != axis and a.is_distributed():
+    if a.split is not None and a.split != axis:
         res = resplit(res, a.split)
     if return_inverse:
-        inv_arr = DNDarray(inv, tuple(inv.shape), types.int64, None, a.device, a.comm, True)
+        nu = uniq.shape[axis]
+        _, inv_all = torch.unique(torch.cat([uniq, src.larray], dim=axis), sorted=True, return_inverse=True,
+                                  dim=axis)
+        inv = inv_all[nu:]
+        inv_arr = DNDarray(inv, (a.gshape[axis],), types.int64, 0, a.device, a.comm, src.balanced)
         return res, inv_arr
     return res
 

@@ -490,3 +490,45 @@ def check_svd_layouts():
     except ValueError:
         raises_ok = True
     assert raises_ok
+
+
+def check_diag_unique_without_gather():
+    """``diag`` of a split vector (one redistribution of the vector into the result's row blocks)
+    and ``unique(axis=...)`` (local uniques + one all-gather of them, inverse from the global
+    uniques) on every split, against numpy."""
+    rng = np.random.default_rng(4)
+    for m in (1, 5, 11):
+        v = rng.standard_normal(m)
+        for off in (-3, -1, 0, 2, 4):
+            for s in (None, 0):
+                d = ht.diag(ht.array(v, split=s), off)
+                assert np.allclose(d.numpy(), np.diag(v, off)), (m, off, s)
+                if s == 0:
+                    assert d.split == 0
+    a = rng.integers(0, 3, (23, 4)).astype(np.float32)
+    for s in (None, 0, 1):
+        for ax in (0, 1):
+            x = ht.array(a, split=s)
+            u, inv = ht.unique(x, return_inverse=True, axis=ax)
+            ru, rinv = np.unique(a, axis=ax, return_inverse=True)
+            assert np.allclose(u.numpy(), ru), (s, ax)
+            assert np.array_equal(inv.numpy().reshape(-1), rinv.reshape(-1)), (s, ax)
+
+
+def check_knn_custom_metric_candidates():
+    """kNN with a user metric whose distance matrix is column-split (replicated queries vs split
+    training rows): per-rank top-k candidates + one all-gather, no gather of the matrix; labels
+    equal a numpy brute force."""
+    rng = np.random.default_rng(8)
+    xt = rng.standard_normal((41, 3)).astype(np.float32)
+    yt = rng.integers(0, 3, 41)
+    onehot = np.eye(3, dtype=np.float32)[yt]
+    q = rng.standard_normal((9, 3)).astype(np.float32)
+    knn = ht.classification.KNeighborsClassifier(n_neighbors=4,
+                                                 effective_metric_=lambda a, b: ht.spatial.cdist(a, b))
+    knn.fit(ht.array(xt, split=0), ht.array(onehot, split=0))
+    pred = knn.predict(ht.array(q)).numpy()
+    d = np.sqrt(((q[:, None, :] - xt[None]) ** 2).sum(-1))
+    nn = np.argsort(d, axis=1, kind="stable")[:, :4]
+    ref = np.argmax(onehot[nn].sum(1), axis=1)
+    assert np.array_equal(pred, ref), (pred, ref)
