@@ -89,14 +89,9 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
     if a.split == 1 and m >= n and (mode == "reduced" or m == n):
         return _qr_split1(a, dtype, calc_q)
 
-    if mode == "complete" and (m < n * a.comm.size or m <= n):
-        # small or wide matrices: the factors are not smaller than the input; factor replicated
-        full = a._gathered().to(tt)
-        q, r = torch.linalg.qr(full, mode="complete")
-        split = a.split
-        R = factories.array(r, split=split, device=a.device, comm=a.comm, dtype=dtype)
-        Q = factories.array(q, split=0 if split == 0 else 1, device=a.device, comm=a.comm, dtype=dtype) if calc_q else None
-        return QR(Q, R)
+    if mode == "complete":
+        # complete Q (m x m): distributed Householder, Q's rows formed locally - no gather
+        return _qr_complete(a, dtype, calc_q)
 
     src = a if a.split == 0 else _resplit(a, 0)
     if not src.is_balanced():
@@ -110,17 +105,6 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
     if not calc_q:
         return QR(None, R)
     Q = DNDarray(Ql, (m, k), dtype, 0, a.device, a.comm, True)
-    if mode == "complete":
-        # complete Q = [Q_reduced | orthonormal complement]: complement from the gathered Q
-        full = Q._gathered()
-        qc, _ = torch.linalg.qr(torch.cat([full, torch.eye(m, m - k, dtype=tt, device=full.device)], dim=1),
-                                mode="reduced")
-        # keep the reduced part exactly as computed, take the complement from the re-orthogonalisation
-        compl = qc[:, k:]
-        compl = compl - full @ (full.T @ compl)
-        compl, _ = torch.linalg.qr(compl, mode="reduced")
-        qfull = torch.cat([full, compl], dim=1)
-        Q = factories.array(qfull, split=0, device=a.device, comm=a.comm, dtype=dtype)
     if a.split == 1:
         Q = _resplit(Q, 1)
     return QR(Q, R)
@@ -218,6 +202,69 @@ def _qr_split1(a: DNDarray, dtype, calc_q: bool):
     if nloc:
         Q *= signs[me].unsqueeze(0)
     return QR(DNDarray(Q, (m, n), dtype, 1, a.device, comm, a.balanced), Rd)
+
+
+def _qr_complete(a: DNDarray, dtype, calc_q: bool) -> QR:
+    """Complete QR (Q m x m) of a distributed matrix without gathering it.
+
+    m >= n: the rows are distributed (a column-split input is redistributed once), blocked
+    Householder with one fp64 all-reduce per column / two per panel (``ops.householder_factor``),
+    R (n x n) assembled by one all-reduce, and every rank forms ITS rows of the complete Q by
+    applying the reflectors to its rows of the identity (``ops.householder_apply``: per panel one
+    nb x m all-reduce). m < n: QR of the leading m x m block, then R = Q^T A as one distributed
+    matmul. Q comes back split 0 (split 1 for a column-split input), R split like the input."""
+    from ... import ops
+    from ..communication import MPI
+    from .basics import matmul, transpose, triu
+
+    m, n = a.gshape
+    comm = a.comm
+    if m < n:
+        lead = _resplit(a[:, :m], 0)
+        q, _ = _qr_complete(lead, dtype, True)
+        r = triu(matmul(transpose(q), a.astype(dtype)))
+        r = r if r.split == a.split else _resplit(r, a.split)
+        if calc_q and a.split == 1:
+            q = _resplit(q, 1)
+        return QR(q if calc_q else None, r)
+    src = a if a.split == 0 else _resplit(a, 0)
+    if not src.is_balanced():
+        src = src.copy()
+        src.balance_()
+    tt = dtype.torch_type()
+    local = src.larray.to(tt)
+    counts = comm.allgather_sizes(local.shape[0])
+    g0 = sum(counts[: comm.rank])
+
+    def red(t):
+        comm.Allreduce(MPI.IN_PLACE, t, MPI.SUM)
+        return t
+
+    A, panels = ops.householder_factor(local, g0, m, red)
+    kmax = min(m, n)
+    m_r = local.shape[0]
+    R = torch.zeros((kmax, n), dtype=tt, device=local.device)
+    lo, hi = max(g0, 0), min(g0 + m_r, kmax)
+    if hi > lo:
+        R[lo:hi] = torch.triu(A[lo - g0: hi - g0], diagonal=lo)
+    red(R)
+    d = torch.sign(torch.diagonal(R))
+    d = torch.where(d == 0, torch.ones_like(d), d)
+    R = d.unsqueeze(1) * R
+    if m > kmax:
+        R = torch.cat([R, R.new_zeros((m - kmax, n))], 0)
+    Rd = factories.array(R, split=a.split, device=a.device, comm=comm, dtype=dtype)
+    if not calc_q:
+        return QR(None, Rd)
+    Q = torch.zeros((m_r, m), dtype=tt, device=local.device)
+    if m_r:
+        Q[torch.arange(m_r, device=Q.device), torch.arange(g0, g0 + m_r, device=Q.device)] = 1
+    ops.householder_apply(A, panels, Q, g0, transpose=False, allreduce=red)
+    Q[:, :kmax] *= d.unsqueeze(0)
+    Qd = DNDarray(Q, (m, m), dtype, 0, a.device, comm, True)
+    if a.split == 1:
+        Qd = _resplit(Qd, 1)
+    return QR(Qd, Rd)
 
 
 def _resplit(x: DNDarray, axis):

@@ -532,3 +532,22 @@ def check_knn_custom_metric_candidates():
     nn = np.argsort(d, axis=1, kind="stable")[:, :4]
     ref = np.argmax(onehot[nn].sum(1), axis=1)
     assert np.array_equal(pred, ref), (pred, ref)
+
+
+def check_qr_complete_without_gather():
+    """Complete-mode QR (Q m x m) of tall, square and wide matrices on every split: orthogonal
+    Q, Q R = A, R upper trapezoidal with a non-negative diagonal, Q split 0 (1 for split-1
+    input) - formed by the distributed Householder path, no gather of A or Q."""
+    rng = np.random.default_rng(17)
+    for (m, n) in ((13, 4), (9, 9), (5, 11), (3, 3), (20, 1)):
+        a = rng.standard_normal((m, n))
+        for s in (0, 1):
+            q, r = ht.linalg.qr(ht.array(a, split=s), mode="complete")
+            Q, R = q.numpy(), r.numpy()
+            assert Q.shape == (m, m) and R.shape == (m, n), (m, n, s)
+            assert np.allclose(Q.T @ Q, np.eye(m), atol=1e-5), (m, n, s)
+            assert np.allclose(Q @ R, a, atol=1e-5), (m, n, s)
+            assert np.allclose(np.tril(R, -1), 0, atol=1e-6)
+            k = min(m, n)
+            assert (np.diagonal(R)[:k] >= -1e-7).all()
+            assert q.split == (0 if s == 0 else 1) and r.split == s
