@@ -5,9 +5,12 @@ full ring pipelines 265-486).
 
 Split rules are the reference's: X split 0 -> result split 0; X replicated and Y split 0 ->
 result split 1; both replicated -> replicated. The local tiles are produced by the native CDNA4
-kernels (``ops.cdist``: fp32-MFMA L2 family with fused epilogue, VALU L1). When both operands are
-split, Y's blocks are either all-gathered once (fits in memory) or streamed around a
-double-buffered ring that overlaps each transfer with the previous tile's kernel.
+kernels (``ops.cdist``): the L2 family by the quadratic expansion on the FP16 matrix cores as a
+3-term fp16 split with fp32 accumulation (``cdist_f16x3.hip``, fp32-GEMM accuracy; the exact
+difference kernel for ``quadratic_expansion=False``) with a fused clamp / sqrt / exp epilogue, L1
+on the VALU. When both operands are split, Y's blocks are either all-gathered once (fits in
+memory) or streamed around a double-buffered ring (``HEAT_RING_MODE=direct``: posted to all peers
+at once) that overlaps each transfer with the previous tile's kernel.
 """
 from __future__ import annotations
 

@@ -7,7 +7,7 @@ the native kernels, with the same NumPy oracles as ``test_distributed.py``."""
 import pytest
 import torch
 
-from . import dist_checks, dist_checks_edge
+from . import dist_checks, dist_checks_edge, vcoll_checks
 from ._dist import run_distributed, run_distributed_batch
 
 pytestmark = pytest.mark.gpu
@@ -19,11 +19,15 @@ ENV = {"HEAT_AMD_DEFAULT_DEVICE": "gpu", "HEAT_COMM_TIMEOUT": "60"}
 _BATCH = {}
 
 
-def _batch(module):
-    if module not in _BATCH:
-        names = [n for m, n in CASES if m == module]
-        _BATCH[module] = run_distributed_batch(module, names, 2, timeout=300, env_extra=ENV, keep_gpu=True)
-    return _BATCH[module]
+VCOLL = [n for n in dir(vcoll_checks) if n.startswith("check_")]
+
+
+def _batch(module, nprocs=2, names=None):
+    key = (module, nprocs)
+    if key not in _BATCH:
+        names = names or [n for m, n in CASES if m == module]
+        _BATCH[key] = run_distributed_batch(module, names, nprocs, timeout=300, env_extra=ENV, keep_gpu=True)
+    return _BATCH[key]
 
 
 @pytest.mark.parametrize("module,name", CASES)
@@ -33,3 +37,15 @@ def test_distributed_on_device(module, name):
     ok, err = _batch(module)[name]
     if not ok:
         pytest.fail("check {} failed with device buffers:\n{}".format(name, err))
+
+
+@pytest.mark.parametrize("nprocs", [3, 5])
+@pytest.mark.parametrize("name", VCOLL)
+def test_vcollectives_uneven_on_device(name, nprocs):
+    """Allgatherv / Alltoallv / Gatherv / Scatterv / reduce-scatter with uneven and EMPTY blocks,
+    device buffers, 3 and 5 ranks on the one card (``tests/vcoll_checks.py``)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ok, err = _batch("tests.vcoll_checks", nprocs, VCOLL)[name]
+    if not ok:
+        pytest.fail("check {} failed with device buffers at {} ranks:\n{}".format(name, nprocs, err))

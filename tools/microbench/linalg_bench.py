@@ -1,0 +1,57 @@
+"""ht.matmul / ht.linalg.qr on the linalg north-star slice (1.25e6 x 4096 per GPU, fp32) through
+the public API, at float32 matmul precision "highest" (exact f32 MFMA kernels) and "high" (fused
+fp16x3 kernels); orthogonality / reconstruction errors on a row sample. JSON lines."""
+import json
+import sys
+import time
+
+import torch
+
+import heat_amd as ht
+
+
+def timed(fn, reps=2):
+    fn()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return best, r
+
+
+def main():
+    m = int(sys.argv[1]) if len(sys.argv) > 1 else 1_250_000
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    ht.use_device("gpu")
+    ht.random.seed(1)
+    a = ht.random.randn(m, n, split=0)
+    b = ht.random.randn(n, n, split=None)
+    rows = torch.randint(0, m, (256,), device="cuda")
+    for prec in ("highest", "high"):
+        torch.set_float32_matmul_precision(prec)
+        t, c = timed(lambda: ht.matmul(a, b))
+        ref = a.larray[rows].double() @ b.larray.double()
+        err = float(((c.larray[rows].double() - ref).abs() / (a.larray[rows].abs().double() @ b.larray.abs().double())).max())
+        print(json.dumps({"op": "matmul", "precision": prec, "shape": [m, n, n], "s": t,
+                          "tflops": 2.0 * m * n * n / t / 1e12, "rel_err_bound_units": err / 2 ** -24 / n}), flush=True)
+        del c
+        t, (q, r) = timed(lambda: ht.linalg.qr(a, mode="reduced"), reps=1)
+        Q, R = q.larray, r.larray.double()
+        sub = Q[rows].double()
+        rec = float((sub @ R - a.larray[rows].double()).abs().max() / a.larray[rows].abs().max())
+        G = torch.zeros(n, n, dtype=torch.float64, device="cuda")
+        for r0 in range(0, m, 1 << 17):
+            blk = Q[r0: r0 + (1 << 17)].double()
+            G += blk.T @ blk
+        orth = float((G - torch.eye(n, dtype=torch.float64, device="cuda")).abs().max())
+        print(json.dumps({"op": "qr", "precision": prec, "shape": [m, n], "s": t, "orth": orth, "rec": rec}),
+              flush=True)
+        del q, r, Q
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
