@@ -140,12 +140,12 @@ def _qr_split1(a: DNDarray, dtype, calc_q: bool):
         shape, blocks = panel_shapes(j)
         if j == me:
             V, panels = fact
-            T = torch.zeros((len(blocks), nb, nb), dtype=tt, device=dev)
+            T = torch.zeros((len(blocks), nb, nb), dtype=torch.float64, device=dev)
             for i, (_, nc, Tm) in enumerate(panels):
                 T[i, :nc, :nc] = Tm
         else:
             V = torch.empty(shape, dtype=tt, device=dev)
-            T = torch.empty((len(blocks), nb, nb), dtype=tt, device=dev)
+            T = torch.empty((len(blocks), nb, nb), dtype=torch.float64, device=dev)
         comm.Bcast(V, root=j)
         comm.Bcast(T, root=j)
         return V, [(k0, nc, T[i, :nc, :nc]) for i, (k0, nc) in enumerate(blocks)]
@@ -293,8 +293,9 @@ def _cholqr(local: torch.Tensor, comm, calc_q: bool, distributed: bool):
 
 def _cholqr_native(A: torch.Tensor, comm, calc_q: bool, distributed: bool):
     """CholeskyQR2 of a device fp32 block entirely on the hand-written kernels: the Gram matrices
-    and both Q products on the 256-tile MFMA GEMMs (``ops/csrc/gemm_tiled.hip``, exact f32 or fused
-    fp16x3 by the float32 matmul precision), the fp64 Cholesky and triangular inverse on
+    (``ops.gram64``: upper-triangle tiles, split-K slices summed in fp64 - an fp64 Gram from fp32
+    MFMA work) and both Q products on the 256-tile MFMA GEMMs (``ops/csrc/gemm_tiled.hip``, exact
+    f32 or fused fp16x3 by the float32 matmul precision), the fp64 Cholesky and triangular inverse on
     ``ops/csrc/linalg64.hip`` (no rocSOLVER / rocBLAS). One n x n all-reduce per pass; one host
     sync per pass for the breakdown / conditioning decision."""
     from ... import ops
@@ -319,11 +320,11 @@ def _cholqr_native(A: torch.Tensor, comm, calc_q: bool, distributed: bool):
             ok = comm.allreduce(int(ok)) == comm.size
         return (R, Rinv) if ok else (None, None)
 
-    R1, Ri1 = factor(allreduce(fgemm(A.T, A)), True)
+    R1, Ri1 = factor(allreduce(ops.gram64(A)), True)
     if R1 is None:
         return None
     Q1 = fgemm(A, Ri1.to(dt))
-    R2, Ri2 = factor(allreduce(fgemm(Q1.T, Q1)), False)
+    R2, Ri2 = factor(allreduce(ops.gram64(Q1)), False)
     if R2 is None:
         return None
     R = ops.gemm64(R2, R1).to(dt)

@@ -46,6 +46,22 @@ __device__ __forceinline__ int64_t tg_xcd_remap(int64_t orig, int64_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// (m0, n0) of workgroup blockIdx.x: all nbm x nbn tiles, or (upper, square grids) only the tiles
+// with tile column >= tile row, enumerated row by row - then the XCD remap spreads the upper
+// triangle's uneven rows evenly over the XCDs.
+__device__ __forceinline__ void tg_tile(int64_t nbm, int64_t nbn, int upper, int64_t& m0, int64_t& n0) {
+  if (!upper) {
+    const int64_t bid = tg_xcd_remap(blockIdx.x, nbm * nbn);
+    m0 = (bid / nbn) * 256;
+    n0 = (bid % nbn) * 256;
+    return;
+  }
+  int64_t bid = tg_xcd_remap(blockIdx.x, nbn * (nbn + 1) / 2), i = 0;
+  while (bid >= nbn - i) { bid -= nbn - i; ++i; }
+  m0 = i * 256;
+  n0 = (i + bid) * 256;
+}
+
 __device__ __forceinline__ void tg_dma16(const void* src, unsigned char* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
@@ -121,19 +137,22 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
                                                    const _Float16* __restrict__ Bhi, const _Float16* __restrict__ Blo,
                                                    const int* __restrict__ eA, const int* __restrict__ eB,
                                                    float* __restrict__ C, int64_t M, int64_t N, int64_t Kp,
-                                                   int64_t Mp, int64_t Np, int64_t ldc, float alpha, int beta) {
+                                                   int64_t Mp, int64_t Np, int64_t ldc, float alpha, int beta,
+                                                   int upper, int64_t kps, int64_t cslice) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * TSTAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t nbn = Np / TB, nbm = Mp / TB;
-  const int64_t bid = tg_xcd_remap(blockIdx.x, nbm * nbn);
-  const int64_t m0 = (bid / nbn) * TB, n0 = (bid % nbn) * TB;
+  int64_t m0, n0;
+  tg_tile(Mp / TB, Np / TB, upper, m0, n0);
+  // split-K: slice blockIdx.y covers stages [y kps, min((y + 1) kps, Kp / TK)) into C + y cslice
+  const int64_t t0 = (int64_t)blockIdx.y * kps;
+  C += (int64_t)blockIdx.y * cslice;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r = lane & 31;
 
   // staging: wave w moves plane w (0 A hi, 1 A lo, 2 B hi, 3 B lo): 2 k-chunks x 4 pieces of 64 rows
   const _Float16* plane = wave == 0 ? Ahi : wave == 1 ? Alo : wave == 2 ? Bhi : Blo;
   const int64_t prow = wave < 2 ? Mp : Np;
-  const _Float16* src0 = plane + ((wave < 2 ? m0 : n0) + lane) * 8;
+  const _Float16* src0 = plane + ((wave < 2 ? m0 : n0) + lane) * 8 + 2 * t0 * prow * 8;
   auto stage = [&](int64_t t) {
     unsigned char* dst = smem + (t & (TNBUF - 1)) * TSTAGE + wave * 8192;
     const _Float16* s = src0 + (2 * t) * prow * 8;
@@ -175,7 +194,7 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
     }
   };
 
-  const int64_t nk = Kp / TK;
+  const int64_t nk = Kp / TK - t0 < kps ? Kp / TK - t0 : kps;
   // Steady-state stage (t + 3 < nk, no branches, so the scheduler sees one region per half): the
   // DMA of stage t+3 issued between the first accumulator row's MFMAs, the counted wait for stage
   // t+1 + barrier, then stage t+1's 16 fragment reads spread between the other 36 MFMAs. Every
@@ -273,12 +292,20 @@ struct F32Frag<true> {
 template <bool AK, bool BK_, bool MI16>
 __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
-                                                    int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta) {
+                                                    int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
+                                                    int upper, int64_t kps, int64_t cslice) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * F32_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t nbn = (N + TB - 1) / TB, nbm = (M + TB - 1) / TB;
-  const int64_t bid = tg_xcd_remap(blockIdx.x, nbm * nbn);
-  const int64_t m0 = (bid / nbn) * TB, n0 = (bid % nbn) * TB;
+  int64_t m0, n0;
+  tg_tile((M + TB - 1) / TB, (N + TB - 1) / TB, upper, m0, n0);
+  // split-K: slice blockIdx.y = k in [y kps TK, min((y + 1) kps TK, K)) into C + y cslice
+  {
+    const int64_t k0 = (int64_t)blockIdx.y * kps * TK;
+    A += AK ? k0 * lda : k0;
+    B += BK_ ? k0 * ldb : k0;
+    K = K - k0 < kps * TK ? K - k0 : kps * TK;
+    C += (int64_t)blockIdx.y * cslice;
+  }
   const int wm = wave >> 1, wn = wave & 1;
 
   // staging: waves 0, 1 move A (16 pieces of 1 KB), waves 2, 3 move B. Piece q (0..15) of an
@@ -678,18 +705,34 @@ __global__ __launch_bounds__(256) void tg_split_cols(const float* __restrict__ X
 
 template <bool AK, bool BK_>
 int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, float alpha, int beta, hipStream_t s) {
-  const int64_t nwg = ((M + TB - 1) / TB) * ((N + TB - 1) / TB);
-  if (nwg > 0x7FFFFFFF) return HA_UNSUPPORTED;
+                int64_t ldc, float alpha, int beta, int upper, int64_t slices, int64_t cslice, hipStream_t s) {
+  const int64_t nbm = (M + TB - 1) / TB, nbn = (N + TB - 1) / TB;
+  const int64_t nwg = upper ? nbn * (nbn + 1) / 2 : nbm * nbn;
+  if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
+  const int64_t nk = (K + TK - 1) / TK, kps = (nk + slices - 1) / slices;
+  const dim3 grid((unsigned)nwg, (unsigned)((nk + kps - 1) / kps));
   // HEAT_GEMM_F32_SHAPE=16 selects the 16x16x4 MFMA shape (A/B benchmarking)
   static const int shape = getenv("HEAT_GEMM_F32_SHAPE") ? atoi(getenv("HEAT_GEMM_F32_SHAPE")) : 32;
   if (shape == 16)
-    hipLaunchKernelGGL((gemm_f32t<AK, BK_, true>), dim3((unsigned)nwg), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb,
-                       ldc, alpha, beta);
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, true>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha,
+                       beta, upper, kps, cslice);
   else
-    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false>), dim3((unsigned)nwg), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb,
-                       ldc, alpha, beta);
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha,
+                       beta, upper, kps, cslice);
   return ha_launch_status();
+}
+
+__global__ __launch_bounds__(256) void tg_sum_slices(const float* __restrict__ P, int64_t S, int64_t M, int64_t N,
+                                                     int64_t cslice, double* __restrict__ out, int64_t ldo, int upper,
+                                                     int accumulate) {
+  const int64_t total = M * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / N, j = e - i * N;
+    if (upper && j < i) continue;
+    double acc = accumulate ? out[i * ldo + j] : 0.0;
+    for (int64_t z = 0; z < S; ++z) acc += (double)P[z * cslice + e];
+    out[i * ldo + j] = acc;
+  }
 }
 
 }  // namespace
@@ -698,35 +741,65 @@ int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, 
 // A[k lda + m] (else A[m lda + k]); b_kmajor: B element (k, n) at B[k ldb + n] (else B[n ldb + k]).
 // Requirements (else HA_UNSUPPORTED, the caller uses ha_gemm_f32): 16-byte aligned bases, leading
 // dimensions multiples of 4, the contiguous extent of each operand a multiple of 4, M, N >= 4.
+// slices > 1: split-K - slice s of the K range (multiples of 16) goes to C + s cslice (partials
+// for ha_sum_slices64). upper (M == N): only the 256-tiles on or above the diagonal are computed.
 HA_EXPORT int ha_gemm_f32t(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
-                           int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, float alpha, int beta, void* stream) {
-  if (M < 0 || N < 0 || K < 0 || !A || !B || !C) return HA_BAD_ARG;
+                           int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, float alpha, int beta, int upper,
+                           int64_t slices, int64_t cslice, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || !A || !B || !C || slices < 1 || (upper && M != N)) return HA_BAD_ARG;
   if (M == 0 || N == 0) return HA_OK;
   if (K < 4 || M < 4 || N < 4 || lda % 4 || ldb % 4 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return HA_UNSUPPORTED;
   if ((a_kmajor ? M : K) % 4 || (b_kmajor ? N : K) % 4) return HA_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
+#define HA_F32T(AK, BK) return f32t_launch<AK, BK>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, upper, slices, cslice, s)
   if (a_kmajor) {
-    if (b_kmajor) return f32t_launch<true, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-    return f32t_launch<true, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+    if (b_kmajor) HA_F32T(true, true);
+    HA_F32T(true, false);
   }
-  if (b_kmajor) return f32t_launch<false, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-  return f32t_launch<false, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+  if (b_kmajor) HA_F32T(false, true);
+  HA_F32T(false, false);
+#undef HA_F32T
 }
 
 // C[M, N] = alpha 2^-(eA_i + eB_j) (Ahi Bhi + Ahi Blo + Alo Bhi) (+ C if beta). Planes in the
 // K8-panel layout [Kp/8][Mp][8] / [Kp/8][Np][8] (Mp, Np multiples of 256, Kp of 16, 16-byte
-// aligned), exponents int32[Mp] / int32[Np].
+// aligned), exponents int32[Mp] / int32[Np]. slices / upper / cslice: as ha_gemm_f32t.
 HA_EXPORT int ha_gemm_h3t(const void* Ahi, const void* Alo, const void* Bhi, const void* Blo, const int* eA,
                           const int* eB, float* C, int64_t M, int64_t N, int64_t Kp, int64_t Mp, int64_t Np,
-                          int64_t ldc, float alpha, int beta, void* stream) {
+                          int64_t ldc, float alpha, int beta, int upper, int64_t slices, int64_t cslice,
+                          void* stream) {
   if (M < 0 || N < 0 || Kp < 0 || Kp % TK || Mp % TB || Np % TB || Mp < M || Np < N) return HA_BAD_ARG;
+  if (slices < 1 || (upper && (M != N || Mp != Np))) return HA_BAD_ARG;
   if (M == 0 || N == 0) return HA_OK;
   if ((((uintptr_t)Ahi | (uintptr_t)Alo | (uintptr_t)Bhi | (uintptr_t)Blo) & 15) != 0) return HA_BAD_ARG;
-  const int64_t nwg = (Mp / TB) * (Np / TB);
-  if (nwg > 0x7FFFFFFF) return HA_UNSUPPORTED;
-  hipLaunchKernelGGL(gemm_h3t, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream, (const _Float16*)Ahi,
-                     (const _Float16*)Alo, (const _Float16*)Bhi, (const _Float16*)Blo, eA, eB, C, M, N, Kp, Mp, Np, ldc,
-                     alpha, beta);
+  const int64_t nbn = Np / TB;
+  const int64_t nwg = upper ? nbn * (nbn + 1) / 2 : (Mp / TB) * nbn;
+  if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
+  const int64_t nk = Kp / TK, kps = nk > 0 ? (nk + slices - 1) / slices : 1;
+  const dim3 grid((unsigned)nwg, (unsigned)(nk > 0 ? (nk + kps - 1) / kps : 1));
+  hipLaunchKernelGGL(gemm_h3t, grid, dim3(256), 0, (hipStream_t)stream, (const _Float16*)Ahi, (const _Float16*)Alo,
+                     (const _Float16*)Bhi, (const _Float16*)Blo, eA, eB, C, M, N, Kp, Mp, Np, ldc, alpha, beta, upper,
+                     kps, cslice);
+  return ha_launch_status();
+}
+
+// The number of K slices ha_gemm_{f32t,h3t} launch for (K, slices): ceil(nk / ceil(nk / slices)).
+HA_EXPORT int64_t ha_gemm_tiled_slices(int64_t K, int64_t slices) {
+  const int64_t nk = (K + TK - 1) / TK;
+  if (nk <= 0 || slices < 1) return 1;
+  const int64_t kps = (nk + slices - 1) / slices;
+  return (nk + kps - 1) / kps;
+}
+
+// out[i, j] (fp64, ldo) (+)= sum over s = 0 .. S-1 of P[s cslice + i N + j] (fp32), in slice order;
+// upper: only j >= i (the rest of out untouched).
+HA_EXPORT int ha_sum_slices64(const float* P, int64_t S, int64_t M, int64_t N, int64_t cslice, double* out,
+                              int64_t ldo, int upper, int accumulate, void* stream) {
+  if (S < 1 || M < 0 || N < 0 || ldo < N) return HA_BAD_ARG;
+  if (M == 0 || N == 0) return HA_OK;
+  const int64_t total = M * N, g = (total + 255) / 256;
+  hipLaunchKernelGGL(tg_sum_slices, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, (hipStream_t)stream, P,
+                     S, M, N, cslice, out, ldo, upper, accumulate);
   return ha_launch_status();
 }
 

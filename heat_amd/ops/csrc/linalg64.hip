@@ -198,6 +198,126 @@ __global__ __launch_bounds__(64) void trtri_diag(const double* __restrict__ R, i
     if (i < nb) X[(o + i) * ldx + o + j] = x[i];
 }
 
+// ---------------------------------------------------------------------------------------------
+// vtc64: W = V^T C with fp64 products and accumulation over a very long contraction (the row
+// count of a tall matrix block: 1.25e6 on the north-star shape) - the "reduction over all rows"
+// GEMM of the blocked Householder QR (W = V^T C of the aggregated 256-column block
+// reflector, Y = V^T V for its T factor). V [m, nc], C [m, N], both row-major fp32 or fp64;
+// fp32 elements are widened exactly, so every product is exact and the only rounding is the
+// fp64 accumulation (what keeps ||Q^T Q - I|| at the 1e-7 level for an fp32 QR).
+//   * 128 x 128 output tile per workgroup (4 waves of 64 x 64 = 4 x 4 v_mfma_f64_16x16x4_f64
+//     accumulators), BK = 16 rows per stage, LDS double buffer in the input type with a row pitch
+//     chosen so the 4 k-rows x 16 lanes of one MFMA operand read hit 64 distinct banks; the next
+//     stage is prefetched into registers during the MFMAs (one barrier per stage);
+//   * split-K over row chunks (blockIdx.z): each split writes its fp64 partial tile P[s] and
+//     vtc64_sum adds the splits in index order - deterministic, no atomics.
+constexpr int VT_T = 128, VT_BK = 16;
+
+template <typename T> struct VtPitch;
+template <> struct VtPitch<float> { static constexpr int P = VT_T + 16; };   // 16 k-rows apart: 16 banks
+template <> struct VtPitch<double> { static constexpr int P = VT_T + 8; };   // 8 doubles = 16 banks
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void vtc64(const T* __restrict__ V, int64_t ldv, const T* __restrict__ C,
+                                             int64_t ldc, int64_t m, int64_t nc, int64_t N, int64_t chunk,
+                                             double* __restrict__ P) {
+  constexpr int PP = VtPitch<T>::P;
+  __shared__ T Vs[2][VT_BK][PP];
+  __shared__ T Cs[2][VT_BK][PP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.y * VT_T, j0 = (int64_t)blockIdx.x * VT_T;
+  const int64_t r0 = (int64_t)blockIdx.z * chunk;
+  const int64_t r1 = r0 + chunk < m ? r0 + chunk : m;
+  const int nst = r1 > r0 ? (int)((r1 - r0 + VT_BK - 1) / VT_BK) : 0;
+  const int wm = wave >> 1, wn = wave & 1;
+  // loader: each operand stage is 16 x 128 elements = 2048 / VEC vectors, LD per thread
+  constexpr int LD = VT_BK * VT_T / VEC / 256;
+  typedef T vec_t __attribute__((ext_vector_type(VEC)));
+  vec_t rv[LD], rc[LD];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < LD; ++q) {
+      const int e = tid + 256 * q;
+      const int kk = e / (VT_T / VEC), cc = (e % (VT_T / VEC)) * VEC;
+      const int64_t g = r0 + (int64_t)t * VT_BK + kk;
+      const bool rok = g < r1;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) { rv[q][v] = T(0); rc[q][v] = T(0); }
+      if (VEC > 1) {
+        if (rok && i0 + cc < nc) rv[q] = *(const vec_t*)(V + g * ldv + i0 + cc);
+        if (rok && j0 + cc < N) rc[q] = *(const vec_t*)(C + g * ldc + j0 + cc);
+      } else {
+        if (rok && i0 + cc < nc) rv[q][0] = V[g * ldv + i0 + cc];
+        if (rok && j0 + cc < N) rc[q][0] = C[g * ldc + j0 + cc];
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < LD; ++q) {
+      const int e = tid + 256 * q;
+      const int kk = e / (VT_T / VEC), cc = (e % (VT_T / VEC)) * VEC;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        Vs[buf][kk][cc + v] = rv[q][v];
+        Cs[buf][kk][cc + v] = rc[q][v];
+      }
+    }
+  };
+  doublex4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (doublex4)(0.0);
+  if (nst > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nst; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nst) load(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < VT_BK; ks += 4) {
+      const int kk = ks + (lane >> 4);
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = (double)Vs[buf][kk][wm * 64 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (double)Cs[buf][kk][wn * 64 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nst) store(buf ^ 1);
+    __syncthreads();
+  }
+  // partial tile (zeros for an empty chunk): P[z][i][j], f64 16x16x4 C/D map
+  double* Pz = P + (int64_t)blockIdx.z * nc * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gj = j0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t gi = i0 + wm * 64 + i * 16 + (lane >> 4) + 4 * g;
+        if (gi < nc && gj < N) Pz[gi * N + gj] = acc[i][j][g];
+      }
+    }
+}
+
+// W[e] (+)= sum over splits s = 0, 1, ... of P[s][e], in split order.
+__global__ __launch_bounds__(256) void vtc64_sum(const double* __restrict__ P, int64_t splits, int64_t plane,
+                                                 double* __restrict__ W, int accumulate) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < plane; e += (int64_t)gridDim.x * 256) {
+    double s = accumulate ? W[e] : 0.0;
+    for (int64_t z = 0; z < splits; ++z) s += P[z * plane + e];
+    W[e] = s;
+  }
+}
+
 template <bool AK, bool BK_, bool UP>
 int gemm64_launch(const double* A, const double* B, double* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                   int64_t ldb, int64_t ldc, int64_t batch, int64_t sA, int64_t sB, int64_t sC, double alpha,
@@ -230,6 +350,60 @@ HA_EXPORT int ha_gemm64(const double* A, const double* B, double* C, int64_t M, 
   if (b_kmajor) HA_G64(false, true, false);
   HA_G64(false, false, false);
 #undef HA_G64
+}
+
+// Row-chunk split count of ha_vtc64 for (m, nc, N): enough workgroups to fill the chip (>= ~1024)
+// with >= 32 stages per split; the caller sizes the partial buffer as splits * nc * N doubles.
+HA_EXPORT int64_t ha_vtc64_splits(int64_t m, int64_t nc, int64_t N) {
+  if (m <= 0 || nc <= 0 || N <= 0) return 1;
+  const int64_t tiles = ((nc + VT_T - 1) / VT_T) * ((N + VT_T - 1) / VT_T);
+  int64_t s = (1024 + tiles - 1) / tiles;
+  const int64_t maxs = (m + 32 * VT_BK - 1) / (32 * VT_BK);
+  if (s > maxs) s = maxs;
+  if (s > 65535) s = 65535;
+  return s < 1 ? 1 : s;
+}
+
+// W [nc, N] (row-major fp64, contiguous) = V^T C (+ W when accumulate), V [m, nc] (ldv) and
+// C [m, N] (ldc) row-major, dtype 0 = fp32 / 1 = fp64; P: ha_vtc64_splits(m, nc, N) * nc * N
+// doubles of scratch. Deterministic (fixed split order).
+HA_EXPORT int ha_vtc64(const void* V, int64_t ldv, const void* C, int64_t ldc, int dtype, int64_t m, int64_t nc,
+                       int64_t N, double* W, double* P, int accumulate, void* stream) {
+  if (m < 0 || nc < 0 || N < 0 || (dtype != 0 && dtype != 1)) return HA_BAD_ARG;
+  if (nc == 0 || N == 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (m == 0) {
+    if (!accumulate) hipMemsetAsync(W, 0, (size_t)(nc * N) * sizeof(double), s);
+    return ha_launch_status();
+  }
+  if ((nc + VT_T - 1) / VT_T > 65535) return HA_UNSUPPORTED;
+  const int64_t splits = ha_vtc64_splits(m, nc, N);
+  const int64_t chunk = ((m + splits - 1) / splits + VT_BK - 1) / VT_BK * VT_BK;
+  const dim3 grid((unsigned)((N + VT_T - 1) / VT_T), (unsigned)((nc + VT_T - 1) / VT_T), (unsigned)splits);
+  if (dtype == 0) {
+    const bool v4 = nc % 4 == 0 && N % 4 == 0 && ldv % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)V & 15) == 0 &&
+                    ((uintptr_t)C & 15) == 0;
+    if (v4)
+      hipLaunchKernelGGL((vtc64<float, 4>), grid, dim3(256), 0, s, (const float*)V, ldv, (const float*)C, ldc, m, nc,
+                         N, chunk, P);
+    else
+      hipLaunchKernelGGL((vtc64<float, 1>), grid, dim3(256), 0, s, (const float*)V, ldv, (const float*)C, ldc, m, nc,
+                         N, chunk, P);
+  } else {
+    const bool v2 = nc % 2 == 0 && N % 2 == 0 && ldv % 2 == 0 && ldc % 2 == 0 && ((uintptr_t)V & 15) == 0 &&
+                    ((uintptr_t)C & 15) == 0;
+    if (v2)
+      hipLaunchKernelGGL((vtc64<double, 2>), grid, dim3(256), 0, s, (const double*)V, ldv, (const double*)C, ldc, m,
+                         nc, N, chunk, P);
+    else
+      hipLaunchKernelGGL((vtc64<double, 1>), grid, dim3(256), 0, s, (const double*)V, ldv, (const double*)C, ldc, m,
+                         nc, N, chunk, P);
+  }
+  const int64_t plane = nc * N;
+  const int64_t g = (plane + 255) / 256;
+  hipLaunchKernelGGL(vtc64_sum, dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0, s, P, splits, plane, W,
+                     accumulate);
+  return ha_launch_status();
 }
 
 // Upper Cholesky G = R^T R of the n x n symmetric fp64 matrix G (row-major, ld; the upper triangle

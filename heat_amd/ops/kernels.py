@@ -18,7 +18,7 @@ __all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", 
            "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "h3_planes", "H3Planes",
            "gemm_h3_planes", "gemm64", "cholesky_upper", "tri_inv_upper", "householder_qr",
-           "householder_factor", "householder_apply", "householder_block",
+           "householder_factor", "householder_apply", "householder_block", "vtc64", "gram64",
            "radix_sort_supported", "sort_rows"]
 
 _NUM_CUS = {}
@@ -951,7 +951,7 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     st = ctypes.c_void_p(stream_ptr(a.device))
     ldc = out.stride(0) if M > 1 else N
     rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(not b_nm),
-                        float(alpha), int(accumulate), st)
+                        float(alpha), int(accumulate), 0, 1, 0, st)
     if rc == _HA_UNSUPPORTED:
         if alpha != 1.0:
             tmp = gemm_f32(a, b)
@@ -1012,7 +1012,7 @@ def gemm_h3_planes(pa: H3Planes, pb: H3Planes, out: torch.Tensor, alpha: float =
     M, N = pa.rows, pb.rows
     check(lib().ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(out),
                             M, N, pa.Kp, pa.Rp, pb.Rp, out.stride(0) if M > 1 else N, float(alpha), int(accumulate),
-                            ctypes.c_void_p(stream_ptr(out.device))), "ha_gemm_h3t")
+                            0, 1, 0, ctypes.c_void_p(stream_ptr(out.device))), "ha_gemm_h3t")
     return out
 
 
@@ -1040,6 +1040,66 @@ def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     if int((pa.flag + pb.flag).item()) != 0:
         return None
     return gemm_h3_planes(pa, pb, out, alpha, accumulate)
+
+
+_GRAM_KCHUNK = max(16, int(os.environ.get("HEAT_GRAM_KCHUNK", "4096")) // 16 * 16)
+_GRAM_PARTIAL_BYTES = 1 << 30
+
+
+def gram64(x: torch.Tensor, exact: Optional[bool] = None) -> torch.Tensor:
+    """Upper triangle (lower triangle zero) of the Gram matrix x^T x of a tall fp32 block as an
+    fp64 [n, n] tensor - the CholeskyQR Gram. One 256-tile MFMA launch per group of K slices
+    (``csrc/gemm_tiled.hip``: upper-triangle tiles only, split-K over ``HEAT_GRAM_KCHUNK`` = 4096
+    rows), fp32 accumulation inside a slice and the slices summed in fp64 in fixed order
+    (``ha_sum_slices64``): the accumulation error of one fp32 sum over all 1.25e6 rows (~u sqrt(m) / 3
+    = 4e-5 relative on the diagonal at m = 1.25e6) drops to ~u chunk / (3 sqrt(m)) = 7e-8. ``exact``: exact fp32
+    products (``gemm_f32t``) instead of the fp16x3 split (``gemm_h3t``); default from
+    torch.get_float32_matmul_precision() ("highest" -> exact). Host / fp64: an fp64 GEMM."""
+    m, n = x.shape
+    if not (x.is_cuda and use_native(x)) or x.dtype != torch.float32:
+        return torch.triu(x.double().T @ x.double())
+    out = torch.zeros((n, n), dtype=torch.float64, device=x.device)
+    if m == 0 or n == 0:
+        return out
+    if exact is None:
+        exact = torch.get_float32_matmul_precision() == "highest"
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(x.device))
+    kc = _GRAM_KCHUNK
+    group = max(1, min(-(-m // kc), _GRAM_PARTIAL_BYTES // (4 * n * n)))
+    P = torch.empty(group * n * n, dtype=torch.float32, device=x.device)
+    pa = None
+    if not exact:
+        pa = h3_planes(x.t(), 1)
+        if int(pa.flag.item()) != 0:
+            pa = None
+            exact = True
+    for k0 in range(0, m, group * kc):
+        k1 = min(m, k0 + group * kc)
+        slices = -(-(k1 - k0) // kc)
+        if exact:
+            xs = x[k0:k1]
+            if xs.stride(1) != 1 or xs.stride(0) % 4 or xs.data_ptr() % 16 or n % 4:
+                xs = xs.contiguous()
+            rc = L.ha_gemm_f32t(_ptr(xs), _ptr(xs), _ptr(P), n, n, k1 - k0, xs.stride(0), xs.stride(0), n, 1, 1,
+                                1.0, 0, 1, slices, n * n, st)
+            if rc == _HA_UNSUPPORTED:   # tiny / unaligned blocks: the 128-tile kernel, one slice
+                res = gemm_f32(xs.t(), xs)
+                out += torch.triu(res.double())
+                continue
+            check(rc, "ha_gemm_f32t")
+            used = L.ha_gemm_tiled_slices(k1 - k0, slices)
+        else:
+            kp0 = k0                       # k0 is a multiple of kc (16 | kc): a plane panel boundary
+            kp1 = min(pa.Kp, k0 + group * kc) if k1 == m else k1
+            off = (kp0 // 8) * pa.Rp * 8 * 2   # bytes into the [Kp/8][Rp][8] fp16 planes
+            check(L.ha_gemm_h3t(ctypes.c_void_p(pa.hi.data_ptr() + off), ctypes.c_void_p(pa.lo.data_ptr() + off),
+                                ctypes.c_void_p(pa.hi.data_ptr() + off), ctypes.c_void_p(pa.lo.data_ptr() + off),
+                                _ptr(pa.ex), _ptr(pa.ex), _ptr(P), n, n, kp1 - kp0, pa.Rp, pa.Rp, n, 1.0, 0, 1,
+                                slices, n * n, st), "ha_gemm_h3t")
+            used = L.ha_gemm_tiled_slices(kp1 - kp0, slices)
+        check(L.ha_sum_slices64(_ptr(P), used, n, n, n * n, _ptr(out), n, 1, 1, st), "ha_sum_slices64")
+    return out
 
 
 def gemm_h3_v1(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
@@ -1192,15 +1252,34 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
     return Q * d.unsqueeze(0), R
 
 
+def _hh_outer(native: bool, nb: int) -> int:
+    """Width of the aggregated block reflector of the two-level Householder factorisation: the
+    trailing matrix is updated once per outer block (W = V^T C on the fp64 matrix cores, then one
+    K = 256 GEMM) instead of once per 32-column panel. Env ``HEAT_HH_OUTER`` overrides (a multiple
+    of the panel width; = panel width: the one-level algorithm)."""
+    env = os.environ.get("HEAT_HH_OUTER")
+    w = int(env) if env else (8 * nb if native else 2 * nb)
+    return max(nb, w // nb * nb)
+
+
 def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] = None, allreduce=None):
     """The factorisation half of :func:`householder_qr`: returns (A, panels) - A holds R in its
     upper triangle and the reflectors below it (LAPACK geqrf layout, rows [g0, g0 + m_r) of the
-    global matrix), ``panels`` the compact-WY blocks as [(k0, nc, T)]."""
+    global matrix), ``panels`` the compact-WY blocks as [(k0, nc, T)].
+
+    Two-level blocking (ref ``heat/core/linalg/qr.py`` factors tiles with torch.linalg.qr; this is
+    the MI355X design): 32-column panels (``csrc/householder.hip``: one kernel per column with
+    fp64 dot products, ``hh_larft`` T factor) update only the rest of their 256-column outer
+    block; the outer block is then applied to the trailing matrix as ONE block reflector
+    Q_b = I - V T V^T with T = (striu(V^T V) + diag(1/tau))^-1 (``tri_inv_upper``), W = V^T C
+    from the fp64 matrix-core kernel (``csrc/linalg64.hip: vtc64``, exact products, split-K in
+    fixed order) and C -= V (T^T W) on the exact-fp32 MFMA GEMM (``gemm_f32``). No library GEMM."""
     m_r, n = local.shape
     m_total = m_r if m_total is None else m_total
     native = local.is_cuda and use_native(local)
     L = lib() if native else None
     nb = L.ha_hh_nb() if native else 32
+    outer = _hh_outer(native, nb)
     slen = L.ha_hh_slen() if native else 2 * nb  # replicated accumulators (the host path: one)
     dev = local.device
     dt = local.dtype
@@ -1211,44 +1290,61 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
     red = allreduce or (lambda t: t)
     rows = torch.arange(g0, g0 + m_r, device=dev).unsqueeze(1)
     panels = []
-    for k0 in range(0, kmax, nb):
-        nc = min(nb, kmax - k0)
-        S = torch.zeros((nc + 1, slen), dtype=torch.float64, device=dev)
-        tau = torch.empty(nc, dtype=dt, device=dev)
-        if native:
-            check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), st), "ha_hh_colsums")
-        else:
-            _hh_colsums_host(A, rows, k0, nc, S[0])
-        red(S[0])
-        for j in range(nc):
-            last = j + 1 == nc
+    for K0 in range(0, kmax, outer):
+        ncol = min(outer, kmax - K0)
+        taus, inner = [], []
+        for k0 in range(K0, K0 + ncol, nb):
+            nc = min(nb, K0 + ncol - k0)
+            S = torch.zeros((nc + 1, slen), dtype=torch.float64, device=dev)
+            tau = torch.empty(nc, dtype=dt, device=dev)
             if native:
-                check(L.ha_hh_step(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, j, _ptr(S[j]),
-                                   _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), st), "ha_hh_step")
+                check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), st),
+                      "ha_hh_colsums")
             else:
-                _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau)
-            if not last:
-                red(S[j + 1])
-        V = _hh_v(A, rows, k0, nc)
-        Y = _vtc(V, V, native, st)   # V^T V, fp64 accumulation (a tall-skinny fp64 BLAS GEMM is slow)
-        red(Y)
-        Tm = torch.empty((nc, nc), dtype=dt, device=dev)
-        if native:
-            check(L.ha_hh_larft(_ptr(Y.contiguous()), _ptr(tau), nc, code, _ptr(Tm), st), "ha_hh_larft")
+                _hh_colsums_host(A, rows, k0, nc, S[0])
+            red(S[0])
+            for j in range(nc):
+                last = j + 1 == nc
+                if native:
+                    check(L.ha_hh_step(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, j, _ptr(S[j]),
+                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), st), "ha_hh_step")
+                else:
+                    _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau)
+                if not last:
+                    red(S[j + 1])
+            taus.append(tau)
+            V = _hh_v(A, rows, k0, nc)
+            Y = _vtc(V, V, native, st)   # V^T V, fp64 accumulation (a tall-skinny fp64 BLAS GEMM is slow)
+            red(Y)
+            Tm = torch.empty((nc, nc), dtype=dt, device=dev)
+            if native:
+                check(L.ha_hh_larft(_ptr(Y.contiguous()), _ptr(tau), nc, code, _ptr(Tm), st), "ha_hh_larft")
+            else:
+                Tm.copy_(_hh_larft_host(Y, tau))
+            inner.append(Tm)
+            if k0 + nc < K0 + ncol:        # the rest of this outer block
+                _hh_block_update(A[:, k0 + nc: K0 + ncol], V, Tm, True, native, st, red)
+        if len(inner) == 1:
+            Tb = inner[0].double()
+            V = _hh_v(A, rows, K0, ncol)
         else:
-            Tm.copy_(_hh_larft_host(Y, tau))
-        panels.append((k0, nc, Tm))
-        if k0 + nc < n:
-            C = A[:, k0 + nc:]
-            W = _vtc(V, C, native, st)   # fp64 reduction over all rows
-            red(W)
-            C.addmm_(V, (Tm.double().T @ W).to(dt), alpha=-1.0)
+            V = _hh_v(A, rows, K0, ncol)
+            Y = _vtc(V, V, native, st)
+            red(Y)
+            tinv = torch.triu(Y, diagonal=1)
+            tinv.diagonal().copy_(1.0 / torch.cat(taus).double())
+            Tb = tri_inv_upper(tinv)
+        panels.append((K0, ncol, Tb))
+        if K0 + ncol < n:
+            _hh_block_update(A[:, K0 + ncol:], V, Tb, True, native, st, red)
     return A, panels
 
 
 def householder_block(t: Optional[torch.Tensor] = None) -> int:
-    """Panel width of the blocked Householder factorisation of ``t``'s device/dtype."""
-    return lib().ha_hh_nb() if t is not None and t.is_cuda and use_native(t) else 32
+    """Width of the compact-WY blocks :func:`householder_factor` returns for ``t``'s device (the
+    outer block: its ``panels`` are [(k0, min(width, kmax - k0), T fp64)] for k0 = 0, width, ...)."""
+    native = t is not None and t.is_cuda and use_native(t)
+    return _hh_outer(native, lib().ha_hh_nb() if native else 32)
 
 
 def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, transpose: bool = True,
@@ -1265,22 +1361,85 @@ def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, tra
         # C = [I; 0] accumulation: columns before k0 are still unit vectors that V (zero above
         # global row k0) does not touch
         Cc = C[:, k0:] if identity_start else C
-        W = _vtc(V, Cc, native, st)
-        red(W)
-        Tt = Tm.double().T if transpose else Tm.double()
-        Cc.addmm_(V, (Tt @ W).to(C.dtype), alpha=-1.0)
+        _hh_block_update(Cc, V, Tm, transpose, native, st, red)
     return C
 
 
+_HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "f32")   # f32 (exact MFMA) | h3 (fp16x3 MFMA) | blas
+
+
+def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpose: bool, native: bool, st,
+                     red) -> None:
+    """C -= V op(T) (V^T C) in place: W = V^T C with fp64 accumulation (summed over the ranks by
+    ``red``), X = op(T) W in fp64 (``gemm64``), then the rank-nc update on the hand-written MFMA
+    GEMMs (fp32: ``gemm_f32`` exact / ``gemm_h3``; fp64: ``gemm64``)."""
+    if C.shape[1] == 0 or V.shape[1] == 0:
+        return
+    W = _vtc(V, C, native, st)
+    red(W)
+    T64 = Tm.double()
+    Tt = T64.T if transpose else T64
+    if not native:
+        C.addmm_(V, (Tt @ W).to(C.dtype), alpha=-1.0)
+        return
+    X = gemm64(Tt, W)
+    if C.dtype == torch.float64:
+        gemm64(V, X, out=C, alpha=-1.0, beta=1.0)
+        return
+    X = X.to(C.dtype)
+    if C.stride(1) != 1 or _HH_UPDATE == "blas":
+        C.addmm_(V, X, alpha=-1.0)
+    elif _HH_UPDATE == "h3" and gemm_h3(V, X, out=C, alpha=-1.0, accumulate=True) is not None:
+        pass
+    else:
+        gemm_f32(V, X, out=C, accumulate=True, alpha=-1.0)
+
+
+def vtc64(V: torch.Tensor, C: torch.Tensor, out: Optional[torch.Tensor] = None,
+          accumulate: bool = False) -> torch.Tensor:
+    """``V^T C`` ([nc, N] fp64) with exact products and fp64 accumulation over the (long) row
+    dimension on the fp64 matrix cores (``csrc/linalg64.hip: vtc64``; split-K partials added in
+    fixed order - deterministic). V [m, nc], C [m, N]: fp32 or fp64 device tensors, rows
+    contiguous. Host tensors: an fp64 GEMM."""
+    nc, N = V.shape[1], C.shape[1]
+    if not (V.is_cuda and use_native(V)) or V.dtype not in (torch.float32, torch.float64):
+        r = V.double().T @ C.double()
+        if out is None:
+            return r
+        return out.add_(r) if accumulate else out.copy_(r)
+    if C.dtype != V.dtype:
+        C = C.to(V.dtype)
+    if V.stride(-1) != 1 or (nc > 1 and V.stride(0) < nc):
+        V = V.contiguous()
+    if C.stride(-1) != 1 or (N > 1 and C.stride(0) < N):
+        C = C.contiguous()
+    if out is None:
+        out = torch.zeros((nc, N), dtype=torch.float64, device=V.device) if accumulate else \
+            torch.empty((nc, N), dtype=torch.float64, device=V.device)
+    elif not out.is_contiguous() or out.shape != (nc, N) or out.dtype != torch.float64:
+        raise ValueError("vtc64: out must be a contiguous float64 [nc, N] tensor")
+    L = lib()
+    m = V.shape[0]
+    P = torch.empty(max(1, L.ha_vtc64_splits(m, nc, N) * nc * N), dtype=torch.float64, device=V.device)
+    check(L.ha_vtc64(_ptr(V), V.stride(0) if m > 1 else nc, _ptr(C), C.stride(0) if m > 1 else N,
+                     0 if V.dtype == torch.float32 else 1, m, nc, N, _ptr(out), _ptr(P), int(accumulate),
+                     ctypes.c_void_p(stream_ptr(V.device))), "ha_vtc64")
+    return out
+
+
 def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:
-    """V^T C in fp64 accumulation (``hh_vtc``; host: an fp64 GEMM)."""
+    """V^T C in fp64 accumulation: panels up to the 32-column panel width on the VALU kernel
+    (``hh_vtc``, memory-bound there), wider block reflectors on the fp64 matrix cores
+    (:func:`vtc64`); host: an fp64 GEMM."""
     if not native:
         return V.double().T @ C.double()
     nc, N = V.shape[1], C.shape[1]
-    W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)
     if C.stride(1) != 1:
         C = C.contiguous()
     L = lib()
+    if nc > L.ha_hh_nb():
+        return vtc64(V, C)
+    W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)
     P = torch.empty(max(1, L.ha_hh_vtc_splits(V.shape[0], N) * nc * N), dtype=torch.float64, device=V.device)
     check(L.ha_hh_vtc(_ptr(V), V.stride(0), _ptr(C), C.stride(0), 0 if V.dtype == torch.float32 else 1,
                       V.shape[0], N, nc, _ptr(W), _ptr(P), st), "ha_hh_vtc")

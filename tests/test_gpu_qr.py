@@ -23,7 +23,7 @@ def _ill(m, n, cond, seed, dtype):
     return ((G * s) @ V.T).to(dtype)
 
 
-@pytest.mark.parametrize("m,n", [(5000, 100), (20000, 256), (777, 65), (300, 300), (4097, 33)])
+@pytest.mark.parametrize("m,n", [(5000, 100), (20000, 256), (777, 65), (300, 300), (4097, 33), (30000, 700)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_householder_qr_device(m, n, dtype):
     from heat_amd import ops
@@ -138,9 +138,73 @@ def test_cholqr_native_path(m, n, precision):
         q, r = ht.linalg.qr(x, mode="reduced")
         Q, R = q.larray.double(), r.larray.double()
         orth = (Q.T @ Q - torch.eye(n, dtype=torch.float64, device=dev)).abs().max().item()
-        assert orth < 1e-4, orth   # fp32 CholeskyQR2: ~ n eps
+        assert orth < 2e-6, orth   # fp32 CholeskyQR2 with the fp64-summed split-K Gram
         rec = (Q @ R - a.to(dev).double()).abs().max().item() / a.abs().max().item()
         assert rec < 1e-5, rec
         assert torch.equal(R, torch.triu(R)) and bool((torch.diagonal(R) >= 0).all())
     finally:
         torch.set_float32_matmul_precision(old)
+
+
+# ------------------------------------------------- two-level Householder / fp64 V^T C / split-K Gram
+@pytest.mark.parametrize("m,nc,N", [(100_000, 256, 1000), (5000, 256, 256), (777, 130, 333), (64, 3, 5),
+                                    (300_001, 128, 128)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_vtc64(m, nc, N, dtype):
+    """V^T C on the fp64 matrix cores: exact products, fp64 accumulation, against an fp64 GEMM
+    (vector and scalar load variants, row/column edges, split-K chunk tails)."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + nc + N)
+    V = torch.randn(m, nc, generator=g, dtype=dtype).to(dev)
+    C = torch.randn(m, N, generator=g, dtype=dtype).to(dev)
+    W = ops.vtc64(V, C)
+    ref = V.double().T @ C.double()
+    scale = (V.double().abs().T @ C.double().abs()).max().item()
+    assert (W - ref).abs().max().item() < 1e-13 * scale
+    # column-offset views (unaligned base: the scalar-load kernel) and accumulation
+    W2 = ops.vtc64(V[:, 1:], C[:, 1:], out=W[1:, 1:].contiguous(), accumulate=True)
+    assert torch.allclose(W2, 2 * ref[1:, 1:], rtol=1e-12, atol=1e-12 * scale)
+    # deterministic: bitwise equal on a re-run
+    assert torch.equal(ops.vtc64(V, C), W)
+
+
+@pytest.mark.parametrize("exact", [True, False])
+@pytest.mark.parametrize("m,n,group_bytes", [(200_000, 512, 1 << 30), (100_000, 300, 1 << 20), (9000, 256, 1 << 30),
+                                              (50_000, 64, 1 << 16)])
+def test_gram64_split_k(m, n, group_bytes, exact, monkeypatch):
+    """Upper-triangle fp64 Gram from fp32 MFMA slices (several slice groups when the partial
+    buffer is small): error at the fp32-per-slice level, far below a single fp32 sum."""
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    monkeypatch.setattr(K, "_GRAM_PARTIAL_BYTES", group_bytes)
+    g = torch.Generator().manual_seed(m + n)
+    x = (torch.randn(m, n, generator=g) * torch.logspace(0, 2, n)).to(dev)
+    G = ops.gram64(x, exact=exact)
+    ref = x.double().T @ x.double()
+    up = torch.ones(n, n, dtype=torch.bool, device=dev).triu()
+    assert torch.equal(G[~up], torch.zeros_like(G[~up]))
+    d = torch.sqrt(torch.diagonal(ref))
+    rel = ((G - ref).abs() / (d.unsqueeze(1) * d.unsqueeze(0)))[up].max().item()
+    # fp32 accumulation inside a slice of kc rows, fp64 across slices: relative diagonal error
+    # ~ u kc / (3 sqrt(m)) (one fp32 sum over all m rows: ~ u sqrt(m) / 3)
+    kc = min(K._GRAM_KCHUNK, m)
+    assert rel < 10 * 2.0 ** -24 * kc / m ** 0.5, rel
+
+
+def test_householder_two_level_orthogonality_fp32():
+    """fp32 Householder with 256-column block reflectors (vtc64 + exact fp32 MFMA update): Q is
+    orthogonal to < 1e-6 for an ill-conditioned input, R matches the host algorithm."""
+    from heat_amd import ops
+
+    dev = _dev()
+    a = _ill(60_000, 640, 1e8, 9, torch.float32)
+    q, r = ops.householder_qr(a.to(dev), 0, a.shape[0], True)
+    Q = q.double()
+    orth = (Q.T @ Q - torch.eye(640, dtype=torch.float64, device=dev)).abs().max().item()
+    assert orth < 1e-6, orth
+    rec = (Q @ r.double() - a.to(dev).double()).abs().max().item() / a.abs().max().item()
+    assert rec < 1e-5, rec

@@ -22,9 +22,18 @@ def timed(fn, reps=2):
     return best, r
 
 
+def orth_err(Q, n, m):
+    G = torch.zeros(n, n, dtype=torch.float64, device="cuda")
+    for r0 in range(0, m, 1 << 17):
+        blk = Q[r0: r0 + (1 << 17)].double()
+        G += blk.T @ blk
+    return float((G - torch.eye(n, dtype=torch.float64, device="cuda")).abs().max())
+
+
 def main():
-    m = int(sys.argv[1]) if len(sys.argv) > 1 else 1_250_000
-    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    m = int(args[0]) if len(args) > 0 else 1_250_000
+    n = int(args[1]) if len(args) > 1 else 4096
     ht.use_device("gpu")
     ht.random.seed(1)
     a = ht.random.randn(m, n, split=0)
@@ -42,15 +51,20 @@ def main():
         Q, R = q.larray, r.larray.double()
         sub = Q[rows].double()
         rec = float((sub @ R - a.larray[rows].double()).abs().max() / a.larray[rows].abs().max())
-        G = torch.zeros(n, n, dtype=torch.float64, device="cuda")
-        for r0 in range(0, m, 1 << 17):
-            blk = Q[r0: r0 + (1 << 17)].double()
-            G += blk.T @ blk
-        orth = float((G - torch.eye(n, dtype=torch.float64, device="cuda")).abs().max())
+        orth = orth_err(Q, n, m)
         print(json.dumps({"op": "qr", "precision": prec, "shape": [m, n], "s": t, "orth": orth, "rec": rec}),
               flush=True)
         del q, r, Q
         torch.cuda.empty_cache()
+    if "--householder" in sys.argv:
+        # the backward-stable path every ill-conditioned / split-1 input takes (two-level blocked)
+        from heat_amd import ops
+
+        t, (Q, R) = timed(lambda: ops.householder_qr(a.larray, 0, m, True), reps=1)
+        rec = float((Q[rows].double() @ R.double() - a.larray[rows].double()).abs().max()
+                    / a.larray[rows].abs().max())
+        print(json.dumps({"op": "householder_qr", "shape": [m, n], "s": t, "orth": orth_err(Q, n, m), "rec": rec}),
+              flush=True)
 
 
 if __name__ == "__main__":
