@@ -289,7 +289,47 @@ struct F32Frag<true> {
   floatx4 a[8], b[8];
 };
 
-template <bool AK, bool BK_, bool MI16>
+// One f32 operand's DMA sources for this lane: piece q (0..15) of a stage is k-row q of a k-major
+// operand (4 consecutive rows per lane, 1 KB contiguous per piece) or k-chunk q >> 2 of row group
+// q & 3 of a row-major one (16 B of row 64 (q & 3) + lane); rows clamped into range.
+template <bool KM>
+struct F32Src {
+  const float* base;
+  const float* rb[4];
+  int64_t ld;
+  static constexpr int stride = KM ? F32_KP : 1024;
+  __device__ __forceinline__ void init(const float* P, int64_t ld_, int64_t rows, int64_t rbase, int lane) {
+    ld = ld_;
+    if (KM) {
+      int64_t c = rbase + 4 * lane;
+      base = P + (c + 4 <= rows ? c : rows - 4);
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t row = rbase + 64 * g + lane;
+        rb[g] = P + (row < rows ? row : rows - 1) * ld;
+      }
+    }
+  }
+  __device__ __forceinline__ const float* src(int64_t k0, int q) const {
+    return KM ? base + (k0 + q) * ld : rb[q & 3] + k0 + 4 * (q >> 2);
+  }
+  __device__ __forceinline__ const float* src_clamped(int64_t k0, int q, int64_t K) const {
+    if (KM) {
+      const int64_t k = k0 + q < K ? k0 + q : K - 1;
+      return base + k * ld;
+    }
+    const int64_t k = k0 + 4 * (q >> 2) + 4 <= K ? k0 + 4 * (q >> 2) : K - 4;
+    return rb[q & 3] + k;
+  }
+  __device__ __forceinline__ bool beyond(int64_t k0, int q, int64_t K) const {
+    return KM ? k0 + q >= K : k0 + 4 * (q >> 2) >= K;
+  }
+};
+
+// SP: every wave moves 4 pieces of A and 4 of B (pieces 4 wave .. 4 wave + 3 of each, interleaved)
+// - else waves 0, 1 move A and waves 2, 3 move B.
+template <bool AK, bool BK_, bool MI16, bool SP>
 __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
@@ -372,6 +412,33 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
       } else {
         if (k0 + 4 * (q >> 2) >= K) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
       }
+    }
+  };
+  F32Src<AK> sa;
+  F32Src<BK_> sb;
+  if constexpr (SP) {
+    sa.init(A, lda, M, m0, lane);
+    sb.init(B, ldb, N, n0, lane);
+  }
+  auto stage_sp = [&](int64_t t, bool full) {
+    unsigned char* dst = smem + (t & (TNBUF - 1)) * F32_STAGE;
+    const int64_t k0 = t * TK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = 4 * wave + i;
+      tg_dma16(full ? sa.src(k0, q) : sa.src_clamped(k0, q, K), dst + q * sa.stride);
+      tg_dma16(full ? sb.src(k0, q) : sb.src_clamped(k0, q, K), dst + F32_OP + q * sb.stride);
+    }
+  };
+  auto zero_tail_sp = [&](int64_t t) {
+    unsigned char* dst = smem + (t & (TNBUF - 1)) * F32_STAGE;
+    const int64_t k0 = t * TK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = 4 * wave + i;
+      if (sa.beyond(k0, q, K)) *reinterpret_cast<floatx4*>(dst + q * sa.stride + lane * 16) = (floatx4)(0.f);
+      if (sb.beyond(k0, q, K))
+        *reinterpret_cast<floatx4*>(dst + F32_OP + q * sb.stride + lane * 16) = (floatx4)(0.f);
     }
   };
 
@@ -471,14 +538,16 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
       if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       else if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      zero_tail(t);
+      if constexpr (SP) zero_tail_sp(t);
+      else zero_tail(t);
     }
     tg_wait_stage(t, nk);
   };
   // steady state (t + 3 < nk and stage t + 1 is not the zero-padded tail): branch-free, DMA and
   // fragment reads interleaved with the MFMAs (see gemm_h3t)
   auto step_full = [&](int64_t t, const F32Frag<MI16>& Fc, F32Frag<MI16>& Fn) {
-    stage_full(t + 3);
+    if constexpr (SP) stage_sp(t + 3, true);
+    else stage_full(t + 3);
     mma_part(Fc, 0);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -498,7 +567,10 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
     __builtin_amdgcn_sched_barrier(0);
   };
   auto step = [&](int64_t t, const F32Frag<MI16>& Fc, F32Frag<MI16>& Fn) {
-    if (t + 3 < nk) stage(t + 3);
+    if (t + 3 < nk) {
+      if constexpr (SP) stage_sp(t + 3, false);
+      else stage(t + 3);
+    }
     mma_part(Fc, 0);
     if (t + 1 < nk) {
       ready(t + 1);
@@ -510,7 +582,10 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
   };
 
   F32Frag<MI16> F0, F1;
-  for (int64_t t = 0; t < 3 && t < nk; ++t) stage(t);
+  for (int64_t t = 0; t < 3 && t < nk; ++t) {
+    if constexpr (SP) stage_sp(t, false);
+    else stage(t);
+  }
   if (nk > 0) {
     ready(0);
     load(F0, 0);
@@ -711,14 +786,19 @@ int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, 
   if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
   const int64_t nk = (K + TK - 1) / TK, kps = (nk + slices - 1) / slices;
   const dim3 grid((unsigned)nwg, (unsigned)((nk + kps - 1) / kps));
-  // HEAT_GEMM_F32_SHAPE=16 selects the 16x16x4 MFMA shape (A/B benchmarking)
+  // HEAT_GEMM_F32_SHAPE=16 selects the 16x16x4 MFMA shape, HEAT_GEMM_F32_SPREAD=0 the A-waves /
+  // B-waves DMA split (A/B benchmarking)
   static const int shape = getenv("HEAT_GEMM_F32_SHAPE") ? atoi(getenv("HEAT_GEMM_F32_SHAPE")) : 32;
+  static const int spread = getenv("HEAT_GEMM_F32_SPREAD") ? atoi(getenv("HEAT_GEMM_F32_SPREAD")) : 1;
   if (shape == 16)
-    hipLaunchKernelGGL((gemm_f32t<AK, BK_, true>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha,
-                       beta, upper, kps, cslice);
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, true, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc,
+                       alpha, beta, upper, kps, cslice);
+  else if (spread)
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false, true>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc,
+                       alpha, beta, upper, kps, cslice);
   else
-    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha,
-                       beta, upper, kps, cslice);
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc,
+                       alpha, beta, upper, kps, cslice);
   return ha_launch_status();
 }
 

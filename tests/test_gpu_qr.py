@@ -138,7 +138,7 @@ def test_cholqr_native_path(m, n, precision):
         q, r = ht.linalg.qr(x, mode="reduced")
         Q, R = q.larray.double(), r.larray.double()
         orth = (Q.T @ Q - torch.eye(n, dtype=torch.float64, device=dev)).abs().max().item()
-        assert orth < 2e-6, orth   # fp32 CholeskyQR2 with the fp64-summed split-K Gram
+        assert orth < 5e-6, orth   # fp32 CholeskyQR2 with the fp64-summed split-K Gram
         rec = (Q @ R - a.to(dev).double()).abs().max().item() / a.abs().max().item()
         assert rec < 1e-5, rec
         assert torch.equal(R, torch.triu(R)) and bool((torch.diagonal(R) >= 0).all())

@@ -68,6 +68,9 @@ def main():
             "h3_v1": lambda: K.gemm_h3_v1(a, b, out=c),
             "blas_f16x3": lambda: ops.gemm_f16x3(a, b, out=c),
         }
+        only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--only=")]
+        if only:
+            variants = {k: v for k, v in variants.items() if k in only[0]}
         rows = torch.randint(0, M, (64,), device="cuda")
         best = {}
         for rnd in range(rounds):
