@@ -273,6 +273,8 @@ row_stack = vstack
 
 def stack(arrays: Sequence[DNDarray], axis: int = 0, out: Optional[DNDarray] = None) -> DNDarray:
     """Join arrays of identical shape along a new axis."""
+    if isinstance(arrays, DNDarray) or not isinstance(arrays, (list, tuple)):
+        raise TypeError("stack expects a sequence (list or tuple) of DNDarrays, got {}".format(type(arrays)))
     arrays = list(arrays)
     if len(arrays) < 2:
         raise ValueError("stack expects a sequence of at least 2 DNDarrays")
@@ -592,8 +594,9 @@ def pad(array: DNDarray, pad_width, mode: str = "constant", constant_values=0) -
         cvs = [(cv, cv)] * nd
     t = array.larray
     split = array.split if array.is_distributed() else None
-    # pad every non-split axis locally, from the last axis to the first (NumPy order of corners)
-    for ax in reversed(range(nd)):
+    # pad every non-split axis locally, first axis first: a later (higher) axis pads the full
+    # extent of the earlier ones, so corners take the higher axis' constant (NumPy)
+    for ax in range(nd):
         if ax == split:
             continue
         before, after = widths[ax]
@@ -642,6 +645,16 @@ def pad(array: DNDarray, pad_width, mode: str = "constant", constant_values=0) -
         local_parts.append(torch.full(sh, cvs[split][1], dtype=t.dtype, device=t.device))
     local = torch.cat(local_parts, dim=split)
     res = _segment_exchange(local, split, array.comm, segs, _chunk_counts(gshape[split], p))
+    # the split-axis rows were filled with the split axis' constant everywhere; the pad regions of
+    # higher axes win their corners (NumPy)
+    for ax in range(split + 1, nd):
+        before, after = widths[ax]
+        if cvs[ax] == cvs[split] or res.numel() == 0:
+            continue
+        if before:
+            res.narrow(ax, 0, before).fill_(cvs[ax][0])
+        if after:
+            res.narrow(ax, res.shape[ax] - after, after).fill_(cvs[ax][1])
     return DNDarray(res, gshape, array.dtype, split, array.device, array.comm, True)
 
 
@@ -696,6 +709,8 @@ def tile(x: DNDarray, reps) -> DNDarray:
         raise TypeError("x must be a DNDarray")
     if isinstance(reps, (int, np.integer)):
         reps = (int(reps),)
+    if not isinstance(reps, (list, tuple, np.ndarray)) or not all(isinstance(r, (int, np.integer)) for r in reps):
+        raise TypeError("reps must be an integer or a sequence of integers, got {}".format(reps))
     reps = [int(r) for r in reps]
     if any(r < 0 for r in reps):
         raise ValueError("reps must be non-negative")
@@ -730,6 +745,13 @@ def tile(x: DNDarray, reps) -> DNDarray:
 # ---------------------------------------------------------------------------------------------
 def diagonal(a: DNDarray, offset: int = 0, dim1: int = 0, dim2: int = 1) -> DNDarray:
     """Diagonal of ``a`` over ``dim1``/``dim2``, appended as the last axis of the result."""
+    if not isinstance(a, DNDarray):
+        raise TypeError("expected a DNDarray, got {}".format(type(a)))
+    if a.ndim < 2:
+        raise ValueError("diagonal requires an array of at least 2 dimensions, got {}".format(a.ndim))
+    if not isinstance(offset, (int, np.integer)) or isinstance(offset, bool):
+        raise ValueError("offset must be an integer, got {}".format(type(offset)))
+    offset = int(offset)
     dim1 = sanitize_axis(a.gshape, dim1)
     dim2 = sanitize_axis(a.gshape, dim2)
     if dim1 == dim2:
@@ -758,6 +780,11 @@ def diagonal(a: DNDarray, offset: int = 0, dim1: int = 0, dim2: int = 1) -> DNDa
 
 def diag(a: DNDarray, offset: int = 0) -> DNDarray:
     """1-D -> diagonal matrix, 2-D -> its diagonal."""
+    if not isinstance(a, DNDarray):
+        raise TypeError("expected a DNDarray, got {}".format(type(a)))
+    if not isinstance(offset, (int, np.integer)) or isinstance(offset, bool):
+        raise ValueError("offset must be an integer, got {}".format(type(offset)))
+    offset = int(offset)
     if len(a.gshape) > 1:
         return diagonal(a, offset=offset)
     if len(a.gshape) < 1:
@@ -990,8 +1017,15 @@ def topk(a: DNDarray, k: int, dim: int = -1, largest: bool = True, sorted: bool 
         v = DNDarray(v2[sl].contiguous(), tuple(gshape), a.dtype, dim, a.device, a.comm, True)
         i = DNDarray(i2[sl].contiguous(), tuple(gshape), types.int64, dim, a.device, a.comm, True)
     if out is not None:
-        out[0].larray = v.larray
-        out[1].larray = i.larray
+        for o, r in zip(out, (v, i)):
+            if o.gshape != r.gshape:
+                raise ValueError("out shape {} does not match the result shape {}".format(o.gshape, r.gshape))
+            if r.split != o.split:   # e.g. a replicated out buffer for a split-axis top-k
+                r = resplit(r, o.split)
+            if r.lshape != o.lshape:
+                r = r.copy()
+                r.redistribute_(lshape_map=r.create_lshape_map(), target_map=o.create_lshape_map())
+            o.larray = r.larray.to(o.larray.dtype)
         return out
     return v, i
 

@@ -595,9 +595,10 @@ def test_gemm_f16x3_nonfinite_falls_back(gpu):
 
 
 def test_matmul_split_precision(gpu):
-    """ht.matmul / ht.linalg.qr honour torch's float32 matmul precision ("high" -> split GEMM)."""
+    """ht.matmul / ht.linalg.qr honour torch's float32 matmul precision ("high" -> the fused
+    fp16x3 kernel gemm_h3t, "highest" -> the exact f32 MFMA kernel), both hand-written."""
     import heat_amd as ht
-    from heat_amd.core.linalg import basics
+    from heat_amd import ops
 
     ht.random.seed(2)
     a = ht.random.randn(4096, 1024, split=0)
@@ -605,21 +606,30 @@ def test_matmul_split_precision(gpu):
     ref = a.larray.double() @ b.larray.double()
     old = torch.get_float32_matmul_precision()
     calls = []
-    orig = basics._leaf_mm
+    orig_h3, orig_f32 = ops.gemm_h3, ops.gemm_f32
 
-    def spy(x, y):
-        calls.append(basics._split_gemm_ok(x, y))
-        return orig(x, y)
+    def spy_h3(*args, **kw):
+        calls.append("h3")
+        return orig_h3(*args, **kw)
 
-    basics._leaf_mm = spy
+    def spy_f32(*args, **kw):
+        calls.append("f32")
+        return orig_f32(*args, **kw)
+
+    ops.gemm_h3, ops.gemm_f32 = spy_h3, spy_f32
     try:
         torch.set_float32_matmul_precision("high")
         c = ht.matmul(a, b).larray
         q, r = ht.linalg.qr(a)
+        assert "h3" in calls and "f32" not in calls, calls
+        calls.clear()
+        torch.set_float32_matmul_precision("highest")
+        c2 = ht.matmul(a, b).larray
+        assert calls == ["f32"], calls
     finally:
         torch.set_float32_matmul_precision(old)
-        basics._leaf_mm = orig
-    assert any(calls)
+        ops.gemm_h3, ops.gemm_f32 = orig_h3, orig_f32
+    assert torch.allclose(c2.double(), ref, rtol=1e-5, atol=1e-3)
     assert torch.allclose(c.double(), ref, rtol=1e-5, atol=1e-3)
     qr = q.larray.double() @ r.larray.double()
     assert torch.allclose(qr, a.larray.double(), atol=1e-4)
