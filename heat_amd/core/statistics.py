@@ -464,6 +464,8 @@ def bincount(x: DNDarray, weights: Optional[DNDarray] = None, minlength: int = 0
     """Occurrences of each value in a non-negative int array (one MAX + one SUM all-reduce)."""
     if not isinstance(x, DNDarray):
         raise TypeError("x must be a DNDarray")
+    if x.ndim != 1:
+        raise ValueError("bincount expects a 1-D array, got {} dimensions".format(x.ndim))
     t = x.larray.reshape(-1).to(torch.int64)
     mx = int(t.max()) + 1 if t.numel() else 0
     length = builtins_max(mx, minlength)
@@ -473,9 +475,12 @@ def bincount(x: DNDarray, weights: Optional[DNDarray] = None, minlength: int = 0
     if weights is not None:
         if weights.gshape != x.gshape:
             raise ValueError("weights and x must have the same shape")
-        w = weights.larray.reshape(-1)
         if weights.split != x.split:
             raise ValueError("weights and x must have the same split")
+        if weights.lshape != x.lshape:   # same split, another partition (e.g. x unbalanced)
+            weights = weights.copy()
+            weights.redistribute_(lshape_map=weights.create_lshape_map(), target_map=x.create_lshape_map())
+        w = weights.larray.reshape(-1)
     counts = torch.bincount(t, weights=None if w is None else w.to(torch.float64), minlength=length)
     # an empty local block must agree with the others on dtype (float64 with weights, like NumPy)
     counts = counts.to(torch.int64 if w is None else torch.float64)
