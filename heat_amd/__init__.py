@@ -23,7 +23,6 @@ from . import classification
 from . import nn
 from . import optim
 from . import utils
-from . import models
 from . import profiling
 from . import datasets
 from . import testing

@@ -478,6 +478,7 @@ __global__ __launch_bounds__(256) void ku_gather4(const float* __restrict__ X, i
 //   * ku_reduce_det: sums[c] = the cluster's range partials added in range order (fp64).
 constexpr int KU_RANGE = 256;
 constexpr int KU_RD = 8;  // rows in flight per gather thread
+constexpr int KU_SB = 8;  // label batches loaded together per wave in ku_scatter_det
 
 __global__ __launch_bounds__(1024) void ku_scatter_det(const int* __restrict__ lab, int64_t n, int k,
                                                        int64_t rows_per_blk, int W, const int* __restrict__ hist,
@@ -491,9 +492,14 @@ __global__ __launch_bounds__(1024) void ku_scatter_det(const int* __restrict__ l
   const int64_t s1 = s0 + sub < r1 ? s0 + sub : r1;
   for (int e = tid; e < W * k; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
-  for (int64_t i = s0 + lane; i < s1; i += 64) {
-    const int l = lab[i];
-    if ((unsigned)l < (unsigned)k) atomicAdd(&cnt[w * k + l], 1);  // integer counts: order-free
+  // 8 label loads in flight per lane (one at a time left the pass latency-bound)
+  for (int64_t i0 = s0 + lane; i0 < s1; i0 += 64 * KU_SB) {
+    int l[KU_SB];
+#pragma unroll
+    for (int u = 0; u < KU_SB; ++u) l[u] = i0 + 64 * u < s1 ? lab[i0 + 64 * u] : -1;
+#pragma unroll
+    for (int u = 0; u < KU_SB; ++u)
+      if ((unsigned)l[u] < (unsigned)k) atomicAdd(&cnt[w * k + l[u]], 1);  // integer counts: order-free
   }
   __syncthreads();
   for (int c = tid; c < k; c += blockDim.x) {
@@ -507,9 +513,15 @@ __global__ __launch_bounds__(1024) void ku_scatter_det(const int* __restrict__ l
   __syncthreads();
   int* my = cnt + w * k;
   const unsigned long long below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= lane
-  for (int64_t b0 = s0; b0 < s1; b0 += 64) {
-    const int64_t i = b0 + lane;
-    const int l = i < s1 ? lab[i] : -1;
+  for (int64_t g0 = s0; g0 < s1; g0 += 64 * KU_SB) {
+  int lg[KU_SB];  // the labels of the next KU_SB batches, loaded together
+#pragma unroll
+  for (int u = 0; u < KU_SB; ++u) lg[u] = g0 + 64 * u + lane < s1 ? lab[g0 + 64 * u + lane] : -1;
+#pragma unroll
+  for (int u = 0; u < KU_SB; ++u) {
+    const int64_t b0 = g0 + 64 * u;
+    if (b0 >= s1) break;
+    const int l = lg[u];
     int key = (unsigned)l < (unsigned)k ? (l << 6) | lane : 0x7FFFFFFF;
     // bitonic sort of the 64 keys across the wave (ascending by label, then lane)
 #pragma unroll
@@ -539,6 +551,7 @@ __global__ __launch_bounds__(1024) void ku_scatter_det(const int* __restrict__ l
     }
     const int b = __shfl(base, mys < 0 ? 0 : mys, 64);
     if (valid) order[b + (lane - mys)] = (int)(b0 + (key & 63));
+  }
   }
 }
 
@@ -618,7 +631,15 @@ __global__ __launch_bounds__(256) void ku_reduce_det(const float* __restrict__ P
   double s = 0.0;
   if (b > a) {
     const int64_t rlo = a / KU_RANGE, rhi = (b - 1) / KU_RANGE;
-    for (int64_t r = rlo; r <= rhi; ++r) s += (double)P[((int64_t)c + r) * f + j];
+    int64_t r = rlo;
+    for (; r + 8 <= rhi + 1; r += 8) {  // 8 loads in flight, added in range order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = P[((int64_t)c + r + u) * f + j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; r <= rhi; ++r) s += (double)P[((int64_t)c + r) * f + j];
   }
   sums[e] = (float)s;
 }

@@ -71,19 +71,23 @@ __device__ __forceinline__ void mom_emit(const Trip& t, int kind, double ddof, v
   reinterpret_cast<float*>(out)[i] = (float)v;
 }
 
-// Publish this block's partial (already stored by thread 0) and take a ticket on the per-output
-// arrival counter; true in every thread of the block that arrived last. Agent-scope release before
-// the ticket, acquire (L1 invalidate) in the last block before it reads the other partials; the
-// last block resets the counter for the next launch on this workspace.
+// This block's partials are stored write-through (ha_store_wt) by the threads that own them; each
+// of those waves drained them (s_waitcnt vmcnt(0)) before the barrier here. Lane 0 takes a ticket
+// on the per-output arrival counter (agent-scope atomic, no release fence: see common.h); true in
+// every thread of the block that arrived last, after ONE agent acquire, which also resets the
+// counter for the next launch on this workspace.
 __device__ __forceinline__ bool mom_last_arrival(unsigned* __restrict__ cnt, unsigned expected) {
   __shared__ bool last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const bool l = atomicAdd(cnt, 1u) == expected - 1;
+    const unsigned t = __hip_atomic_fetch_add((ha_gu32*)(cnt), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const bool l = t == expected - 1;
     if (l) {
-      __threadfence();
-      *cnt = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store((ha_gu32*)(cnt), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     last = l;
   }
@@ -93,9 +97,42 @@ __device__ __forceinline__ bool mom_last_arrival(unsigned* __restrict__ cnt, uns
 
 __device__ __forceinline__ Trip mom_load(const double* p) { return Trip{p[0], p[1], p[2]}; }
 
+// Chan merge of the triples p[q * stride], q in [q0, q1), in q order; 8 triples loaded per round
+// (the loads are independent of the merge chain, so 8 are in flight instead of one).
+__device__ __forceinline__ Trip mom_merge_strided(const double* p, int q0, int q1, int64_t stride) {
+  Trip t = {0.0, 0.0, 0.0};
+  int q = q0;
+  for (; q + 8 <= q1; q += 8) {
+    Trip v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = mom_load(p + (int64_t)(q + u) * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t = chan(t, v[u]);
+  }
+  for (; q < q1; ++q) t = chan(t, mom_load(p + (int64_t)q * stride));
+  return t;
+}
+
+// Chan merge of one triple per thread over a 256-thread block (wave butterflies, then the 4 wave
+// results in wave order); the result is valid in thread 0. sh: 4 x 3 doubles of LDS.
+__device__ __forceinline__ Trip mom_block_merge(Trip t, double (*sh)[3]) {
+  t = wave_merge(t);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sh[w][0] = t.n;
+    sh[w][1] = t.mean;
+    sh[w][2] = t.m2;
+  }
+  __syncthreads();
+  Trip acc = {sh[0][0], sh[0][1], sh[0][2]};
+  for (int k = 1; k < 4; ++k) acc = chan(acc, Trip{sh[k][0], sh[k][1], sh[k][2]});
+  return acc;
+}
+
 // rows: x[r * ld + i], i in [0, len).  Grid.x = nrows * nchunks; part[(r*nchunks + c)*3 + {0,1,2}]
 __global__ __launch_bounds__(256) void mom_rows(const float* __restrict__ x, int64_t nrows, int64_t len,
-                                                int64_t ld, int nchunks, double* __restrict__ part,
+                                                int64_t ld, int nchunks, int G, double* __restrict__ part,
                                                 void* __restrict__ out, int kind, double ddof,
                                                 unsigned* __restrict__ arrive) {
   const int64_t g = blockIdx.x;
@@ -177,29 +214,39 @@ __global__ __launch_bounds__(256) void mom_rows(const float* __restrict__ x, int
       mom_emit(acc, kind, ddof, out, r);
     } else {
       double* o = part + g * 3;
-      o[0] = acc.n;
-      o[1] = acc.mean;
-      o[2] = acc.m2;
+      if (out != nullptr) {  // handed to the row's last block
+        ha_store_wt(o, acc.n);
+        ha_store_wt(o + 1, acc.mean);
+        ha_store_wt(o + 2, acc.m2);
+      } else {
+        o[0] = acc.n;
+        o[1] = acc.mean;
+        o[2] = acc.m2;
+      }
     }
   }
   if (out == nullptr || nchunks == 1) return;
-  // fused epilogue: the last of the row's nchunks blocks merges their partials in chunk order
-  if (!mom_last_arrival(arrive + r, (unsigned)nchunks)) return;
-  Trip m = {0.0, 0.0, 0.0};
-  for (int q = tid; q < nchunks; q += 256) m = chan(m, mom_load(part + (r * nchunks + q) * 3));
-  m = wave_merge(m);
-  __syncthreads();
-  if ((tid & 63) == 0) {
-    sh[w][0] = m.n;
-    sh[w][1] = m.mean;
-    sh[w][2] = m.m2;
-  }
-  __syncthreads();
+  // fused epilogue, a two-level tree: the last-arriving block of each group of G consecutive
+  // chunks merges the group (one partial per thread, fixed lane order), the last group merges the
+  // group partials. One counter for all chunks serialised ~2K same-address atomics (+40 us on a
+  // 0.64 ms pass); a group's G adds spread over ~sqrt(nchunks) counters.
+  const int ngroups = (nchunks + G - 1) / G, grp = c / G;
+  unsigned* ctr = arrive + r * (ngroups + 1);
+  const int q0 = grp * G, q1 = q0 + G < nchunks ? q0 + G : nchunks;
+  if (!mom_last_arrival(ctr + grp, (unsigned)(q1 - q0))) return;
+  double* gpart = part + nrows * nchunks * 3;
+  Trip m = q0 + tid < q1 ? mom_load(part + (r * nchunks + q0 + tid) * 3) : Trip{0.0, 0.0, 0.0};
+  m = mom_block_merge(m, sh);
   if (tid == 0) {
-    Trip acc = {sh[0][0], sh[0][1], sh[0][2]};
-    for (int k = 1; k < 4; ++k) acc = chan(acc, Trip{sh[k][0], sh[k][1], sh[k][2]});
-    mom_emit(acc, kind, ddof, out, r);
+    double* o = gpart + (r * ngroups + grp) * 3;
+    ha_store_wt(o, m.n);
+    ha_store_wt(o + 1, m.mean);
+    ha_store_wt(o + 2, m.m2);
   }
+  if (!mom_last_arrival(ctr + ngroups, (unsigned)ngroups)) return;
+  m = tid < ngroups ? mom_load(gpart + (r * ngroups + tid) * 3) : Trip{0.0, 0.0, 0.0};
+  m = mom_block_merge(m, sh);
+  if (tid == 0) mom_emit(m, kind, ddof, out, r);
 }
 
 // Short rows (nchunks == 1, len <= 16K): one wave per row, 4 rows per workgroup.  All lanes share
@@ -270,7 +317,7 @@ __global__ __launch_bounds__(256) void mom_rows_wave(const float* __restrict__ x
 // columns; grid = (ceil(ncols / (256*VEC)), nchunks).  part[(c*ncols + col)*3 + {0,1,2}]
 template <int VEC>
 __global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int64_t len, int64_t ncols,
-                                                int64_t ld, int nchunks, double* __restrict__ part,
+                                                int64_t ld, int nchunks, int G, double* __restrict__ part,
                                                 void* __restrict__ out, int kind, double ddof,
                                                 unsigned* __restrict__ cnt) {
   const int64_t col0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
@@ -296,14 +343,15 @@ __global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int
     }
   }
   int64_t i = r0;
-  // 8 rows (128 B per thread) in flight: ~64-128 KB per CU at 2-4 workgroups per CU
+  // 16 rows (256 B per thread) in flight: ~128 KB per CU at 2 workgroups per CU (8 rows left the
+  // few-chunk grid short of bytes in flight; more chunks instead cost partials and merge depth)
   if (VEC == 4) {
-    for (; i + 7 < r1; i += 8) {
-      floatx4 a[8];
+    for (; i + 15 < r1; i += 16) {
+      floatx4 a[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(x + (i + u) * ld + col0));
+      for (int u = 0; u < 16; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(x + (i + u) * ld + col0));
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < 16; ++u)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float d = a[u][e] - K[e];
@@ -355,41 +403,76 @@ __global__ __launch_bounds__(256) void mom_cols(const float* __restrict__ x, int
         mom_emit(t, kind, ddof, out, col);
       } else {
         double* o = part + ((int64_t)c * ncols + col) * 3;
-        o[0] = t.n;
-        o[1] = t.mean;
-        o[2] = t.m2;
+        if (out != nullptr) {  // handed to the group's last block
+          ha_store_wt(o, t.n);
+          ha_store_wt(o + 1, t.mean);
+          ha_store_wt(o + 2, t.m2);
+        } else {
+          o[0] = t.n;
+          o[1] = t.mean;
+          o[2] = t.m2;
+        }
       }
     }
   }
   }
   if (out == nullptr || nchunks == 1) return;
-  // every thread's partial is stored: retire them before the block's release + ticket
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // fused epilogue: the last of the column block's nchunks blocks merges them in chunk order
-  if (!mom_last_arrival(cnt + blockIdx.x, (unsigned)nchunks)) return;
+  // fused epilogue as a two-level tree (a serial merge of ~2K partials per column in ONE block
+  // was latency-bound: 1e6 x 1000 axis 0 took 2x the HBM time): the last-arriving block of each
+  // group of G consecutive chunks merges the group's partials (chunk order) into gpart, the last
+  // group merges the group partials (group order) - deterministic whatever the arrival order.
+  const int ngroups = (nchunks + G - 1) / G, grp = c / G;
+  unsigned* ctr = cnt + (int64_t)blockIdx.x * (ngroups + 1);
+  const int q0 = grp * G, q1 = q0 + G < nchunks ? q0 + G : nchunks;
+  if (!mom_last_arrival(ctr + grp, (unsigned)(q1 - q0))) return;
+  double* gpart = part + (int64_t)nchunks * ncols * 3;
+  if (col0 < ncols) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const int64_t col = col0 + e;
+      if (col < ncols) {
+        const Trip t = mom_merge_strided(part + col * 3, q0, q1, ncols * 3);
+        double* o = gpart + ((int64_t)grp * ncols + col) * 3;
+        ha_store_wt(o, t.n);
+        ha_store_wt(o + 1, t.mean);
+        ha_store_wt(o + 2, t.m2);
+      }
+    }
+  }
+  if (!mom_last_arrival(ctr + ngroups, (unsigned)ngroups)) return;
   if (col0 >= ncols) return;
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
     const int64_t col = col0 + e;
-    if (col < ncols) {
-      Trip t = {0.0, 0.0, 0.0};
-      for (int q = 0; q < nchunks; ++q) t = chan(t, mom_load(part + ((int64_t)q * ncols + col) * 3));
-      mom_emit(t, kind, ddof, out, col);
-    }
+    if (col < ncols) mom_emit(mom_merge_strided(gpart + col * 3, 0, ngroups, ncols * 3), kind, ddof, out, col);
   }
 }
 
 }  // namespace
 
+// Chunks per merge group of the fused epilogues (ceil(sqrt(nchunks)): both tree levels short).
+static int mom_group(int nchunks) {
+  int g = 1;
+  while (g * g < nchunks) ++g;
+  return g;
+}
+
+// Workspace of ha_moments_rows' fused epilogue (nchunks > 1): doubles of part, zeroed counters.
+HA_EXPORT void ha_moments_rows_workspace(int64_t nrows, int nchunks, int64_t* part_doubles, int64_t* counters) {
+  const int g = mom_group(nchunks > 0 ? nchunks : 1);
+  const int64_t ngroups = (nchunks + g - 1) / g;
+  *part_doubles = nrows * (nchunks + (nchunks > 1 ? ngroups : 0)) * 3;
+  *counters = nchunks > 1 ? nrows * (ngroups + 1) : 0;
+}
+
 // (n, mean, M2) of each row x[r * ld + i], i < len. out == null: per-chunk partial triples into
 // part[(r nchunks + c) 3 + {0, 1, 2}]; else the final value per row (kind: 0 triple fp64, 1 mean,
-// 2 var, 3 std as fp32) into out - chunks merged by the row's last block (cnt: nrows zeroed
-// counters, reset by the kernel).
+// 2 var, 3 std as fp32) into out - chunks merged by a two-level tree of last-arriving blocks
+// (part / cnt sized by ha_moments_rows_workspace; the counters zeroed, reset by the kernel).
 HA_EXPORT int ha_moments_rows(const float* x, int64_t nrows, int64_t len, int64_t ld, int nchunks, double* part,
                               void* out, int kind, double ddof, unsigned* cnt, void* stream) {
   if (nrows <= 0) return HA_OK;
-  if (nchunks < 1 || (out != nullptr && nchunks > 1 && cnt == nullptr)) return HA_BAD_ARG;
+  if (nchunks < 1 || nchunks > 65536 || (out != nullptr && nchunks > 1 && cnt == nullptr)) return HA_BAD_ARG;
   if (nchunks == 1 && len > 0 && len <= 16384) {
     const int64_t blocks = (nrows + 3) / 4;
     if (blocks > 0x7fffffffLL) return HA_UNSUPPORTED;
@@ -400,12 +483,15 @@ HA_EXPORT int ha_moments_rows(const float* x, int64_t nrows, int64_t len, int64_
   const int64_t grid = nrows * nchunks;
   if (grid > 0x7fffffffLL) return HA_UNSUPPORTED;
   hipLaunchKernelGGL(mom_rows, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, x, nrows, len, ld, nchunks,
+                     mom_group(nchunks),
                      part, out, kind, ddof, cnt);
   return ha_launch_status();
 }
 
-// (n, mean, M2) of each column x[i * ld + col], i < len; out / kind / cnt as ha_moments_rows (cnt:
-// one counter per block of 256 * VEC columns, i.e. ceil(ncols / 256) suffice).
+// (n, mean, M2) of each column x[i * ld + col], i < len; out / kind as ha_moments_rows. With out
+// and nchunks > 1, part needs (nchunks + ceil(nchunks / G)) * ncols * 3 doubles and cnt
+// ceil(ncols / 256) * (ceil(nchunks / G) + 1) zeroed counters (ha_moments_cols_counters), G as
+// mom_group.
 HA_EXPORT int ha_moments_cols(const float* x, int64_t len, int64_t ncols, int64_t ld, int nchunks, double* part,
                               void* out, int kind, double ddof, unsigned* cnt, void* stream) {
   if (ncols <= 0) return HA_OK;
@@ -414,11 +500,19 @@ HA_EXPORT int ha_moments_cols(const float* x, int64_t len, int64_t ncols, int64_
   if (vec) {
     const int64_t gx = (ncols / 4 + 255) / 256;
     hipLaunchKernelGGL(mom_cols<4>, dim3((unsigned)gx, nchunks), dim3(256), 0, (hipStream_t)stream, x, len, ncols,
-                       ld, nchunks, part, out, kind, ddof, cnt);
+                       ld, nchunks, mom_group(nchunks), part, out, kind, ddof, cnt);
   } else {
     const int64_t gx = (ncols + 255) / 256;
     hipLaunchKernelGGL(mom_cols<1>, dim3((unsigned)gx, nchunks), dim3(256), 0, (hipStream_t)stream, x, len, ncols,
-                       ld, nchunks, part, out, kind, ddof, cnt);
+                       ld, nchunks, mom_group(nchunks), part, out, kind, ddof, cnt);
   }
   return ha_launch_status();
+}
+
+// Workspace of ha_moments_cols' fused epilogue: doubles of part (first) and counters (second).
+HA_EXPORT void ha_moments_cols_workspace(int64_t ncols, int nchunks, int64_t* part_doubles, int64_t* counters) {
+  const int g = mom_group(nchunks > 0 ? nchunks : 1);
+  const int64_t ngroups = (nchunks + g - 1) / g;
+  *part_doubles = (nchunks + (nchunks > 1 ? ngroups : 0)) * ncols * 3;
+  *counters = ((ncols + 255) / 256) * (ngroups + 1);
 }

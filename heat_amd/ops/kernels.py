@@ -315,6 +315,14 @@ def _mom_counters(device, n: int) -> torch.Tensor:
     return c
 
 
+def _mom_rows_workspace(device, nrows: int, nchunks: int):
+    """Partials + arrival counters of ha_moments_rows' fused epilogue (counters None if unused)."""
+    pd, nc = ctypes.c_int64(), ctypes.c_int64()
+    lib().ha_moments_rows_workspace(nrows, nchunks, ctypes.byref(pd), ctypes.byref(nc))
+    part = torch.empty(max(pd.value, 1), dtype=torch.float64, device=device)
+    return part, (_mom_counters(device, nc.value) if nc.value > 0 else None)
+
+
 def _moments_native(x: torch.Tensor, axis, final=None, ddof: int = 0):
     """One launch (``csrc/moments.hip``): per-chunk partials merged by each output's last block.
     final None: (N, mean, M2) fp64 triples; 'mean' / 'var' / 'std': the fp32 result itself."""
@@ -338,11 +346,12 @@ def _moments_native(x: torch.Tensor, axis, final=None, ddof: int = 0):
         if not flat.is_contiguous():
             flat = flat.contiguous()
         numel = flat.numel()
-        nchunks = max(1, min(8 * ncu, (numel + 16383) // 16384))
-        part = torch.empty((1, nchunks, 3), dtype=torch.float64, device=x.device)
+        cpc = int(os.environ.get("HEAT_MOM_ROW_CHUNKS_PER_CU", "4"))
+        nchunks = max(1, min(cpc * ncu, (numel + 16383) // 16384))
+        part, cnt = _mom_rows_workspace(x.device, 1, nchunks)
         out = out_for(())
         check(L.ha_moments_rows(_ptr(flat), 1, numel, numel, nchunks, _ptr(part), _ptr(out), kind, float(ddof),
-                                _ptr(_mom_counters(x.device, 1)), s), "ha_moments_rows")
+                                _ptr(cnt), s), "ha_moments_rows")
         return finish(out, ())
     if not x.is_contiguous():
         x = x.contiguous()
@@ -358,22 +367,24 @@ def _moments_native(x: torch.Tensor, axis, final=None, ddof: int = 0):
     if inner == 1:
         nrows = outer
         nchunks = max(1, min((2 * 8 * ncu + nrows - 1) // max(nrows, 1), (red + 4095) // 4096))
-        part = torch.empty((nrows, nchunks, 3), dtype=torch.float64, device=x.device)
+        part, cnt = _mom_rows_workspace(x.device, nrows, nchunks)
         out = out_for(out_shape)
         check(L.ha_moments_rows(_ptr(x), nrows, red, red, nchunks, _ptr(part), _ptr(out), kind, float(ddof),
-                                _ptr(_mom_counters(x.device, nrows) if nchunks > 1 else None), s), "ha_moments_rows")
+                                _ptr(cnt), s), "ha_moments_rows")
         return finish(out, out_shape)
     if outer == 1:
         ncols = inner
         col_blocks = max(1, (ncols + 1023) // 1024)
-        # row chunks: ~2 workgroups per CU, 8 rows in flight per thread (1e6 x 1000, axis 0: 8 per
-        # CU 0.91 ms, 4 0.81 ms, 2 0.76 ms = 5.3 TB/s; fewer partials for the merge too)
-        cpc = int(os.environ.get("HEAT_MOM_COL_CHUNKS_PER_CU", "2"))
+        # row chunks per CU (8 rows in flight per thread); the chunk partials are merged by a
+        # two-level tree inside the kernel (moments.hip), so many chunks cost no serial merge
+        cpc = int(os.environ.get("HEAT_MOM_COL_CHUNKS_PER_CU", "1"))
         nchunks = max(1, min(65535, (cpc * ncu + col_blocks - 1) // col_blocks, (red + 63) // 64))
-        part = torch.empty((nchunks, ncols, 3), dtype=torch.float64, device=x.device)
+        pd, nc = ctypes.c_int64(), ctypes.c_int64()
+        L.ha_moments_cols_workspace(ncols, nchunks, ctypes.byref(pd), ctypes.byref(nc))
+        part = torch.empty(pd.value, dtype=torch.float64, device=x.device)
         out = out_for(out_shape)
         check(L.ha_moments_cols(_ptr(x), red, ncols, ncols, nchunks, _ptr(part), _ptr(out), kind, float(ddof),
-                                _ptr(_mom_counters(x.device, (ncols + 255) // 256)), s), "ha_moments_cols")
+                                _ptr(_mom_counters(x.device, nc.value)), s), "ha_moments_cols")
         return finish(out, out_shape)
     y = x.movedim(axis, -1).contiguous()
     return _moments_native(y, y.dim() - 1, final, ddof)

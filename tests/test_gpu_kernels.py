@@ -333,6 +333,28 @@ def test_moments_fused_final(shape, axis, final):
         assert torch.equal(mu.float(), r)
 
 
+@pytest.mark.parametrize("shape,axis", [((4_000_000, 64), 0), ((64, 4_000_000), None), ((2000, 3000), 0)])
+def test_moments_handoff_fresh_each_call(shape, axis):
+    """The fused epilogue hands partials between blocks with write-through stores and a ticket
+    (no per-block release fence). Refill the SAME input buffer with new values before every call
+    (the workspaces come back from the caching allocator at the same addresses), so a stale
+    partial from the previous call would show up as a wrong result."""
+    from heat_amd import ops
+
+    dev = _dev()
+    x = torch.empty(*shape, device=dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    for it in range(12):
+        x.normal_(mean=float(it * 7 - 30), std=1.0 + it, generator=g)
+        r = ops.moments(x, axis, "var", 0)
+        xd = x.double()
+        rv = torch.var(xd, correction=0) if axis is None else torch.var(xd, dim=axis, correction=0)
+        assert torch.allclose(r.double(), rv, rtol=1e-5, atol=1e-6), (it, (r.double() - rv).abs().max())
+        m = ops.moments(x, axis, "mean")
+        rm = xd.mean() if axis is None else xd.mean(axis)
+        assert torch.allclose(m.double(), rm, rtol=1e-6, atol=1e-5), (it, (m.double() - rm).abs().max())
+
+
 @pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian", "manhattan"])
 @pytest.mark.parametrize("m,n,f", [(100, 50, 3), (1000, 777, 18), (257, 300, 128), (64, 64, 200)])
