@@ -9,6 +9,8 @@
 // vs ~6.3 for the default policy).
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 struct Trip {
@@ -313,6 +315,82 @@ __global__ __launch_bounds__(256) void mom_rows_wave(const float* __restrict__ x
   }
 }
 
+// Short aligned rows (4 <= len <= 1024, 16-byte aligned rows): a grid of a few workgroups per CU,
+// each wave walking rows r, r + nwaves, ... with the NEXT row's loads (<= 4 x 16 B per lane) issued
+// before the current row is reduced - one launch-free pipeline instead of a workgroup per 4 rows
+// (1e6 x 1000 axis 1: the per-row kernel left HBM at 5.6 TB/s, dispatch-bound on 250K workgroups).
+__device__ __forceinline__ void mom_row_loads(const float* row, int nv, int lane, floatx4 (&a)[4]) {
+  const floatx4* v4 = reinterpret_cast<const floatx4*>(row);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = lane + 64 * u;
+    a[u] = q < nv ? __builtin_nontemporal_load(v4 + q) : (floatx4)(0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void mom_rows_pipe(const float* __restrict__ x, int64_t nrows, int64_t len,
+                                                     int64_t ld, double* __restrict__ part, void* __restrict__ out,
+                                                     int kind, double ddof) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nv = (int)(len / 4), rem = (int)(len - 4 * (int64_t)nv);
+  floatx4 cur[4], nxt[4];
+  float tcur = 0.f, tnxt = 0.f;  // the scalar tail element of this lane (lane < rem)
+  if (r < nrows) {
+    mom_row_loads(x + r * ld, nv, lane, cur);
+    if (lane < rem) tcur = x[r * ld + 4 * nv + lane];
+  }
+  for (; r < nrows; r += nw) {
+    const int64_t rn = r + nw;
+    if (rn < nrows) {
+      mom_row_loads(x + rn * ld, nv, lane, nxt);
+      if (lane < rem) tnxt = x[rn * ld + 4 * nv + lane];
+    }
+    // the row is in registers: shift by its fp32 mean (one extra wave sum, no memory traffic) -
+    // a shift by row[0] lost ~10x in M2 when row[0] sat far in a tail (var of 5e4 rows of
+    // N(100, 9): 3e-6 relative)
+    float sm = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64 * u < nv) sm += (cur[u][0] + cur[u][1]) + (cur[u][2] + cur[u][3]);
+    if (lane < rem) sm += tcur;
+    const float K = ha_wave_sum(sm) / (float)len;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (lane + 64 * u < nv) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = cur[u][e] - K;
+          s1 += d;
+          s2 = fmaf(d, d, s2);
+        }
+      }
+    }
+    if (lane < rem) {
+      const float d = tcur - K;
+      s1 += d;
+      s2 = fmaf(d, d, s2);
+    }
+    s1 = ha_wave_sum(s1);
+    s2 = ha_wave_sum(s2);
+    if (lane == 0) {
+      const Trip t = trip_from_shifted((double)len, K, s1, s2);
+      if (out != nullptr) {
+        mom_emit(t, kind, ddof, out, r);
+      } else {
+        part[r * 3 + 0] = t.n;
+        part[r * 3 + 1] = t.mean;
+        part[r * 3 + 2] = t.m2;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+    tcur = tnxt;
+  }
+}
+
 // columns: x[i * ld + col], reduce over i in [0, len).  Each thread owns VEC consecutive
 // columns; grid = (ceil(ncols / (256*VEC)), nchunks).  part[(c*ncols + col)*3 + {0,1,2}]
 template <int VEC>
@@ -473,6 +551,17 @@ HA_EXPORT int ha_moments_rows(const float* x, int64_t nrows, int64_t len, int64_
                               void* out, int kind, double ddof, unsigned* cnt, void* stream) {
   if (nrows <= 0) return HA_OK;
   if (nchunks < 1 || nchunks > 65536 || (out != nullptr && nchunks > 1 && cnt == nullptr)) return HA_BAD_ARG;
+  static const bool pipe = [] { const char* e = getenv("HEAT_MOM_ROWS_PIPE"); return !e || atoi(e) != 0; }();
+  if (pipe && nchunks == 1 && len >= 4 && len <= 1024 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t want = (int64_t)ncu * 8, need = (nrows + 3) / 4;
+    const int64_t blocks = want < need ? want : need;
+    hipLaunchKernelGGL(mom_rows_pipe, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, nrows, len, ld,
+                       part, out, kind, ddof);
+    return ha_launch_status();
+  }
   if (nchunks == 1 && len > 0 && len <= 16384) {
     const int64_t blocks = (nrows + 3) / 4;
     if (blocks > 0x7fffffffLL) return HA_UNSUPPORTED;

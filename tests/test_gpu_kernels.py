@@ -304,7 +304,8 @@ def test_moments(shape, axis):
 
 @pytest.mark.parametrize("shape,axis", [((3_000_000,), None), ((1000, 5000), None), ((300, 70001), 1),
                                         ((70001, 300), 0), ((200_000, 3), 0), ((5, 1_000_001), 1),
-                                        ((64, 50, 33), 1), ((1000, 1001), 0), ((1000, 1001), 1)])
+                                        ((64, 50, 33), 1), ((1000, 1001), 0), ((1000, 1001), 1),
+                                        ((50_000, 1000), 1), ((100_000, 4), 1), ((33, 1024), 1), ((7, 8), 1)])
 @pytest.mark.parametrize("final", ["mean", "var", "std"])
 def test_moments_fused_final(shape, axis, final):
     """ONE launch per call: the per-chunk partials are merged by each output's last-arriving block
