@@ -37,5 +37,37 @@ def test_datasets():
     assert np.bincount(y.numpy()).tolist() == [50, 50, 50]
     km = ht.cluster.KMeans(n_clusters=3, init="kmeans++", random_state=1).fit(X)
     assert km.cluster_centers_.shape == (3, 4)
-    Xd, yd = ht.datasets.diabetes()
+    Xd, yd = ht.datasets.diabetes(synthetic=True)
     assert Xd.shape == (442, 10) and yd.shape == (442, 1)
+    Xs, ys = ht.datasets.iris(synthetic=True)
+    assert Xs.shape == (150, 4) and np.bincount(ys.numpy()).tolist() == [50, 50, 50]
+
+
+def test_dataset_fixtures():
+    """The reference fixtures (when a Heat checkout or $HEAT_DATASETS_DIR provides them) load through
+    every format with the same values, on every split axis; iris() / diabetes() return them."""
+    import numpy as np
+    import pytest
+    import heat_amd as ht
+
+    if ht.datasets.fixture_path("iris.csv") is None:
+        pytest.skip("reference fixtures not available")
+    ref = np.loadtxt(ht.datasets.fixture_path("iris.csv"), delimiter=";", dtype=np.float32)
+    assert ref.shape == (150, 4)
+    for name in ("iris.csv", "iris.h5", "iris.nc"):
+        for split in (None, 0, 1):
+            a = ht.datasets.load_fixture(name, split=split)
+            assert a.split == split and a.shape == (150, 4)
+            np.testing.assert_allclose(a.numpy(), ref, rtol=1e-6)
+    X, y = ht.datasets.iris(split=0)
+    np.testing.assert_allclose(X.numpy(), ref, rtol=1e-6)
+    # Fisher's iris: class means of petal length are ~1.46 / 4.26 / 5.55 (rows ordered by class)
+    pl = ref[:, 2].reshape(3, 50).mean(1)
+    np.testing.assert_allclose(pl, [1.46, 4.26, 5.55], atol=5e-3)
+    Xd, yd = ht.datasets.diabetes(split=0)
+    assert Xd.shape == (442, 11) and yd.shape[0] == 442
+    assert np.allclose(Xd.numpy()[:, 0], 1.0) or Xd.numpy().std(0).min() >= 0
+    train = ht.datasets.load_fixture("iris_X_train.csv", split=0)
+    assert train.shape == (75, 4)
+    with pytest.raises(FileNotFoundError):
+        ht.datasets.load_fixture("no_such_fixture.csv")
