@@ -551,3 +551,35 @@ def check_qr_complete_without_gather():
             k = min(m, n)
             assert (np.diagonal(R)[:k] >= -1e-7).all()
             assert q.split == (0 if s == 0 else 1) and r.split == s
+
+
+def check_kmeans_bit_reproducible():
+    """Two fits with the same seed give bit-identical centroids, labels and inertia on every rank
+    (the deterministic update: no float atomics, fixed-order partial sums), the centroids are the
+    same on all ranks, and the labels are the nearest centroids (NumPy fp64 check, ties aside).
+    k = 40 takes the MFMA assignment + counting-sort update on a GPU, k = 8 the fused small-k step."""
+    import torch
+
+    rng = np.random.default_rng(21)
+    centres = rng.standard_normal((40, 16)) * 6
+    pts = (centres[rng.integers(0, 40, 6000)] + rng.standard_normal((6000, 16))).astype(np.float32)
+    for k in (40, 8):
+        runs = []
+        for _ in range(2):
+            X = ht.array(pts, split=0)
+            km = ht.cluster.KMeans(n_clusters=k, init="random", max_iter=12, tol=None, random_state=5)
+            km.fit(X)
+            runs.append((km.cluster_centers_.larray.clone(), km.labels_.larray.clone(), float(km.inertia_)))
+        (c0, l0, i0), (c1, l1, i1) = runs
+        assert torch.equal(c0, c1), (k, (c0 - c1).abs().max())
+        assert torch.equal(l0, l1) and i0 == i1
+        # replicated centroids: identical bits on every rank
+        gathered = X.comm.allgather_tensor(c0.reshape(1, -1).contiguous(), 0)
+        assert all(torch.equal(gathered[0], g) for g in gathered)
+        # labels_ belong to the last assignment (against the centroids before the final update,
+        # as in the reference); predict() assigns against the final ones
+        lab = km.predict(X).numpy().reshape(-1)
+        c = km.cluster_centers_.numpy().astype(np.float64)
+        d = ((pts.astype(np.float64)[:, None, :] - c[None]) ** 2).sum(-1)
+        best = d.min(1)
+        assert np.all(d[np.arange(len(pts)), lab] <= best * (1 + 1e-5) + 1e-4)
