@@ -1,0 +1,179 @@
+"""
+Randomised differential checks: seeded random cases (the same on every rank), each a random shape,
+dtype and split axis, against NumPy. Where ``dist_checks`` pins every operation on hand-picked
+data, these sweep the layout space - uneven blocks, split extents smaller than the world (empty
+ranks), length-1 axes, negative axes, keepdims - the way the reference's ``assert_func_equal``
+draws random arrays for every split (``heat/core/tests/test_suites/basic_test.py:142-306``).
+
+Run in a world of one (``test_core_local.py``), at 2-8 gloo ranks and host-staged
+(``test_distributed.py``), and with device buffers on the GPU (``test_gpu_dist.py``).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import heat_amd as ht
+
+from .dist_checks import assert_array_equal
+
+N_CASES = 12
+
+
+def _cases(seed, n=N_CASES, max_ndim=3, max_extent=7, float_only=False):
+    """(numpy array, split) pairs: random ndim 1..max_ndim, extents 1..max_extent, dtype, split."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        nd = int(rng.integers(1, max_ndim + 1))
+        shape = tuple(int(v) for v in rng.integers(1, max_extent + 1, nd))
+        kind = "f" if float_only else rng.choice(["f", "d", "i"])
+        if kind == "i":
+            a = rng.integers(-20, 20, shape).astype(np.int64)
+        else:
+            a = rng.standard_normal(shape).astype(np.float32 if kind == "f" else np.float64)
+        split = None if rng.random() < 0.2 else int(rng.integers(0, nd))
+        out.append((a, split))
+    return out, rng
+
+
+def _tol(a):
+    return (1e-4, 1e-5) if a.dtype == np.float32 else (1e-9, 1e-10)
+
+
+def check_random_elementwise():
+    cases, rng = _cases(101)
+    for a, split in cases:
+        x = ht.array(a, split=split)
+        rt, at = _tol(a)
+        b = rng.standard_normal(a.shape[-1:]).astype(a.dtype) if a.dtype.kind == "f" else \
+            rng.integers(1, 5, a.shape[-1:]).astype(a.dtype)
+        y = ht.array(b)  # replicated, broadcast along the last axis
+        assert_array_equal(x + y, a + b, rtol=rt, atol=at)
+        assert_array_equal(x * y - x, a * b - a, rtol=rt, atol=at)
+        assert_array_equal(ht.abs(x), np.abs(a), rtol=rt, atol=at)
+        assert_array_equal(x > 0, a > 0)
+        assert_array_equal(ht.where(x > 0, x, 0), np.where(a > 0, a, 0), rtol=rt, atol=at)
+        if a.dtype.kind == "f":
+            assert_array_equal(ht.exp(ht.clip(x, -3, 3)), np.exp(np.clip(a, -3, 3)), rtol=rt, atol=at)
+            assert_array_equal(ht.sqrt(ht.abs(x)), np.sqrt(np.abs(a)), rtol=rt, atol=at)
+        else:
+            assert_array_equal(x // 3, a // 3)
+            assert_array_equal(x % 4, a % 4)
+
+
+def check_random_reductions():
+    cases, rng = _cases(202)
+    for a, split in cases:
+        x = ht.array(a, split=split)
+        rt, at = _tol(a)
+        rt, at = rt * 10, at * 10
+        ax = int(rng.integers(-a.ndim, a.ndim))
+        keep = bool(rng.random() < 0.5)
+        assert_array_equal(ht.sum(x, axis=ax, keepdim=keep), a.sum(axis=ax, keepdims=keep), rtol=rt, atol=at,
+                           check_split_chunks=False)
+        assert_array_equal(ht.max(x, axis=ax, keepdim=keep), a.max(axis=ax, keepdims=keep), check_split_chunks=False)
+        assert_array_equal(ht.min(x, axis=ax), a.min(axis=ax), check_split_chunks=False)
+        assert_array_equal(ht.argmax(x, axis=ax), a.argmax(axis=ax), check_split_chunks=False)
+        assert_array_equal(ht.argmin(x, axis=ax), a.argmin(axis=ax), check_split_chunks=False)
+        if a.dtype.kind == "f":
+            assert_array_equal(ht.mean(x, axis=ax), a.mean(axis=ax), rtol=rt, atol=at, check_split_chunks=False)
+            if a.shape[ax] > 1:
+                assert_array_equal(ht.var(x, axis=ax, ddof=1), a.var(axis=ax, ddof=1), rtol=rt * 10, atol=at * 10,
+                                   check_split_chunks=False)
+            assert abs(float(ht.mean(x)) - float(a.mean())) <= 1e-4 * (1 + abs(float(a.mean())))
+        assert abs(float(ht.sum(x)) - float(a.sum())) <= 1e-3 * (1 + float(np.abs(a).sum()))
+
+
+def check_random_manipulations():
+    cases, rng = _cases(303)
+    for a, split in cases:
+        x = ht.array(a, split=split)
+        perm = tuple(int(v) for v in rng.permutation(a.ndim))
+        assert_array_equal(ht.transpose(x, perm), np.transpose(a, perm), check_split_chunks=False)
+        ax = int(rng.integers(0, a.ndim))
+        assert_array_equal(ht.flip(x, ax), np.flip(a, ax), check_split_chunks=False)
+        sh = int(rng.integers(-5, 6))
+        assert_array_equal(ht.roll(x, sh, ax), np.roll(a, sh, ax), check_split_chunks=False)
+        assert_array_equal(ht.concatenate([x, x], axis=ax), np.concatenate([a, a], axis=ax), check_split_chunks=False)
+        # the split must name an axis of the new shape (reference reshape: new_split defaults to
+        # the old split and is sanitised against the new shape)
+        ns = None if split is None else 0
+        flat = ht.reshape(x, (-1,), new_split=ns)
+        assert_array_equal(flat, a.reshape(-1), check_split_chunks=False)
+        n = a.size
+        div = [d for d in range(1, n + 1) if n % d == 0]
+        d = int(rng.choice(div))
+        ns = None if split is None else int(rng.integers(0, 2))
+        r2 = ht.reshape(x, (d, n // d), new_split=ns)
+        assert r2.split == ns
+        assert_array_equal(r2, a.reshape(d, n // d))
+        srt = ht.sort(x, axis=ax)[0]
+        assert_array_equal(srt, np.sort(a, axis=ax, kind="stable"), check_split_chunks=False)
+        assert_array_equal(ht.expand_dims(x, 0), a[None], check_split_chunks=False)
+        if split is not None:
+            new = int(rng.integers(0, a.ndim))
+            r = ht.resplit(x, new)
+            assert r.split == new
+            assert_array_equal(r, a)
+
+
+def check_random_indexing():
+    cases, rng = _cases(404)
+    for a, split in cases:
+        x = ht.array(a, split=split)
+        key = []
+        for s in a.shape:
+            lo = int(rng.integers(0, s))
+            hi = int(rng.integers(lo, s + 1))
+            step = int(rng.integers(1, 3))
+            key.append(slice(lo, hi, step))
+        key = tuple(key)
+        assert_array_equal(x[key], a[key], check_split_chunks=False)
+        i = int(rng.integers(-a.shape[0], a.shape[0]))
+        assert_array_equal(x[i], a[i], check_split_chunks=False)
+        mask = a > 0
+        got = x[ht.array(mask, split=split)]
+        assert_array_equal(got, a[mask], check_split_chunks=False)
+        idx = rng.integers(0, a.shape[0], 4)
+        assert_array_equal(x[ht.array(idx)], a[idx], check_split_chunks=False)
+        # owner-computes assignment of a broadcast value into a slice
+        y = x.copy()
+        b = a.copy()
+        y[key] = 7
+        b[key] = 7
+        assert_array_equal(y, b)
+
+
+def check_random_linalg_matmul():
+    rng = np.random.default_rng(505)
+    for _ in range(8):
+        m, k, n = (int(v) for v in rng.integers(1, 9, 3))
+        a = rng.standard_normal((m, k))
+        b = rng.standard_normal((k, n))
+        for sa in (None, 0, 1):
+            sb = [None, 0, 1][int(rng.integers(0, 3))]
+            c = ht.matmul(ht.array(a, split=sa), ht.array(b, split=sb))
+            assert_array_equal(c, a @ b, rtol=1e-9, atol=1e-9, check_split_chunks=False)
+        t = ht.array(a, split=int(rng.integers(0, 2)))
+        assert_array_equal(ht.linalg.transpose(t), a.T, check_split_chunks=False)
+        if m >= k:
+            q, r = ht.linalg.qr(ht.array(a, split=0), mode="reduced")
+            qn, rn = q.numpy(), r.numpy()
+            assert qn.shape == (m, k) and rn.shape == (k, k)
+            assert np.allclose(qn @ rn, a, atol=1e-8)
+            assert np.allclose(qn.T @ qn, np.eye(k), atol=1e-8)
+
+
+def check_random_statistics():
+    cases, rng = _cases(606, float_only=True)
+    for a, split in cases:
+        x = ht.array(a, split=split)
+        ax = int(rng.integers(0, a.ndim))
+        q = float(rng.uniform(0, 100))
+        assert_array_equal(ht.percentile(x, q, axis=ax), np.percentile(a, q, axis=ax), rtol=1e-5, atol=1e-5,
+                           check_split_chunks=False)
+        assert_array_equal(ht.median(x, axis=ax), np.median(a, axis=ax), rtol=1e-5, atol=1e-5,
+                           check_split_chunks=False)
+        assert_array_equal(ht.cumsum(x, axis=ax), np.cumsum(a, axis=ax), rtol=1e-4, atol=1e-4,
+                           check_split_chunks=False)
+        assert_array_equal(ht.std(x, axis=ax), np.std(a, axis=ax), rtol=1e-4, atol=1e-5, check_split_chunks=False)
