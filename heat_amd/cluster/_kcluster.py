@@ -39,17 +39,17 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         # "exact": bit-exact fp32 (f32-input MFMA) assignment
         self.precision = "fast"
         self._pack_cache = None
-        # certified one-term assignment (ops.kmeans_assign(certified=True)) while it pays: a
+        # certified one-term assignment (ops.kmeans_assign(certified=True)) while it pays: every
         # certified call posts its re-check count to the host (pinned copy + event); the next call
         # waits for that event (the previous iteration, normally finished) and decides. Once more
-        # than CERT_MAX_RECHECK of the points needed the 3-term re-run, the full kernel takes over
-        # until the points change; while it pays, it is re-checked every CERT_REPROBE calls.
+        # than CERT_MAX_RECHECK of the points needed the 3-term re-run (the filter costs ~55 % of
+        # the full kernel, the re-run of a fraction q about q of it), the full kernel takes over
+        # until the points change.
         self._certify = True
         self._cert_probe = None
         self._cert_calls = 0
 
-    CERT_MAX_RECHECK = 0.25
-    CERT_REPROBE = 8
+    CERT_MAX_RECHECK = 0.35
 
     def _assign_labels(self, X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
         """int32 nearest-centroid labels of the local points (native fused kernels)."""
@@ -66,7 +66,7 @@ class _KCluster(ClusteringMixin, BaseEstimator):
         certified = packed is not None and self._certify
         labels, _ = ops.kmeans_assign(X, C, want_mind=False, packed=packed, certified=certified)
         self._cert_calls += 1
-        if certified and X.shape[0] > 0 and (self._cert_calls <= 2 or self._cert_calls % self.CERT_REPROBE == 0):
+        if certified and X.shape[0] > 0:
             host = torch.empty(1, dtype=torch.int32, pin_memory=True)
             host.copy_(ops.kernels.kmeans_assign.last_rechecked.reshape(1), non_blocking=True)  # unwrapped by profiling
             ev = torch.cuda.Event()

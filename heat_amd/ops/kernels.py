@@ -153,12 +153,14 @@ def kmeans_assign(X: torch.Tensor, C: torch.Tensor, want_mind: bool = True,
         ws = torch.empty(L.ha_h3_workspace_bytes(k, f), dtype=torch.uint8, device=X.device)
         labels = torch.empty(n, dtype=torch.int32, device=X.device)
         if certified and not want_mind:
-            amb = torch.empty(n + 1, dtype=torch.int32, device=X.device)
+            # uncertain-point lists (one per shard of the filter's workgroups) + their counts
+            cap = L.ha_h3_amb_rows(n)
+            amb = torch.empty(cap + L.ha_h3_amb_shards(), dtype=torch.int32, device=X.device)
             rc = L.ha_h3_assign_certified(_ptr(packed.planes), _ptr(packed.sx), n, f, _ptr(Cc), k, Cc.stride(0),
-                                          _ptr(ws), _ptr(labels), _ptr(amb), _ptr(amb[n:]),
+                                          _ptr(ws), _ptr(labels), _ptr(amb), _ptr(amb[cap:]),
                                           ctypes.c_void_p(stream_ptr(X.device)))
             check(rc, "ha_h3_assign_certified")
-            kmeans_assign.last_rechecked = amb[n]
+            kmeans_assign.last_rechecked = amb[cap:].sum(dtype=torch.int32)
             return labels, None
         mind = torch.empty(n, dtype=torch.float32, device=X.device) if want_mind else None
         phases = L.ha_h3r_phases(k, f)

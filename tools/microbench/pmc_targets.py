@@ -1,0 +1,46 @@
+"""Short, fixed workloads for rocprofv3 --pmc passes (one pass per counter group, see
+tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up and run 3 times.
+  kmeans  - one Lloyd step, k = 1024, 1.25e7 x 64 (h3_assign_p + deterministic update)
+  moments - mean of 1e9 fp32, axis None / 0 / 1 (moments.hip, one kernel per call)
+  gemm    - ht.matmul 8192^3 fp32 at precision highest (gemm_f32t) and high (gemm_h3t)
+  cdist   - one 32768 x 32768 x 128 distance tile (cdist_f16x3.hip)"""
+import sys
+
+import torch
+
+import heat_amd as ht
+from heat_amd import ops
+
+
+def main():
+    which = sys.argv[1]
+    ht.use_device("gpu")
+    ht.random.seed(11)
+    if which == "kmeans":
+        x = ht.random.randn(12_500_000, 64, split=0)
+        km = ht.cluster.KMeans(n_clusters=1024, init="random", max_iter=1, tol=None, random_state=3)
+        for _ in range(5):
+            km.step(x)
+    elif which == "moments":
+        x = ht.random.rand(1_000_000, 1000, split=0)
+        for axis in (None, 0, 1):
+            for _ in range(3):
+                ht.mean(x, axis=axis)
+    elif which == "gemm":
+        a = torch.randn(8192, 8192, device="cuda")
+        b = torch.randn(8192, 8192, device="cuda")
+        A, B = ht.array(a, split=0), ht.array(b)
+        for prec in ("highest", "high"):
+            torch.set_float32_matmul_precision(prec)
+            for _ in range(3):
+                ht.matmul(A, B)
+    elif which == "cdist":
+        x = torch.rand(32768, 128, device="cuda")
+        for _ in range(3):
+            ops.cdist(x, x)
+    torch.cuda.synchronize()
+    print("done", which)
+
+
+if __name__ == "__main__":
+    main()
