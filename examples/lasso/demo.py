@@ -1,6 +1,7 @@
 """
 Lasso demo (reference ``examples/lasso/demo.py``): regularisation path of coordinate-descent
-Lasso on the (synthetic) diabetes data; prints the coefficients per lambda.
+Lasso on the diabetes data (the reference fixture when available, else a synthetic stand-in);
+prints the coefficients per lambda.
 
     python -m heat_amd.run -n 2 examples/lasso/demo.py
 """

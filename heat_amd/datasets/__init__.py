@@ -106,12 +106,13 @@ def write_iris_csv(path: str, seed: int = 0, sep: str = ";") -> str:
 
 def diabetes(split: Optional[int] = 0, device=None, comm=None, seed: int = 0,
              synthetic: bool = False) -> Tuple[DNDarray, DNDarray]:
-    """442 x 11 features (first column = 1 for the Lasso intercept) and targets: the reference's
-    ``diabetes.h5`` (datasets ``x`` and ``y``) when available, else a synthetic problem."""
+    """442 x 11 features (first column = 1 for the Lasso intercept) and a (442, 1) target column:
+    the reference's ``diabetes.h5`` (datasets ``x`` and ``y``) when available, else a synthetic
+    problem of the same layout (442 x 10)."""
     if not synthetic and fixture_path("diabetes.h5") is not None:
         X = load_fixture("diabetes.h5", "x", split=split, device=device, comm=comm)
-        y = load_fixture("diabetes.h5", "y", split=split, device=device, comm=comm)
-        return X, y
+        y = load_fixture("diabetes.h5", "y", split=split if split in (None, 0) else None, device=device, comm=comm)
+        return X, ht.reshape(y, (-1, 1), new_split=y.split)
     X, y = make_regression(442, 10, noise=0.5, seed=seed, as_numpy=True)
     X[:, 0] = 1.0
     return ht.array(X, split=split, device=device, comm=comm), ht.array(y, split=split, device=device, comm=comm)

@@ -11,6 +11,8 @@
 
 namespace {
 
+constexpr int LASSO_SLOTS = 4;  // partial[0] result, [1] arrival counter, then one slot per block
+
 __global__ __launch_bounds__(256) void lasso_pass(const float* __restrict__ xt, int64_t m, int64_t ldxt, int jprev,
                                                   int jnext, const float* __restrict__ delta, float* __restrict__ r,
                                                   float* __restrict__ partial) {
@@ -51,11 +53,37 @@ __global__ __launch_bounds__(256) void lasso_pass(const float* __restrict__ xt, 
     if (xn) acc = fmaf(xn[i], rv, acc);
   }
   if (xn) {
+    // deterministic dot product: the block's sum goes to its own slot (written through, sc1) and
+    // the last-arriving block adds the slots in block order (a float atomicAdd made theta depend
+    // on the arrival order of the blocks); partial[0] = result, partial[1] = arrival counter
     acc = ha_wave_sum(acc);
     __shared__ float sh[4];
+    __shared__ bool last;
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(partial, sh[0] + sh[1] + sh[2] + sh[3]);
+    if (threadIdx.x == 0) {
+      const float b = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+      __hip_atomic_store((ha_gu32*)(partial + LASSO_SLOTS + blockIdx.x), __float_as_uint(b), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add((ha_gu32*)(partial + 1), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      last = t == gridDim.x - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((ha_gu32*)(partial + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    if (!last) return;
+    float t = 0.f;
+    for (unsigned q = threadIdx.x; q < gridDim.x; q += blockDim.x) t += partial[LASSO_SLOTS + q];
+    t = ha_wave_sum(t);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[0] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
   }
 }
 
@@ -69,7 +97,6 @@ __global__ void lasso_update(float* __restrict__ theta, int j, float* __restrict
   else nw = rho < -lam ? rho + lam : (rho > lam ? rho - lam : 0.f);
   theta[j] = nw;
   *delta = nw - old;
-  partial[0] = 0.f;
 }
 
 // Fit preparation in one pass over X (row-major [m][n]): XT = X^T (feature-major, the layout of
@@ -78,7 +105,7 @@ __global__ void lasso_update(float* __restrict__ theta, int j, float* __restrict
 // Replaces torch's transpose copy + (XT*XT).sum(1), which took 4 ms of a 5 ms sweep at 1e7 x 16.
 __global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
                                                      float* __restrict__ xt, int64_t ldxt,
-                                                     float* __restrict__ colsq) {
+                                                     float* __restrict__ colpart) {
   __shared__ float tile[64][65];
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
@@ -114,7 +141,7 @@ __global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x
     }
     __syncthreads();
   }
-  if (ty == 0 && c0 + tx < n) atomicAdd(&colsq[c0 + tx], sq);
+  if (ty == 0 && c0 + tx < n) colpart[(int64_t)blockIdx.x * n + c0 + tx] = sq;
 }
 
 // Narrow X (n <= 64 features, e.g. 16): one row per thread. A thread loads its whole row (16-byte
@@ -125,7 +152,7 @@ __global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x
 template <int NC, bool VEC>
 __global__ __launch_bounds__(256) void lasso_prepare_rows(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
                                                           float* __restrict__ xt, int64_t ldxt,
-                                                          float* __restrict__ colsq) {
+                                                          float* __restrict__ colpart) {
   __shared__ float red[4][NC];
   float sq[NC];
 #pragma unroll
@@ -162,16 +189,28 @@ __global__ __launch_bounds__(256) void lasso_prepare_rows(const float* __restric
   __syncthreads();
   if (threadIdx.x < n) {
     const int j = threadIdx.x;
-    atomicAdd(&colsq[j], (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]));
+    colpart[(int64_t)blockIdx.x * n + j] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
   }
+}
+
+// colsq[j] = sum over the B workgroup partials colpart[b][j] in a fixed order (one workgroup per
+// column: strided per-thread sums, then wave butterflies and the 4 wave sums in order)
+__global__ __launch_bounds__(256) void lasso_colsq(const float* __restrict__ colpart, int64_t B, int n,
+                                                   float* __restrict__ colsq) {
+  __shared__ float sh[4];
+  const int j = blockIdx.x;
+  float t = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 256) t += colpart[b * n + j];
+  t = ha_wave_sum(t);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) colsq[j] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
 }  // namespace
 
-HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, float* xt, int64_t ldxt, float* colsq,
-                               void* stream) {
-  if (m <= 0 || n <= 0) return HA_OK;
-  hipMemsetAsync(colsq, 0, sizeof(float) * (size_t)n, (hipStream_t)stream);
+// Workgroups of ha_lasso_prepare for (m, n): its colpart scratch holds blocks * n floats.
+static int64_t lasso_prepare_blocks(int64_t m, int n) {
   if (n <= 64) {
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -179,15 +218,31 @@ HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, fl
       ncu = 256;
     int64_t blocks = (m + 255) / 256;
     if (blocks > 8LL * ncu) blocks = 8LL * ncu;
+    return blocks < 1 ? 1 : blocks;
+  }
+  return (m + 255) / 256;
+}
+
+HA_EXPORT int64_t ha_lasso_prepare_scratch(int64_t m, int n) {
+  return m <= 0 || n <= 0 ? 1 : lasso_prepare_blocks(m, n) * (int64_t)n;
+}
+
+// XT = X^T and colsq[j] = sum_i X[i][j]^2 (fixed-order, bit-reproducible); colpart: scratch of
+// ha_lasso_prepare_scratch(m, n) floats.
+HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, float* xt, int64_t ldxt, float* colsq,
+                               float* colpart, void* stream) {
+  if (m <= 0 || n <= 0) return HA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t blocks = lasso_prepare_blocks(m, n);
+  if (n <= 64) {
     const bool vec = n % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
-    hipStream_t s = (hipStream_t)stream;
 #define HA_LP(NC)                                                                                           \
   if (vec)                                                                                                  \
     hipLaunchKernelGGL((lasso_prepare_rows<NC, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, m, n, ldx, xt, \
-                       ldxt, colsq);                                                                        \
+                       ldxt, colpart);                                                                      \
   else                                                                                                      \
     hipLaunchKernelGGL((lasso_prepare_rows<NC, false>), dim3((unsigned)blocks), dim3(256), 0, s, x, m, n, ldx, xt, \
-                       ldxt, colsq);
+                       ldxt, colpart);
     if (n <= 16) {
       HA_LP(16)
     } else if (n <= 32) {
@@ -196,14 +251,18 @@ HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, fl
       HA_LP(64)
     }
 #undef HA_LP
-    return ha_launch_status();
+  } else {
+    if (blocks > 0x7fffffffLL || (n + 63) / 64 > 65535) return HA_UNSUPPORTED;
+    hipLaunchKernelGGL(lasso_prepare, dim3((unsigned)blocks, (unsigned)((n + 63) / 64)), dim3(256), 0, s, x, m, n,
+                       ldx, xt, ldxt, colpart);
   }
-  const int64_t gx = (m + 255) / 256;
-  if (gx > 0x7fffffffLL || (n + 63) / 64 > 65535) return HA_UNSUPPORTED;
-  hipLaunchKernelGGL(lasso_prepare, dim3((unsigned)gx, (unsigned)((n + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
-                     x, m, n, ldx, xt, ldxt, colsq);
+  hipLaunchKernelGGL(lasso_colsq, dim3((unsigned)n), dim3(256), 0, s, colpart, blocks, n, colsq);
   return ha_launch_status();
 }
+
+// Floats of ha_lasso_pass's partial buffer: result, arrival counter (zero before the first pass,
+// reset by every pass), padding, one slot per workgroup.
+HA_EXPORT int64_t ha_lasso_partial_floats(int num_cus) { return LASSO_SLOTS + (int64_t)num_cus * 4; }
 
 HA_EXPORT int ha_lasso_pass(const float* xt, int64_t m, int64_t ldxt, int jprev, int jnext, const float* delta,
                             float* r, float* partial, int num_cus, void* stream) {

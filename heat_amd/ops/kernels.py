@@ -308,8 +308,11 @@ _MOM_COUNTERS = {}
 
 
 def _mom_counters(device, n: int) -> torch.Tensor:
-    """Zeroed arrival counters of the fused moments epilogue (the kernels reset what they use)."""
-    key = device.index if device.index is not None else torch.cuda.current_device()
+    """Zeroed arrival counters of the fused moments epilogue (the kernels reset what they use).
+    One set per (device, stream): launches on one stream run in order, so a set is never shared by
+    two kernels in flight."""
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    key = (dev, stream_ptr(device))
     c = _MOM_COUNTERS.get(key)
     if c is None or c.numel() < n:
         c = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
@@ -654,10 +657,12 @@ def lasso_prepare(X: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """(X^T contiguous [n, m], sum of squares per column [n]) in one pass over X."""
     m, n = X.shape
     if use_native(X) and X.dtype == torch.float32 and X.stride(-1) == 1:
+        L = lib()
         XT = torch.empty((n, m), dtype=torch.float32, device=X.device)
         colsq = torch.empty(n, dtype=torch.float32, device=X.device)
-        check(lib().ha_lasso_prepare(_ptr(X), m, n, X.stride(0), _ptr(XT), XT.stride(0), _ptr(colsq),
-                                     ctypes.c_void_p(stream_ptr(X.device))), "ha_lasso_prepare")
+        colpart = torch.empty(max(1, L.ha_lasso_prepare_scratch(m, n)), dtype=torch.float32, device=X.device)
+        check(L.ha_lasso_prepare(_ptr(X), m, n, X.stride(0), _ptr(XT), XT.stride(0), _ptr(colsq), _ptr(colpart),
+                                 ctypes.c_void_p(stream_ptr(X.device))), "ha_lasso_prepare")
         return XT, colsq
     XT = X.t().contiguous()
     return XT, (XT * XT).sum(1)
@@ -710,14 +715,15 @@ def lasso_epoch(XT: torch.Tensor, r: torch.Tensor, theta: torch.Tensor, colsq: t
     if use_native(XT) and XT.dtype == torch.float32:
         L = lib()
         s = ctypes.c_void_p(stream_ptr(XT.device))
-        partial = torch.zeros(1, dtype=torch.float32, device=XT.device)
-        delta = torch.zeros(1, dtype=torch.float32, device=XT.device)
         ncu = num_cus(XT.device)
+        # [result, arrival counter (zero), pad, per-workgroup slots]: deterministic dot products
+        partial = torch.zeros(L.ha_lasso_partial_floats(ncu), dtype=torch.float32, device=XT.device)
+        delta = torch.zeros(1, dtype=torch.float32, device=XT.device)
         for j in range(n):
             check(L.ha_lasso_pass(_ptr(XT), m, XT.stride(0), j - 1, j, _ptr(delta), _ptr(r), _ptr(partial), ncu, s),
                   "ha_lasso_pass")
             if allreduce is not None:
-                allreduce(partial)
+                allreduce(partial[:1])
             check(L.ha_lasso_update(_ptr(theta), j, _ptr(partial), _ptr(colsq), ctypes.c_float(lam),
                                     ctypes.c_float(inv_m), _ptr(delta), 1 if j == 0 else 0, s), "ha_lasso_update")
         # apply the last coordinate's change to the residual

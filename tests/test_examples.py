@@ -65,7 +65,7 @@ def test_dataset_fixtures():
     pl = ref[:, 2].reshape(3, 50).mean(1)
     np.testing.assert_allclose(pl, [1.46, 4.26, 5.55], atol=5e-3)
     Xd, yd = ht.datasets.diabetes(split=0)
-    assert Xd.shape == (442, 11) and yd.shape[0] == 442
+    assert Xd.shape == (442, 11) and yd.shape == (442, 1)
     assert np.allclose(Xd.numpy()[:, 0], 1.0) or Xd.numpy().std(0).min() >= 0
     train = ht.datasets.load_fixture("iris_X_train.csv", split=0)
     assert train.shape == (75, 4)

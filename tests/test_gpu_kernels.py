@@ -559,7 +559,29 @@ def test_lasso_graph_replay_matches_eager(gpu, monkeypatch):
         est = ht.regression.Lasso(lam=0.01, max_iter=20, tol=None)
         est.fit(x, y)
         res.append(est.theta.larray.clone())
-    assert torch.allclose(res[0], res[1], atol=1e-5)
+    assert torch.equal(res[0], res[1]), (res[0] - res[1]).abs().max()
+
+
+@pytest.mark.parametrize("n", [12, 90])
+def test_lasso_sweep_bit_reproducible(gpu, monkeypatch, n):
+    """The sweep solver's dot products and column norms are summed in a fixed order (per-workgroup
+    slots, last-arriving block / one workgroup per column): repeated fits give identical bits."""
+    import heat_amd as ht
+    from heat_amd import ops
+
+    ht.random.seed(9)
+    x = ht.random.randn(300_001, n)
+    y = ht.matmul(x, ht.random.randn(n, 1)) + 0.05 * ht.random.randn(300_001, 1)
+    monkeypatch.setenv("HEAT_LASSO_SOLVER", "sweep")
+    res = []
+    for _ in range(3):
+        est = ht.regression.Lasso(lam=0.01, max_iter=5, tol=None)
+        est.fit(x, y)
+        res.append(est.theta.larray.clone())
+    assert torch.equal(res[0], res[1]) and torch.equal(res[1], res[2])
+    XT, colsq = ops.lasso_prepare(x.larray)
+    for _ in range(3):
+        assert torch.equal(ops.lasso_prepare(x.larray)[1], colsq)
 
 
 @pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 512, 768), (4099, 130, 65), (64, 4096, 64),
