@@ -16,15 +16,14 @@
 //
 // Layout: A row-major (lda), rows of this rank = global rows [g0, g0 + m). 8 lanes own one row (4
 // consecutive panel columns each: 16- or 32-byte accesses, a row segment per 8 lanes), 32 rows per
-// 256-thread block, grid-stride over the rows; block partial sums go through LDS and one atomicAdd
-// per column per block.
+// 256-thread block, grid-stride over the rows; block partial sums go through LDS, then a
+// fixed-order two-level sum (hh_block_sum) - no float atomics, bit-reproducible.
 #include "common.h"
 
 namespace {
 
 constexpr int HH_NB = 32;     // panel width (8 lanes x 4 columns)
-constexpr int HH_COPIES = 32; // replicated S accumulators: block b adds into copy b % 32, so the
-                              // fp64 atomics of the ~2 blocks/CU spread over 32x the addresses
+constexpr int HH_COPIES = 32; // S accumulator copies: copy g = the fixed-order sum of block group g
 constexpr int HH_SLEN = 2 * HH_NB;  // one copy: S[NB] | rowd[NB]
 
 template <typename T>
@@ -59,8 +58,14 @@ __device__ __forceinline__ void hh_store4(T* p, const Vec4<T>& r, int ncols_here
 }
 
 // Block-reduce the per-lane partials acc[4] (columns 4 q .. 4 q + 3, q = lane % 8) over the 32
-// row groups of the block, then one atomicAdd per column into out[0 .. NB).
-__device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __restrict__ out, double* red) {
+// row groups of the block, then a FIXED-ORDER tree instead of float atomics (whose arrival order
+// made the factorization differ run to run in the last bits): the block's column sums go to its
+// own slot of `part` (write-through), the blocks form HH_COPIES groups of consecutive blocks, and
+// the last-arriving block of each group (ticket on cnt[group], reset by it) adds its group's slots
+// in block order into accumulator copy `group` of out; hh_gather_s then adds the copies in order.
+__device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __restrict__ out, double* red,
+                                             double* __restrict__ part, unsigned* __restrict__ cnt) {
+  __shared__ bool last;
   const int tid = threadIdx.x, q = tid & 7, grp = tid >> 3;
 #pragma unroll
   for (int i = 0; i < 4; ++i) red[grp * HH_NB + 4 * q + i] = acc[i];
@@ -68,7 +73,28 @@ __device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __r
   if (tid < HH_NB) {
     double s = 0.0;
     for (int g = 0; g < 32; ++g) s += red[g * HH_NB + tid];
-    if (s != 0.0) atomicAdd(out + (blockIdx.x % HH_COPIES) * HH_SLEN + tid, s);
+    ha_store_wt(part + (int64_t)blockIdx.x * HH_NB + tid, s);
+  }
+  const int gb = (gridDim.x + HH_COPIES - 1) / HH_COPIES;  // blocks per group
+  const int group = blockIdx.x / gb;
+  const int b0 = group * gb, b1 = b0 + gb < (int)gridDim.x ? b0 + gb : (int)gridDim.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add((ha_gu32*)(cnt + group), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (unsigned)(b1 - b0 - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store((ha_gu32*)(cnt + group), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (last && tid < HH_NB) {
+    double s = 0.0;
+    for (int b = b0; b < b1; ++b) s += part[(int64_t)b * HH_NB + tid];
+    out[group * HH_SLEN + tid] = s;
   }
   __syncthreads();
 }
@@ -87,7 +113,8 @@ __device__ __forceinline__ void hh_gather_s(const double* __restrict__ S, double
 // S / rowd of the first column of a panel: S[c] = sum_{g >= d} A[g][0] A[g][c], rowd = row d.
 template <typename T>
 __global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64_t m, int64_t lda, int64_t g0,
-                                                  int64_t k0, int ncols, int64_t d, double* __restrict__ S) {
+                                                  int64_t k0, int ncols, int64_t d, double* __restrict__ S,
+                                                  double* __restrict__ part, unsigned* __restrict__ cnt) {
   __shared__ double red[32 * HH_NB];
   const int q = threadIdx.x & 7;
   const int nh = ncols - 4 * q < 4 ? (ncols - 4 * q > 0 ? ncols - 4 * q : 0) : 4;
@@ -102,10 +129,10 @@ __global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64
     if (g == d) {
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        if (c < nh) atomicAdd(S + HH_NB + 4 * q + c, (double)a.v[c]);
+        if (c < nh) S[HH_NB + 4 * q + c] = (double)a.v[c];  // row d: exactly one writer
     }
   }
-  hh_block_sum(acc, S, red);
+  hh_block_sum(acc, S, red, part, cnt);
 }
 
 // One panel column: apply reflector j (from Sin) to this rank's rows, store v / R, accumulate the
@@ -113,7 +140,8 @@ __global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64
 template <typename T>
 __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int64_t lda, int64_t g0, int64_t k0,
                                                int ncols, int j, const double* __restrict__ Sin,
-                                               double* __restrict__ Sout, T* __restrict__ tau) {
+                                               double* __restrict__ Sout, T* __restrict__ tau,
+                                               double* __restrict__ part, unsigned* __restrict__ cnt) {
   __shared__ double red[32 * HH_NB];
   __shared__ double sin_[HH_SLEN];
   hh_gather_s(Sin, sin_);
@@ -176,11 +204,11 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
       if (g == d + 1) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if (c < nh) atomicAdd(Sout + HH_NB + 4 * q + c, (double)a.v[c]);
+          if (c < nh) Sout[HH_NB + 4 * q + c] = (double)a.v[c];  // row d + 1: one writer
       }
     }
   }
-  if (Sout) hh_block_sum(acc, Sout, red);
+  if (Sout) hh_block_sum(acc, Sout, red, part, cnt);
 }
 
 // larft: T (nb x nb, upper triangular, row-major, ldt = nb) of the compact WY form
@@ -215,8 +243,8 @@ __global__ __launch_bounds__(64) void hh_larft(const double* __restrict__ Y, con
 // orthogonality - and rocBLAS's fp64 GEMM is slow on these tall-skinny shapes. Block = 256
 // columns of C x a row slice (split-K over blockIdx.y); thread (jl = t % 64, c-group = t / 64)
 // owns W rows 8 cg .. 8 cg + 7 of columns jl + 64 u (u < 4): every V value read from LDS feeds 4
-// fp64 FMAs. V rows are staged through LDS 64 at a time (broadcast reads); partials land by fp64
-// atomicAdd.
+// fp64 FMAs. V rows are staged through LDS 64 at a time (broadcast reads); per-split partials are
+// summed in split order by hh_vtc_sum.
 template <typename T>
 __global__ __launch_bounds__(256) void hh_vtc(const T* __restrict__ V, int64_t ldv, const T* __restrict__ C,
                                               int64_t ldc, int64_t m, int64_t N, int nc, int64_t rows_per_split,
@@ -298,36 +326,40 @@ int hh_grid(int64_t m) {
 HA_EXPORT int ha_hh_nb() { return HH_NB; }
 // doubles per S buffer (HH_COPIES replicated accumulators of S[NB] | rowd[NB])
 HA_EXPORT int ha_hh_slen() { return HH_COPIES * HH_SLEN; }
+// doubles of the per-block partial slots of ha_hh_colsums / ha_hh_step for m local rows, and the
+// number of (zeroed, self-resetting) group counters
+HA_EXPORT int64_t ha_hh_part_len(int64_t m) { return (int64_t)hh_grid(m) * HH_NB; }
+HA_EXPORT int ha_hh_counters() { return HH_COPIES; }
 
 // S (2 NB doubles, zeroed by the caller) += column-0 sums of the panel at column k0 (ncols <= NB
 // columns) over this rank's rows g >= d, and row d's values if this rank owns it.
 HA_EXPORT int ha_hh_colsums(const void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols,
-                            int64_t d, double* S, void* stream) {
+                            int64_t d, double* S, double* part, unsigned* cnt, void* stream) {
   if (ncols <= 0 || ncols > HH_NB || m < 0) return HA_BAD_ARG;
   if (m == 0) return HA_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 0)
     hipLaunchKernelGGL(hh_colsums<float>, dim3(hh_grid(m)), dim3(256), 0, s, (const float*)A, m, lda, g0, k0, ncols,
-                       d, S);
+                       d, S, part, cnt);
   else
     hipLaunchKernelGGL(hh_colsums<double>, dim3(hh_grid(m)), dim3(256), 0, s, (const double*)A, m, lda, g0, k0, ncols,
-                       d, S);
+                       d, S, part, cnt);
   return ha_launch_status();
 }
 
 // Reflector j of the panel (see the header); Sout (zeroed, 2 NB doubles) receives column j + 1's
 // partial sums unless it is null.
 HA_EXPORT int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols, int j,
-                         const double* Sin, double* Sout, void* tau, void* stream) {
+                         const double* Sin, double* Sout, void* tau, double* part, unsigned* cnt, void* stream) {
   if (ncols <= 0 || ncols > HH_NB || j < 0 || j >= ncols || m < 0) return HA_BAD_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int grid = hh_grid(m);
   if (dtype == 0)
     hipLaunchKernelGGL(hh_step<float>, dim3(grid), dim3(256), 0, s, (float*)A, m, lda, g0, k0, ncols, j, Sin, Sout,
-                       (float*)tau);
+                       (float*)tau, part, cnt);
   else
     hipLaunchKernelGGL(hh_step<double>, dim3(grid), dim3(256), 0, s, (double*)A, m, lda, g0, k0, ncols, j, Sin, Sout,
-                       (double*)tau);
+                       (double*)tau, part, cnt);
   return ha_launch_status();
 }
 

@@ -585,7 +585,7 @@ __global__ __launch_bounds__(256) void ku_gather_det(const float* __restrict__ X
     };
     auto row = [&](int idx) {
       const float* src = X + (int64_t)idx * ldx + col;
-      if (VEC) return *reinterpret_cast<const floatx4*>(src);
+      if (VEC) return __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(src));  // streamed once
       floatx4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = col + q < f ? src[q] : 0.f;

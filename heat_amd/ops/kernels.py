@@ -1308,6 +1308,10 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
     st = ctypes.c_void_p(stream_ptr(dev)) if native else None
     red = allreduce or (lambda t: t)
     rows = torch.arange(g0, g0 + m_r, device=dev).unsqueeze(1)
+    if native:
+        # per-block partial slots + self-resetting group counters of the fixed-order panel sums
+        hpart = torch.empty(max(1, L.ha_hh_part_len(m_r)), dtype=torch.float64, device=dev)
+        hcnt = torch.zeros(L.ha_hh_counters(), dtype=torch.int32, device=dev)
     panels = []
     for K0 in range(0, kmax, outer):
         ncol = min(outer, kmax - K0)
@@ -1317,8 +1321,8 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
             S = torch.zeros((nc + 1, slen), dtype=torch.float64, device=dev)
             tau = torch.empty(nc, dtype=dt, device=dev)
             if native:
-                check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), st),
-                      "ha_hh_colsums")
+                check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), _ptr(hpart),
+                                      _ptr(hcnt), st), "ha_hh_colsums")
             else:
                 _hh_colsums_host(A, rows, k0, nc, S[0])
             red(S[0])
@@ -1326,7 +1330,8 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
                 last = j + 1 == nc
                 if native:
                     check(L.ha_hh_step(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, j, _ptr(S[j]),
-                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), st), "ha_hh_step")
+                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), _ptr(hpart), _ptr(hcnt),
+                                       st), "ha_hh_step")
                 else:
                     _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau)
                 if not last:
