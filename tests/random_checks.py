@@ -177,3 +177,83 @@ def check_random_statistics():
         assert_array_equal(ht.cumsum(x, axis=ax), np.cumsum(a, axis=ax), rtol=1e-4, atol=1e-4,
                            check_split_chunks=False)
         assert_array_equal(ht.std(x, axis=ax), np.std(a, axis=ax), rtol=1e-4, atol=1e-5, check_split_chunks=False)
+
+
+def _tmpdir():
+    import tempfile
+
+    comm = ht.MPI_WORLD
+    return comm.bcast(tempfile.mkdtemp() if comm.rank == 0 else None, root=0)
+
+
+def check_random_io_roundtrips():
+    """Random shapes / dtypes written from one split and read back into another, through the
+    built-in HDF5 writer (contiguous, and chunked with random chunk shapes + deflate / shuffle /
+    fletcher32 filters), NetCDF, .npy and CSV - every rank writes its slab in parallel."""
+    import os
+
+    comm = ht.MPI_WORLD
+    d = _tmpdir()
+    rng = np.random.default_rng(707)
+    for case in range(8):
+        nd = int(rng.integers(1, 4))
+        shape = tuple(int(v) for v in rng.integers(1, 9, nd))
+        kind = rng.choice(["f", "d", "i"])
+        a = (rng.standard_normal(shape) * 10).astype({"f": np.float32, "d": np.float64, "i": np.int32}[kind])
+        if kind == "i":
+            a = rng.integers(-1000, 1000, shape).astype(np.int32)
+        ws = None if rng.random() < 0.25 else int(rng.integers(0, nd))
+        rs = None if rng.random() < 0.25 else int(rng.integers(0, nd))
+        x = ht.array(a, split=ws)
+        h5 = os.path.join(d, "r{}.h5".format(case))
+        ht.save_hdf5(x, h5, "plain")
+        kw = {"chunks": tuple(int(rng.integers(1, s + 1)) for s in shape)}
+        if rng.random() < 0.7:
+            kw["compression"] = "gzip"
+            kw["compression_opts"] = int(rng.integers(1, 10))
+        kw["shuffle"] = bool(rng.random() < 0.5)
+        kw["fletcher32"] = bool(rng.random() < 0.5)
+        ht.save_hdf5(x, h5, "chunked", mode="a", **kw)
+        for name in ("plain", "chunked"):
+            y = ht.load_hdf5(h5, name, dtype=x.dtype, split=rs)
+            assert y.split == rs and y.dtype == x.dtype, (name, y.split, y.dtype)
+            assert_array_equal(y, a)
+        nc = os.path.join(d, "r{}.nc".format(case))
+        ht.save(x, nc, "v")
+        assert_array_equal(ht.load(nc, "v", dtype=x.dtype, split=rs), a)
+        npy = os.path.join(d, "r{}.npy".format(case))
+        ht.save(x, npy)
+        assert_array_equal(ht.load(npy, split=rs), a)
+        if nd == 2 and kind != "i":
+            csv = os.path.join(d, "r{}.csv".format(case))
+            ht.save_csv(x, csv, decimals=9)
+            got = ht.load_csv(csv, dtype=ht.float64, split=rs if rs in (None, 0) else 0)
+            assert_array_equal(got, a.astype(np.float64), rtol=1e-5, atol=1e-5)
+    comm.Barrier()
+
+
+def check_random_resplit_chain():
+    """A random chain of resplits / balances / redistributions keeps values and the chunking rule."""
+    rng = np.random.default_rng(808)
+    for _ in range(6):
+        nd = int(rng.integers(1, 4))
+        shape = tuple(int(v) for v in rng.integers(1, 10, nd))
+        a = rng.standard_normal(shape)
+        x = ht.array(a, split=int(rng.integers(0, nd)))
+        for _ in range(4):
+            op = rng.choice(["resplit", "balance", "unbalance", "none"])
+            if op == "resplit":
+                x = ht.resplit(x, None if rng.random() < 0.2 else int(rng.integers(0, nd)))
+            elif op == "balance" and x.split is not None:
+                x = x.balance()
+            elif op == "unbalance" and x.split is not None and x.shape[x.split] > 1:
+                # slicing along the split axis leaves the blocks unbalanced (not rebalanced)
+                k = int(rng.integers(1, x.shape[x.split] + 1))
+                key = [slice(None)] * nd
+                key[x.split] = slice(0, k)
+                x = x[tuple(key)]
+                sl = [slice(None)] * nd
+                sl[x.split] = slice(0, k)
+                a = a[tuple(sl)]
+            assert_array_equal(x, a, check_split_chunks=bool(x.balanced))
+        assert abs(float(ht.sum(x)) - float(a.sum())) < 1e-8 * (1 + np.abs(a).sum())
