@@ -100,8 +100,8 @@ __global__ void lasso_update(float* __restrict__ theta, int j, float* __restrict
 }
 
 // Fit preparation in one pass over X (row-major [m][n]): XT = X^T (feature-major, the layout of
-// lasso_pass) and colsq[j] += sum_i X[i][j]^2.  64 x 64 tiles through LDS (+1 padding), 256 rows
-// per workgroup along m; the column sums go out with one float atomic per (workgroup, column).
+// lasso_pass) and the per-workgroup column sums of squares.  64 x 64 tiles through LDS (+1
+// padding), workgroups striding over 64-row bands; lasso_colsq adds the partials in order.
 // Replaces torch's transpose copy + (XT*XT).sum(1), which took 4 ms of a 5 ms sweep at 1e7 x 16.
 __global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x, int64_t m, int n, int64_t ldx,
                                                      float* __restrict__ xt, int64_t ldxt,
@@ -110,9 +110,9 @@ __global__ __launch_bounds__(256) void lasso_prepare(const float* __restrict__ x
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
   float sq = 0.f;                                          // column c0 + tx (thread rows ty = 0 only)
-  for (int sub = 0; sub < 4; ++sub) {
-    const int64_t r0 = ((int64_t)blockIdx.x * 4 + sub) * 64;
-    if (r0 >= m) break;
+  // grid-stride over 64-row bands (bounded grid: the column partials are gridDim.x x n floats)
+  for (int64_t band = blockIdx.x; band * 64 < m; band += gridDim.x) {
+    const int64_t r0 = band * 64;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int rr = ty * 16 + i;
@@ -220,7 +220,8 @@ static int64_t lasso_prepare_blocks(int64_t m, int n) {
     if (blocks > 8LL * ncu) blocks = 8LL * ncu;
     return blocks < 1 ? 1 : blocks;
   }
-  return (m + 255) / 256;
+  const int64_t bands = (m + 63) / 64;
+  return bands < 2048 ? bands : 2048;
 }
 
 HA_EXPORT int64_t ha_lasso_prepare_scratch(int64_t m, int n) {
@@ -252,7 +253,7 @@ HA_EXPORT int ha_lasso_prepare(const float* x, int64_t m, int n, int64_t ldx, fl
     }
 #undef HA_LP
   } else {
-    if (blocks > 0x7fffffffLL || (n + 63) / 64 > 65535) return HA_UNSUPPORTED;
+    if ((n + 63) / 64 > 65535) return HA_UNSUPPORTED;
     hipLaunchKernelGGL(lasso_prepare, dim3((unsigned)blocks, (unsigned)((n + 63) / 64)), dim3(256), 0, s, x, m, n,
                        ldx, xt, ldxt, colpart);
   }
