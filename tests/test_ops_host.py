@@ -90,3 +90,83 @@ def test_lasso_gram_blocked_matches_fp64():
         A = torch.cat([X, y[:, None]], 1).double()
         ref = A.T @ A
         assert torch.allclose(_gram_blocked(X, y), ref, rtol=0, atol=1e-6 * ref.abs().max().item())
+
+
+# ---- C ABI workspace contracts of the fused / fixed-order kernels (host functions of the library;
+# the GPU tests exercise the kernels that rely on them)
+def _lib():
+    import pytest
+
+    try:
+        return ops.lib()
+    except Exception as e:  # pragma: no cover - library not built
+        pytest.skip("native library unavailable: {}".format(e))
+
+
+def _group(n):
+    g = 1
+    while g * g < n:
+        g += 1
+    return g
+
+
+def test_moments_workspace_contracts():
+    import ctypes
+
+    L = _lib()
+    pd, nc = ctypes.c_int64(), ctypes.c_int64()
+    for nrows in (1, 3, 1000):
+        for nchunks in (1, 2, 17, 1024, 4096, 65536):
+            L.ha_moments_rows_workspace(nrows, nchunks, ctypes.byref(pd), ctypes.byref(nc))
+            g = _group(nchunks)
+            ngroups = (nchunks + g - 1) // g
+            assert g <= 256 and ngroups <= 256          # one partial per thread at each tree level
+            if nchunks == 1:
+                assert pd.value == nrows * 3 and nc.value == 0
+            else:
+                assert pd.value == nrows * (nchunks + ngroups) * 3
+                assert nc.value == nrows * (ngroups + 1)
+    for ncols in (1, 4, 1000, 4097):
+        for nchunks in (1, 5, 256, 65535):
+            L.ha_moments_cols_workspace(ncols, nchunks, ctypes.byref(pd), ctypes.byref(nc))
+            g = _group(nchunks)
+            ngroups = (nchunks + g - 1) // g
+            extra = ngroups if nchunks > 1 else 0
+            assert pd.value == (nchunks + extra) * ncols * 3
+            assert nc.value == ((ncols + 255) // 256) * (ngroups + 1)
+
+
+def test_certified_assignment_list_capacity():
+    """Every filter workgroup (256 points) appends to list blockIdx % shards: a list must hold the
+    points of ceil(workgroups / shards) workgroups, and all lists together at least n."""
+    L = _lib()
+    shards = L.ha_h3_amb_shards()
+    assert shards >= 1
+    for n in (1, 255, 256, 257, 4096, 12_500_000, 100_000_007):
+        total = L.ha_h3_amb_rows(n)
+        assert total % shards == 0
+        cap = total // shards
+        wgs = (n + 255) // 256
+        assert cap >= -(-wgs // shards) * 256 and total >= n
+
+
+def test_lasso_scratch_contracts():
+    L = _lib()
+    for m, n in ((1, 1), (1000, 3), (10_000_000, 16), (4_000_000, 256), (300, 1024)):
+        s = L.ha_lasso_prepare_scratch(m, n)
+        assert s >= n and s % n == 0                    # whole per-workgroup column partials
+        assert s // n <= max(2048, 8 * 256)             # bounded grid, whatever m
+    for ncu in (1, 80, 256, 304):
+        assert L.ha_lasso_partial_floats(ncu) >= 4 + 4 * ncu   # result, counter, pad, one slot/block
+
+
+def test_householder_partial_contracts():
+    L = _lib()
+    nb, copies = L.ha_hh_nb(), L.ha_hh_counters()
+    assert L.ha_hh_slen() == copies * 2 * nb
+    for m in (1, 31, 32, 33, 1000, 1_250_000, 10**8):
+        part = L.ha_hh_part_len(m)
+        blocks = part // nb
+        assert part % nb == 0 and 1 <= blocks <= max(1, -(-m // 32))
+        gb = -(-blocks // copies)                       # blocks per group of the fixed-order tree
+        assert -(-blocks // gb) <= copies               # every group has an accumulator copy
