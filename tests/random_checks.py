@@ -257,3 +257,57 @@ def check_random_resplit_chain():
                 a = a[tuple(sl)]
             assert_array_equal(x, a, check_split_chunks=bool(x.balanced))
         assert abs(float(ht.sum(x)) - float(a.sum())) < 1e-8 * (1 + np.abs(a).sum())
+
+
+def check_random_linalg_misc():
+    """norms, dot / vecdot / outer, trace, tril / triu, cov on random layouts."""
+    rng = np.random.default_rng(909)
+    for _ in range(8):
+        m, n = (int(v) for v in rng.integers(1, 9, 2))
+        a = rng.standard_normal((m, n))
+        s = None if rng.random() < 0.25 else int(rng.integers(0, 2))
+        x = ht.array(a, split=s)
+        assert abs(float(ht.linalg.norm(x)) - np.linalg.norm(a)) < 1e-10 * (1 + np.linalg.norm(a))
+        assert_array_equal(ht.linalg.vector_norm(x, axis=1), np.linalg.norm(a, axis=1), rtol=1e-10, atol=1e-12,
+                           check_split_chunks=False)
+        assert_array_equal(ht.linalg.vector_norm(x, axis=0, ord=1), np.abs(a).sum(0), rtol=1e-10, atol=1e-12,
+                           check_split_chunks=False)
+        assert abs(float(ht.linalg.matrix_norm(x, ord="fro")) - np.linalg.norm(a, "fro")) < 1e-9
+        assert abs(float(ht.linalg.matrix_norm(x, ord=1)) - np.linalg.norm(a, 1)) < 1e-9 * (1 + np.abs(a).sum())
+        k = int(rng.integers(-3, 4))
+        assert_array_equal(ht.tril(x, k), np.tril(a, k), check_split_chunks=False)
+        assert_array_equal(ht.triu(x, k), np.triu(a, k), check_split_chunks=False)
+        assert abs(float(ht.trace(x)) - np.trace(a)) < 1e-10 * (1 + np.abs(a).sum())
+        u = rng.standard_normal(m)
+        v = rng.standard_normal(n)
+        su = None if rng.random() < 0.3 else 0
+        sv = None if rng.random() < 0.3 else 0
+        assert_array_equal(ht.outer(ht.array(u, split=su), ht.array(v, split=sv)), np.outer(u, v), rtol=1e-12,
+                           atol=1e-12, check_split_chunks=False)
+        assert abs(float(ht.dot(ht.array(u, split=su), ht.array(u, split=su))) - u @ u) < 1e-10 * (1 + u @ u)
+        if m > 1 and n > 1:
+            assert_array_equal(ht.cov(ht.array(a.T.copy(), split=s)), np.cov(a.T), rtol=1e-8, atol=1e-10,
+                               check_split_chunks=False)
+
+
+def check_random_logical_and_sets():
+    """any / all / isclose / allclose / unique / nonzero on random layouts (incl. empty results)."""
+    cases, rng = _cases(1010)
+    for a, split in cases:
+        x = ht.array(a, split=split)
+        ax = int(rng.integers(0, a.ndim))
+        thr = float(rng.uniform(-1.5, 1.5))
+        assert bool(ht.any(x > thr)) == bool(np.any(a > thr))
+        assert bool(ht.all(x > thr)) == bool(np.all(a > thr))
+        assert_array_equal(ht.any(x > thr, axis=ax), np.any(a > thr, axis=ax), check_split_chunks=False)
+        assert_array_equal(ht.all(x > thr, axis=ax), np.all(a > thr, axis=ax), check_split_chunks=False)
+        b = a + (1e-9 if a.dtype.kind == "f" else 0)
+        assert bool(ht.allclose(x, ht.array(b, split=split)))
+        assert_array_equal(ht.isclose(x, ht.array(b, split=split)), np.isclose(a, b), check_split_chunks=False)
+        r = np.round(a).astype(np.int64)
+        u = ht.unique(ht.array(r, split=split), sorted=True)
+        assert_array_equal(u, np.unique(r), check_split_chunks=False)
+        nz = ht.nonzero(x > thr)
+        ref = np.stack(np.nonzero(a > thr), axis=1) if a.ndim > 1 else np.nonzero(a > thr)[0][:, None]
+        got = nz.numpy().reshape(-1, a.ndim) if a.ndim > 1 else nz.numpy().reshape(-1, 1)
+        assert got.shape == ref.shape and np.array_equal(got, ref), (got, ref)
