@@ -334,6 +334,61 @@ def test_moments_fused_final(shape, axis, final):
         assert torch.equal(mu.float(), r)
 
 
+def test_moments_concurrent_streams():
+    """Fused moments on two streams at once: each (device, stream) has its own arrival counters,
+    so the two kernels' ticket trees never share a word."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    xs = [(torch.randn(3_000_000, generator=g) * (i + 1) + 10 * i).to(dev) for i in range(2)]
+    ys = [(torch.randn(20_000, 300, generator=g) + i).to(dev) for i in range(2)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    res = [None, None]
+    for _ in range(5):
+        for i, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                res[i] = (ops.moments(xs[i], None, "var"), ops.moments(ys[i], 0, "mean"))
+        torch.cuda.synchronize()
+        for i in range(2):
+            assert abs(res[i][0].item() - xs[i].double().var(correction=0).item()) < 1e-5 * (1 + (i + 1) ** 2)
+            assert torch.allclose(res[i][1].double(), ys[i].double().mean(0), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("rows,length,ld", [(5000, 1021, 1024), (777, 7, 8), (64, 1024, 1024), (3, 5, 12)])
+@pytest.mark.parametrize("kind", [1, 2, 3])
+def test_moments_short_rows_padded_stride(rows, length, ld, kind):
+    """The short-row pipeline (a few workgroups per CU, next row in flight, register mean shift)
+    on rows of `length` inside a padded row stride `ld` (16-byte aligned rows, scalar tail of
+    length % 4 elements) through the C ABI directly: mean / var / std against fp64."""
+    import ctypes
+
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(rows + length)
+    buf = (torch.randn(rows, ld, generator=g) * 2 + 50).to(dev)
+    x = buf[:, :length]
+    out = torch.empty(rows, dtype=torch.float32, device=dev)
+    part = torch.empty(rows * 3, dtype=torch.float64, device=dev)
+    L = ops.lib()
+    st = ctypes.c_void_p(ops.stream_ptr(dev))
+    ops.check(L.ha_moments_rows(K._ptr(buf), rows, length, ld, 1, K._ptr(part), K._ptr(out), kind, 0.0, None, st),
+              "ha_moments_rows")
+    xd = x.double()
+    ref = {1: xd.mean(1), 2: xd.var(1, correction=0), 3: xd.var(1, correction=0).sqrt()}[kind]
+    assert torch.allclose(out.double(), ref, rtol=2e-6, atol=1e-6), (out.double() - ref).abs().max()
+    # triples (kind 0) of the same rows
+    trip = torch.empty(rows, 3, dtype=torch.float64, device=dev)
+    ops.check(L.ha_moments_rows(K._ptr(buf), rows, length, ld, 1, K._ptr(part), K._ptr(trip), 0, 0.0, None, st),
+              "ha_moments_rows")
+    assert torch.all(trip[:, 0] == length)
+    assert torch.allclose(trip[:, 1], xd.mean(1), rtol=1e-9, atol=1e-9)
+    assert torch.allclose(trip[:, 2] / length, xd.var(1, correction=0), rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("shape,axis", [((4_000_000, 64), 0), ((64, 4_000_000), None), ((2000, 3000), 0)])
 def test_moments_handoff_fresh_each_call(shape, axis):
     """The fused epilogue hands partials between blocks with write-through stores and a ticket
