@@ -1,6 +1,6 @@
 """Short, fixed workloads for rocprofv3 --pmc passes (one pass per counter group, see
 tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up and run 3 times.
-  kmeans  - one Lloyd step, k = 1024, 1.25e7 x 64 (h3_assign_p + deterministic update)
+  kmeans  - 8 Lloyd steps, k = 1024, 1.25e7 x 64 (h3_assign_p + deterministic update)
   moments - mean of 1e9 fp32, axis None / 0 / 1 (moments.hip, one kernel per call)
   gemm    - ht.matmul 8192^3 fp32 at precision highest (gemm_f32t) and high (gemm_h3t)
   cdist   - one 32768 x 32768 x 128 distance tile (cdist_f16x3.hip)"""
@@ -19,7 +19,7 @@ def main():
     if which == "kmeans":
         x = ht.random.randn(12_500_000, 64, split=0)
         km = ht.cluster.KMeans(n_clusters=1024, init="random", max_iter=1, tol=None, random_state=3)
-        for _ in range(5):
+        for _ in range(8):  # the first steps probe the certified filter, then the full kernel runs
             km.step(x)
     elif which == "moments":
         x = ht.random.rand(1_000_000, 1000, split=0)
