@@ -605,7 +605,9 @@ def percentile(x: DNDarray, q, axis: Optional[int] = None, out: Optional[DNDarra
         split = None
     else:
         t = src.larray.to(tdt)
-        qt = torch.tensor(qv, dtype=tdt, device=t.device) / 100.0
+        # q / 100 on the host: a device division by a scalar is a multiply by its reciprocal, which
+        # moves e.g. 95 / 100 one ulp up and flips "nearest" at a half position (28.5 -> 29 for n = 31)
+        qt = torch.tensor([v / 100.0 for v in qv], dtype=tdt, device=t.device)
         r = torch.quantile(t, qt, dim=ax, interpolation=interpolation) if t.numel() else \
             torch.empty((len(qv),) + tuple(s for i, s in enumerate(t.shape) if i != ax), dtype=tdt, device=t.device)
         split = None
