@@ -14,6 +14,9 @@ seeded random problems, for every split the estimator accepts.
   labels equal sklearn's ``KMeans(algorithm="lloyd", n_init=1)``.
 * cdist / rbf / manhattan: ``scipy.spatial.distance.cdist`` on every split pairing.
 * skew / kurtosis / percentile / cov: ``scipy.stats`` and NumPy, biased and unbiased.
+* KMedians / KMedoids: a NumPy transcription of the reference's L1 Lloyd iteration.
+* GaussianNB (fit, weighted fit, partial_fit, probabilities) and KNN votes: sklearn.
+* float32 inputs (the native kernels' dtype on the GPU) at fp32 tolerances.
 
 Run in a world of one (``test_core_local.py``) and at 2-8 gloo ranks (``test_distributed.py``).
 """
@@ -178,3 +181,150 @@ def check_oracle_cov_numpy():
             xt = ht.array(a.T.copy(), split=split)
             assert_array_equal(ht.cov(xt, rowvar=False), np.cov(a.T, rowvar=False), rtol=1e-10, atol=1e-12)
             assert_array_equal(ht.cov(x, ht.array(b, split=split)), np.cov(a, b), rtol=1e-10, atol=1e-12)
+
+
+def _l1_lloyd(X, C, iters, medoids):
+    """NumPy k-medians / k-medoids (the reference's algorithm, ``heat/cluster/kmedians.py:57-100``,
+    ``kmedoids.py:56-114``): L1 assignment, per-cluster coordinate median; k-medoids then moves each
+    centre to the sample closest (L1) to that median. Stops when the centres stop moving."""
+    C = C.copy()
+    for _ in range(iters):
+        lab = np.abs(X[:, None, :] - C[None, :, :]).sum(-1).argmin(1)
+        new = C.copy()
+        for i in range(len(C)):
+            pts = X[lab == i]
+            if len(pts) == 0:
+                continue
+            med = np.median(pts, axis=0)
+            new[i] = X[np.abs(X - med).sum(1).argmin()] if medoids else med
+        if np.array_equal(new, C):
+            break
+        C = new
+    return C, np.abs(X[:, None, :] - C[None, :, :]).sum(-1).argmin(1)
+
+
+def check_oracle_kmedians_kmedoids_numpy():
+    for seed, (k, f, per) in enumerate([(3, 2, 30), (5, 4, 21)]):
+        X, rng = _blobs(100 + seed, k, f, per, spread=1.0)
+        init = X[rng.choice(len(X), k, replace=False)]
+        for est_cls, medoids in ((ht.cluster.KMedians, False), (ht.cluster.KMedoids, True)):
+            for iters in (1, 2, 30):
+                C_ref, lab_ref = _l1_lloyd(X, init, iters, medoids)
+                for split in (None, 0):
+                    kw = {} if medoids else {"tol": None}     # KMedoids has no tol (reference API)
+                    est = est_cls(n_clusters=k, init=ht.array(init), max_iter=iters, **kw)
+                    est.fit(ht.array(X, split=split))
+                    np.testing.assert_allclose(est.cluster_centers_.numpy(), C_ref, rtol=1e-12, atol=1e-12,
+                                               err_msg="{} seed {} iters {} split {}".format(
+                                                   est_cls.__name__, seed, iters, split))
+                    np.testing.assert_array_equal(est.predict(ht.array(X, split=split)).numpy().ravel(), lab_ref)
+
+
+def _nb_var(nb):
+    """Per-class variances (``sigma_``, the reference's name; sklearn >= 1.0 calls them ``var_``)."""
+    return (nb.var_ if hasattr(nb, "var_") else nb.sigma_).numpy()
+
+
+def check_oracle_gaussian_nb_sklearn():
+    """fp64 GaussianNB against sklearn to round-off: one-shot fit, incremental ``partial_fit`` over
+    three batches (the reference's chunked mean/variance merge), sample weights, probabilities."""
+    from sklearn.naive_bayes import GaussianNB as SkNB
+
+    rng = np.random.default_rng(21)
+    X = np.concatenate([rng.normal(c, 1.0 + 0.2 * i, (35 + 3 * i, 4)) for i, c in enumerate((-2.0, 0.5, 2.5))])
+    y = np.repeat(np.arange(3), [35, 38, 41])
+    p = rng.permutation(len(y))
+    X, y = X[p], y[p]
+    w = rng.uniform(0.5, 2.0, len(y))
+    sk = SkNB().fit(X, y)
+    skw = SkNB().fit(X, y, sample_weight=w)
+    skp = SkNB()
+    for part in np.array_split(np.arange(len(y)), 3):
+        skp.partial_fit(X[part], y[part], classes=np.arange(3))
+    for split in (None, 0):
+        hx, hy = ht.array(X, split=split), ht.array(y, split=split)
+        nb = ht.naive_bayes.GaussianNB().fit(hx, hy)
+        np.testing.assert_allclose(nb.theta_.numpy(), sk.theta_, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(_nb_var(nb), sk.var_, rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(nb.class_prior_.numpy(), sk.class_prior_, rtol=1e-12)
+        np.testing.assert_array_equal(nb.predict(hx).numpy().ravel(), sk.predict(X))
+        np.testing.assert_allclose(nb.predict_proba(hx).numpy(), sk.predict_proba(X), rtol=1e-8, atol=1e-12)
+        np.testing.assert_allclose(nb.predict_log_proba(hx).numpy(), sk.predict_log_proba(X), rtol=1e-8, atol=1e-8)
+        nbw = ht.naive_bayes.GaussianNB().fit(hx, hy, sample_weight=ht.array(w, split=split))
+        np.testing.assert_allclose(nbw.theta_.numpy(), skw.theta_, rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(_nb_var(nbw), skw.var_, rtol=1e-10, atol=1e-12)
+        nbp = ht.naive_bayes.GaussianNB()
+        for part in np.array_split(np.arange(len(y)), 3):
+            nbp.partial_fit(ht.array(X[part], split=split), ht.array(y[part], split=split),
+                            classes=ht.array(np.arange(3)))
+        np.testing.assert_allclose(nbp.theta_.numpy(), skp.theta_, rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(_nb_var(nbp), skp.var_, rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(nbp.class_count_.numpy(), skp.class_count_)
+
+
+def check_oracle_knn_sklearn():
+    """fp64 k-nearest-neighbour votes equal sklearn's on continuous data (no distance ties) for
+    odd k and two classes (no vote ties), every split of the training and query sets."""
+    from sklearn.neighbors import KNeighborsClassifier as SkKNN
+
+    rng = np.random.default_rng(22)
+    X = np.concatenate([rng.normal(0.0, 1.0, (40, 3)), rng.normal(1.2, 1.0, (45, 3))])
+    y = np.repeat([0, 1], [40, 45])
+    Q = rng.normal(0.6, 1.3, (33, 3))
+    for k in (1, 5, 9):
+        ref = SkKNN(n_neighbors=k).fit(X, y).predict(Q)
+        for sx in (None, 0):
+            for sq in (None, 0):
+                knn = ht.classification.KNeighborsClassifier(n_neighbors=k)
+                knn.fit(ht.array(X, split=sx), ht.array(y, split=sx))
+                np.testing.assert_array_equal(knn.predict(ht.array(Q, split=sq)).numpy().ravel(), ref)
+
+
+def check_oracle_fp32_paths():
+    """float32 inputs - the dtype the native MFMA / VALU kernels take on the GPU - against fp64
+    library results, at fp32 tolerances: Lloyd from a fixed init on well-separated blobs (labels
+    exact), the exact and expanded distance kernels, both Lasso solvers, mean / var / std."""
+    from scipy.spatial.distance import cdist as sp_cdist
+    from sklearn.cluster import KMeans as SkKMeans
+    from sklearn.linear_model import Lasso as SkLasso
+
+    X, rng = _blobs(31, 6, 8, 50, spread=0.4)
+    init = X[rng.choice(len(X), 6, replace=False)]
+    sk = SkKMeans(n_clusters=6, init=init, n_init=1, max_iter=20, tol=0.0, algorithm="lloyd").fit(X)
+    X32 = X.astype(np.float32)
+    for split in (None, 0):
+        km = ht.cluster.KMeans(n_clusters=6, init=ht.array(init.astype(np.float32)), max_iter=20, tol=None)
+        km.fit(ht.array(X32, split=split))
+        np.testing.assert_allclose(km.cluster_centers_.numpy(), sk.cluster_centers_, rtol=2e-5, atol=2e-5)
+        np.testing.assert_array_equal(km.predict(ht.array(X32, split=split)).numpy().ravel(), sk.labels_)
+
+    a = rng.standard_normal((70, 19)).astype(np.float32)
+    b = rng.standard_normal((45, 19)).astype(np.float32)
+    d = sp_cdist(a.astype(np.float64), b.astype(np.float64))
+    for split in (None, 0):
+        A, B = ht.array(a, split=split), ht.array(b)
+        assert_array_equal(ht.spatial.cdist(A, B), d, rtol=1e-5, atol=1e-5)
+        assert_array_equal(ht.spatial.cdist(A, B, quadratic_expansion=True), d, rtol=1e-4, atol=1e-4)
+        assert_array_equal(ht.spatial.manhattan(A, B), sp_cdist(a.astype(np.float64), b.astype(np.float64),
+                                                                "cityblock"), rtol=1e-5, atol=1e-5)
+
+    Xa, y = _lasso_problem(32, 400, 10)
+    ref = SkLasso(alpha=0.05, tol=1e-14, max_iter=200000).fit(Xa[:, 1:], y)
+    ref = np.concatenate([[ref.intercept_], ref.coef_])
+    for solver in ("gram", "sweep"):
+        for split in (None, 0):
+            with _env("HEAT_LASSO_SOLVER", solver):
+                est = ht.regression.Lasso(lam=0.05, max_iter=2000, tol=1e-7)
+                est.fit(ht.array(Xa.astype(np.float32), split=split), ht.array(y.astype(np.float32), split=split))
+            np.testing.assert_allclose(est.theta.numpy().ravel(), ref, rtol=1e-4, atol=1e-4)
+
+    m = rng.gamma(2.0, 1.0, (300, 17)).astype(np.float32)
+    for split in (None, 0, 1):
+        x = ht.array(m, split=split)
+        for axis in (None, 0, 1):
+            assert_array_equal(ht.mean(x, axis=axis), np.asarray(m.astype(np.float64).mean(axis=axis)),
+                               rtol=1e-5, atol=1e-6)
+            assert_array_equal(ht.var(x, axis=axis, ddof=1), np.asarray(m.astype(np.float64).var(axis=axis, ddof=1)),
+                               rtol=1e-4, atol=1e-6)
+            assert_array_equal(ht.std(x, axis=axis), np.asarray(m.astype(np.float64).std(axis=axis)),
+                               rtol=1e-4, atol=1e-6)
