@@ -328,3 +328,53 @@ def check_oracle_fp32_paths():
                                rtol=1e-4, atol=1e-6)
             assert_array_equal(ht.std(x, axis=axis), np.asarray(m.astype(np.float64).std(axis=axis)),
                                rtol=1e-4, atol=1e-6)
+
+
+def check_oracle_linalg_numpy():
+    """fp64 linear algebra against NumPy/SciPy for every split: matmul (all 9 split pairings),
+    QR (R up to row signs, Q orthonormal), singular values, vector / matrix norms of every order,
+    conjugate gradients on an SPD system, and Lanczos (T = V^T A V, orthonormal V)."""
+    import scipy.linalg as sla
+
+    rng = np.random.default_rng(41)
+    a = rng.standard_normal((23, 7))
+    b = rng.standard_normal((7, 11))
+    for sa in (None, 0, 1):
+        for sb in (None, 0, 1):
+            assert_array_equal(ht.matmul(ht.array(a, split=sa), ht.array(b, split=sb)), a @ b, rtol=1e-10, atol=1e-10)
+    for split in (None, 0, 1):
+        x = ht.array(a, split=split)
+        q, r = ht.linalg.qr(x, mode="reduced")
+        rn = np.linalg.qr(a, mode="r")
+        sgn = np.sign(np.diag(r.numpy())) * np.sign(np.diag(rn))
+        np.testing.assert_allclose(r.numpy(), sgn[:, None] * rn, rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(q.numpy().T @ q.numpy(), np.eye(7), atol=1e-10)
+        np.testing.assert_allclose(q.numpy() @ r.numpy(), a, atol=1e-10)
+        s = ht.linalg.svd(x, compute_uv=False)
+        np.testing.assert_allclose(s.numpy(), np.linalg.svd(a, compute_uv=False), rtol=1e-10, atol=1e-10)
+        for ordv in (None, "fro", "nuc", 1, -1, 2, -2, np.inf, -np.inf):
+            assert_array_equal(ht.linalg.matrix_norm(x, ord=ordv), np.asarray(np.linalg.norm(a, ord=ordv)),
+                               rtol=1e-9, atol=1e-10)
+    v = rng.standard_normal(29)
+    for split in (None, 0):
+        xv = ht.array(v, split=split)
+        for ordv in (None, 0, 1, 2, 3, np.inf, -np.inf, 0.5):
+            assert_array_equal(ht.linalg.vector_norm(xv, ord=ordv), np.asarray(np.linalg.norm(v, ord=ordv)),
+                               rtol=1e-10, atol=1e-10)
+
+    n = 24
+    m = rng.standard_normal((n, n))
+    A = m @ m.T + n * np.eye(n)                           # SPD, well conditioned
+    rhs = rng.standard_normal(n)
+    ref = sla.solve(A, rhs, assume_a="pos")
+    for split in (None, 0):
+        sol = ht.linalg.cg(ht.array(A, split=split), ht.array(rhs, split=split), ht.zeros(n, dtype=ht.float64,
+                                                                                           split=split))
+        np.testing.assert_allclose(sol.numpy(), ref, rtol=1e-8, atol=1e-8)
+        V, T = ht.linalg.lanczos(ht.array(A, split=split), 10, v0=ht.array(np.ones(n) / np.sqrt(n), split=split))
+        Vn, Tn = V.numpy(), T.numpy()
+        np.testing.assert_allclose(Vn.T @ Vn, np.eye(10), atol=1e-8)
+        np.testing.assert_allclose(Vn.T @ A @ Vn, Tn, atol=1e-8)
+        # the extreme Ritz values bracket inside the spectrum
+        ev, rv = np.linalg.eigvalsh(A), np.linalg.eigvalsh(Tn)
+        assert ev[0] - 1e-9 <= rv[0] and rv[-1] <= ev[-1] + 1e-9
