@@ -24,7 +24,7 @@ from ..core.communication import MPI
 from .. import ops
 from ..parallel.ring import ring_pass
 
-__all__ = ["cdist", "cdist_stream", "manhattan", "rbf"]
+__all__ = ["cdist", "cdist_argmin", "cdist_stream", "cdist_topk", "manhattan", "rbf"]
 
 _ALLGATHER_BYTES = 2 << 30
 
@@ -201,3 +201,94 @@ def cdist_stream(X: DNDarray, Y: Optional[DNDarray], consume: Callable[[torch.Te
         ring_pass(y.contiguous(), lambda blk, src: visit(blk, displs[src]), comm, counts)
     else:
         visit(y, 0)
+
+
+def cdist_topk(X: DNDarray, Y: Optional[DNDarray] = None, k: int = 1):
+    """The ``k`` nearest rows of ``Y`` (euclidean) for every row of ``X``, without the m x n
+    distance matrix: ``(distances, indices)``, both (m, k), ascending, split like ``X``; the
+    indices are global row numbers of ``Y``. Equal distances are ordered by index, so the result
+    does not depend on the number of ranks (on the fused fp32 device kernel: among the candidates it
+    returns - of exactly duplicated rows of ``Y`` at the k-th place it keeps one).
+
+    The fused reduction the reference leaves to the caller (it materialises ``cdist`` and runs a
+    distributed ``topk``, ``heat/classification/kneighborsclassifier.py:117-160``): device fp32 runs
+    the fused MFMA distance + register top-k kernel (``ops.knn_topk``) per ``Y`` block, other inputs
+    exact distance tiles in query blocks; a split ``Y`` circulates around the ring
+    (``parallel.ring_pass``) and every rank keeps a running top-k of its own queries."""
+    if Y is None:
+        Y = X
+    if not isinstance(X, DNDarray) or not isinstance(Y, DNDarray):
+        raise TypeError("X and Y must be DNDarrays")
+    if X.ndim != 2 or Y.ndim != 2:
+        raise NotImplementedError("Only 2D data matrices are currently supported")
+    if X.gshape[1] != Y.gshape[1]:
+        raise ValueError("X and Y must have the same number of features, got {} and {}".format(X.gshape[1], Y.gshape[1]))
+    if X.split not in (None, 0) or Y.split not in (None, 0):
+        raise NotImplementedError("Splittings other than 0 or None currently not supported.")
+    n = Y.gshape[0]
+    if not isinstance(k, int) or k < 1 or k > n:
+        raise ValueError("k must be an integer in [1, {}], got {}".format(n, k))
+    dtype = types.promote_types(types.promote_types(X.dtype, Y.dtype), types.float32)
+    if dtype not in (types.float32, types.float64):
+        raise NotImplementedError("Datatype {} currently not supported as input".format(dtype))
+    tt = dtype.torch_type()
+    x = X.larray.to(tt)
+    y = Y.larray.to(tt)
+    nq = x.shape[0]
+    best_d = torch.full((nq, k), float("inf"), dtype=tt, device=x.device)
+    best_i = torch.full((nq, k), -1, dtype=torch.int64, device=x.device)
+
+    def block_topk(block: torch.Tensor):
+        kk = min(k, block.shape[0])
+        if tt == torch.float32 and ops.use_native(x):
+            dv, di = ops.knn_topk(x, block, kk)
+            return dv.to(tt), di.to(torch.int64)
+        step = max(1, (1 << 26) // max(block.shape[0], 1))
+        ds, ids = [], []
+        for q0 in range(0, nq, step):
+            d = ops.cdist(x[q0: q0 + step], block, "sqeuclidean", exact=True).to(tt)
+            # the kk smallest, ties at the kk-th value resolved to the lowest indices: everything
+            # below the threshold, then the lowest-index entries equal to it
+            thr = torch.topk(d, kk, dim=1, largest=False).values[:, -1:]
+            col = torch.arange(d.shape[1], device=d.device).expand_as(d)
+            key = torch.where(d < thr, torch.full_like(col, -1),
+                              torch.where(d == thr, col, torch.full_like(col, d.shape[1])))
+            di = torch.topk(key, kk, dim=1, largest=False).indices
+            ds.append(torch.gather(d, 1, di))
+            ids.append(di)
+        return torch.cat(ds), torch.cat(ids)
+
+    def merge(block: torch.Tensor, off: int):
+        nonlocal best_d, best_i
+        if block.shape[0] == 0 or nq == 0:
+            return
+        dv, di = block_topk(block)
+        cd = torch.cat([best_d, dv.to(x.device)], dim=1)
+        ci = torch.cat([best_i, di.to(x.device) + off], dim=1)
+        # (distance, index) order: stable sort by index, then stable sort by distance
+        o = torch.sort(ci, dim=1, stable=True).indices
+        cd, ci = torch.gather(cd, 1, o), torch.gather(ci, 1, o)
+        o = torch.sort(cd, dim=1, stable=True).indices[:, :k]
+        best_d, best_i = torch.gather(cd, 1, o), torch.gather(ci, 1, o)
+
+    if Y.is_distributed():
+        counts, displs = Y.counts_displs()
+        ring_pass(y.contiguous(), lambda blk, src: merge(blk, displs[src]), Y.comm, counts)
+    else:
+        merge(y, 0)
+    dist = torch.sqrt(torch.clamp(best_d, min=0))
+    split = 0 if X.split == 0 else None
+    bal = X.balanced if split is not None else True
+    return (DNDarray(dist, (X.gshape[0], k), dtype, split, X.device, X.comm, bal),
+            DNDarray(best_i, (X.gshape[0], k), types.int64, split, X.device, X.comm, bal))
+
+
+def cdist_argmin(X: DNDarray, Y: Optional[DNDarray] = None):
+    """Nearest row of ``Y`` for every row of ``X``: ``(distance, index)``, both (m,), split like
+    ``X`` - :func:`cdist_topk` with k = 1 (vector quantisation / k-means ``predict`` without the
+    distance matrix)."""
+    d, i = cdist_topk(X, Y, 1)
+    split = 0 if X.split == 0 else None
+    bal = X.balanced if split is not None else True
+    return (DNDarray(d.larray.reshape(-1), (X.gshape[0],), d.dtype, split, X.device, X.comm, bal),
+            DNDarray(i.larray.reshape(-1), (X.gshape[0],), i.dtype, split, X.device, X.comm, bal))

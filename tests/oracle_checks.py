@@ -378,3 +378,40 @@ def check_oracle_linalg_numpy():
         # the extreme Ritz values bracket inside the spectrum
         ev, rv = np.linalg.eigvalsh(A), np.linalg.eigvalsh(Tn)
         assert ev[0] - 1e-9 <= rv[0] and rv[-1] <= ev[-1] + 1e-9
+
+
+def check_oracle_cdist_topk_sklearn():
+    """``spatial.cdist_topk`` / ``cdist_argmin`` (fused nearest-neighbour reduction, no distance
+    matrix) against sklearn's exact ``NearestNeighbors`` for every split of X and Y, fp64 and fp32;
+    exact duplicates in Y check the (distance, index) tie order."""
+    from sklearn.neighbors import NearestNeighbors
+
+    rng = np.random.default_rng(51)
+    a = rng.standard_normal((37, 6))
+    b = rng.standard_normal((29, 6))
+    for k in (1, 4, 29):
+        nn = NearestNeighbors(n_neighbors=k, algorithm="brute").fit(b)
+        ref_d, ref_i = nn.kneighbors(a)
+        for sa in (None, 0):
+            for sb in (None, 0):
+                for dt, tol in ((np.float64, 1e-10), (np.float32, 2e-5)):
+                    d, i = ht.spatial.cdist_topk(ht.array(a.astype(dt), split=sa), ht.array(b.astype(dt), split=sb), k)
+                    assert d.split == sa and i.split == sa and d.gshape == (37, k)
+                    np.testing.assert_allclose(d.numpy(), ref_d, rtol=tol, atol=tol)
+                    np.testing.assert_array_equal(i.numpy(), ref_i)
+    # exact duplicates (fp64, exact path): equal distances come in index order, on any split
+    bd = b.copy()
+    bd[7] = bd[3]
+    bd[20] = bd[3]
+    for sb in (None, 0):
+        for k in (1, 2, 3):
+            d, i = ht.spatial.cdist_topk(ht.array(bd[3:4] + 1e-3), ht.array(bd, split=sb), k)
+            np.testing.assert_array_equal(i.numpy(), [[3, 7, 20][:k]])
+            assert np.all(d.numpy() == d.numpy()[0, 0])
+    dm, im = ht.spatial.cdist_argmin(ht.array(a, split=0), ht.array(b, split=0))
+    ref_d, ref_i = NearestNeighbors(n_neighbors=1, algorithm="brute").fit(b).kneighbors(a)
+    np.testing.assert_array_equal(im.numpy(), ref_i[:, 0])
+    np.testing.assert_allclose(dm.numpy(), ref_d[:, 0], rtol=1e-10)
+    # self-query: every row's nearest neighbour is itself at distance 0
+    ds, is_ = ht.spatial.cdist_topk(ht.array(a, split=0), None, 1)
+    np.testing.assert_array_equal(is_.numpy()[:, 0], np.arange(37))
