@@ -415,3 +415,23 @@ def check_oracle_cdist_topk_sklearn():
     # self-query: every row's nearest neighbour is itself at distance 0
     ds, is_ = ht.spatial.cdist_topk(ht.array(a, split=0), None, 1)
     np.testing.assert_array_equal(is_.numpy()[:, 0], np.arange(37))
+
+
+def check_cdist_topk_arguments():
+    a = ht.array(np.zeros((4, 3)), split=0)
+    for bad_k in (0, 5, 1.5):
+        try:
+            ht.spatial.cdist_topk(a, a, bad_k)
+        except ValueError:
+            pass
+        else:
+            raise AssertionError("k={} accepted".format(bad_k))
+    for args, exc in (((a, ht.array(np.zeros((4, 2)))), ValueError), ((ht.array(np.zeros((4, 3)), split=1), a),
+                                                                      NotImplementedError),
+                      ((np.zeros((4, 3)), a), TypeError), ((ht.array(np.zeros((4, 3), dtype=np.int64)), a), None)):
+        try:
+            ht.spatial.cdist_topk(*args)
+        except Exception as e:   # noqa: BLE001 - the exact type is checked below
+            assert exc is not None and isinstance(e, exc), (args, e)
+        else:
+            assert exc is None, args          # integer input promotes to float32 (like cdist)
