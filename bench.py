@@ -9,8 +9,9 @@ Data are synthetic (Threefry normal samples generated on the device, random-init
 quantity the reference's benchmark scales with); ``ms_per_step`` the wall time of one iteration.
 
 Run: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
-Secondary workloads: ``--workload cdist`` (distance_matrix, streamed) and ``--workload moments``
-(statistical_moments mean/var of 1e9 float32).
+Secondary workloads: ``--workload cdist`` (distance_matrix, streamed), ``--workload knn`` (the
+distance_matrix config reduced to each row's ``--topk`` nearest rows by the fused kernel, no
+matrix) and ``--workload moments`` (statistical_moments mean/var of 1e9 float32).
 """
 from __future__ import annotations
 
@@ -28,11 +29,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="kmeans", choices=["kmeans", "cdist", "moments"])
+    p.add_argument("--workload", default="kmeans", choices=["kmeans", "cdist", "knn", "moments"])
     p.add_argument("--n-per-gpu", type=int, default=None,
                    help="kmeans: points per GPU (1.25e7); moments: elements per GPU (1e9)")
     p.add_argument("--rows", type=int, default=1_000_000, help="cdist: total rows (strong scaling)")
     p.add_argument("--k", type=int, default=1024)
+    p.add_argument("--topk", type=int, default=8, help="knn: neighbours per row")
     p.add_argument("--f", type=int, default=None, help="features (kmeans 64, cdist 128)")
     p.add_argument("--precision", default="fast", choices=["fast", "exact"],
                    help="kmeans: 'fast' = distances by a 3-term fp16 split on the matrix cores (fp32-GEMM "
@@ -147,6 +149,28 @@ def main():
         extra["flop_convention"] = "2*n*n*f (the distance GEMM of the quadratic expansion)"
         extra["distances_per_s"] = n * n / (ms * 1e-3)
         extra.update(validate_cdist(x, comm))
+        scaling = "strong"
+    elif args.workload == "knn":
+        # the same 1e6 x 128 self-distance problem, each row reduced to its topk nearest rows by the
+        # fused MFMA distance + register top-k kernel (Y blocks around the ring; no distance matrix)
+        n, f = args.rows, args.f or 128
+        ht.random.seed(7)
+        x = ht.random.rand(n, f, split=0, device=dev)
+        for _ in range(args.warmup):
+            ht.spatial.cdist_topk(x, x, args.topk)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            d, idx = ht.spatial.cdist_topk(x, x, args.topk)
+        sync()
+        dt = time.perf_counter() - t0
+        ms = rank_times(comm, dt, args.steps, extra)
+        value = 2.0 * n * n * f / (ms * 1e-3) / 1e9
+        metric, unit = "knn_gflops", "GFLOP/s (fp32-equivalent)"
+        cfg = {"model": "cdist_topk euclidean n={} f={} k={} float32 split=0".format(n, f, args.topk),
+               "global_batch": n, "seq_len": f, "parallelism": "dp{}".format(n_gpus)}
+        extra["flop_convention"] = "2*n*n*f (the distance GEMM of the quadratic expansion)"
+        extra.update(validate_knn(x, d, idx, comm))
         scaling = "strong"
     else:
         args.n_per_gpu = args.n_per_gpu or 1_000_000_000
@@ -268,6 +292,25 @@ def validate_cdist(x, comm) -> dict:
         err = float(((d.double() ** 2 - ref[off: off + rows] ** 2).abs() / scale).max())
     err = comm.allreduce(err, ht.MPI.MAX) if comm.size > 1 else err
     return {"sample_max_sq_err_rel_vs_fp64": err}
+
+
+def validate_knn(x, d, idx, comm) -> dict:
+    """Rank 0's first 64 local queries against an fp64 brute force over the gathered data (the
+    self-match must come first at distance 0)."""
+    xs = x.larray
+    full = comm.allgather_tensor(xs.contiguous(), 0, x.split_counts()) if x.is_distributed() else xs
+    q = xs[:64].double()
+    ok = {}
+    if q.shape[0]:
+        ref = torch.cdist(q, full.double())
+        rd, ri = torch.topk(ref, idx.gshape[1], dim=1, largest=False)
+        r0 = x.counts_displs()[1][comm.rank] if x.is_distributed() else 0
+        ok["self_first"] = bool((idx.larray[:64, 0] == torch.arange(q.shape[0], device=q.device) + r0).all())
+        ok["index_agreement"] = float((idx.larray[:64] == ri).float().mean())
+        ok["max_rel_dist_err"] = float(((d.larray[:64].double() - rd).abs() / rd.clamp(min=1e-6)).max())
+    if comm.size > 1:
+        ok = comm.bcast(ok, root=0)
+    return ok
 
 
 def rccl_world_size(comm) -> int:

@@ -53,7 +53,7 @@ def test_bench_multi_rank_one_json_line(ranks):
     assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= 1e-6 * rec["value"]
 
 
-@pytest.mark.parametrize("workload", ["moments", "cdist"])
+@pytest.mark.parametrize("workload", ["moments", "cdist", "knn"])
 def test_bench_secondary_workloads_validate(workload):
     env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     extra_args = ["--n-per-gpu", "100000"] if workload == "moments" else ["--rows", "6000", "--f", "8"]
@@ -67,5 +67,8 @@ def test_bench_secondary_workloads_validate(workload):
     ex = lines[0]["extra"]
     if workload == "moments":
         assert ex["mean_abs_err_vs_fp64"] < 1e-5 and ex["var_rel_err_vs_fp64"] < 1e-5
-    else:
+    elif workload == "cdist":
         assert ex["sample_max_sq_err_rel_vs_fp64"] < 1e-5
+    else:
+        assert lines[0]["scaling"] == "strong" and lines[0]["config"]["global_batch"] == 6000
+        assert ex["self_first"] is True and ex["index_agreement"] == 1.0 and ex["max_rel_dist_err"] < 1e-5
