@@ -412,6 +412,11 @@ def check_oracle_cdist_topk_sklearn():
     ref_d, ref_i = NearestNeighbors(n_neighbors=1, algorithm="brute").fit(b).kneighbors(a)
     np.testing.assert_array_equal(im.numpy(), ref_i[:, 0])
     np.testing.assert_allclose(dm.numpy(), ref_d[:, 0], rtol=1e-10)
+    # fewer query rows than ranks (empty local blocks) and a Y smaller than the world
+    d3, i3 = ht.spatial.cdist_topk(ht.array(a[:3], split=0), ht.array(b[:2], split=0), 2)
+    r3 = NearestNeighbors(n_neighbors=2, algorithm="brute").fit(b[:2]).kneighbors(a[:3])
+    np.testing.assert_array_equal(i3.numpy(), r3[1])
+    np.testing.assert_allclose(d3.numpy(), r3[0], rtol=1e-10)
     # self-query: every row's nearest neighbour is itself at distance 0
     ds, is_ = ht.spatial.cdist_topk(ht.array(a, split=0), None, 1)
     np.testing.assert_array_equal(is_.numpy()[:, 0], np.arange(37))
