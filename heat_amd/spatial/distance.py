@@ -243,7 +243,7 @@ def cdist_topk(X: DNDarray, Y: Optional[DNDarray] = None, k: int = 1):
         if tt == torch.float32 and ops.use_native(x):
             dv, di = ops.knn_topk(x, block, kk)
             return dv.to(tt), di.to(torch.int64)
-        step = max(1, (1 << 26) // max(block.shape[0], 1))
+        step = max(1, (1 << 24) // max(block.shape[0], 1))  # <= 16M entries per tile (x3 tensors)
         ds, ids = [], []
         for q0 in range(0, nq, step):
             d = ops.cdist(x[q0: q0 + step], block, "sqeuclidean", exact=True).to(tt)
