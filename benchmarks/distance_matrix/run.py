@@ -6,6 +6,8 @@ of ``cdist(data, data, quadratic_expansion=False/True)``.
   matrix materialised (6.4 GB), split 0.
 * ``--case northstar``: BASELINE.json config, 1e6 x 128 vs itself; the 4 TB result is streamed
   tile by tile (``ht.spatial.cdist_stream``) through one reused HBM tile.
+* ``--case knn``: the northstar size reduced to every row's ``--k`` nearest rows by the fused
+  distance + top-k kernel (``ht.spatial.cdist_topk``; no matrix at all).
 GFLOP/s convention: 3*m*n*f for the exact path (sub, mul, add), 2*m*n*f for the expansion GEMM.
 """
 import argparse
@@ -16,16 +18,22 @@ from benchmarks.common import ht, report, setup, timed
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--case", default="susy", choices=["susy", "northstar"])
+    p.add_argument("--case", default="susy", choices=["susy", "northstar", "knn"])
     p.add_argument("--rows", type=int, default=None)
     p.add_argument("--features", type=int, default=None)
     p.add_argument("--trials", type=int, default=5)
+    p.add_argument("--k", type=int, default=8, help="knn: neighbours per row")
     a = p.parse_args()
     dev = setup()
     n = a.rows or (40_000 if a.case == "susy" else 1_000_000)
     f = a.features or (18 if a.case == "susy" else 128)
     ht.random.seed(1)
     data = ht.random.rand(n, f, split=0, device=dev)
+    if a.case == "knn":
+        t = timed(lambda: ht.spatial.cdist_topk(data, data, a.k), a.trials)
+        report("distance_matrix", {"case": "knn", "n": n, "f": f, "k": a.k}, t,
+               {"gflops": 2.0 * n * n * f / 1e9, "distances_per_s": float(n) * n})
+        return
     for qe in (False, True):
         if a.case == "susy":
             fn = lambda: ht.spatial.cdist(data, data, quadratic_expansion=qe)  # noqa: E731

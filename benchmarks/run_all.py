@@ -19,6 +19,7 @@ SUITE = {
     "kmeans": ("benchmarks.kmeans.run", []),
     "kmeans_reference": ("benchmarks.kmeans.run", ["--case", "reference"]),   # k = 8, 30 iterations
     "distance_matrix": ("benchmarks.distance_matrix.run", []),
+    "knn": ("benchmarks.distance_matrix.run", ["--case", "knn"]),               # 1e6 x 1e6 x 128, k = 8
     "statistical_moments": ("benchmarks.statistical_moments.run", []),
     "lasso": ("benchmarks.lasso.run", []),
     "linalg": ("benchmarks.linalg.run", []),
@@ -28,6 +29,7 @@ QUICK = {
     "kmeans": ["--rows-per-gpu", "200000", "--trials", "2"],
     "kmeans_reference": ["--rows-per-gpu", "200000", "--trials", "2"],
     "distance_matrix": ["--rows", "8000", "--trials", "2"],
+    "knn": ["--rows", "8000", "--trials", "2"],
     "statistical_moments": ["--rows-per-gpu", "10000", "--cols", "100", "--trials", "2"],
     "lasso": ["--rows", "100000", "--trials", "2"],
     "linalg": ["--rows-per-gpu", "20000", "--cols", "256", "--trials", "2"],
