@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 A="GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
 rc=0
-for w in kmeans moments gemm cdist; do
+for w in ${PMC_TARGETS:-kmeans moments gemm cdist topk}; do
   timeout -s KILL 120 rocprofv3 --pmc $A --kernel-trace --output-format csv -d "$OUT/${w}_A" -o a -- python3 "$ROOT/tools/microbench/pmc_targets.py" $w > "$OUT/${w}_A.log" 2>&1 || { rc=$?; break; }
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/${w}_B" -o b -- python3 "$ROOT/tools/microbench/pmc_targets.py" $w > "$OUT/${w}_B.log" 2>&1 || { rc=$?; break; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/${w}_C" -o c -- python3 "$ROOT/tools/microbench/pmc_targets.py" $w > "$OUT/${w}_C.log" 2>&1 || { rc=$?; break; }

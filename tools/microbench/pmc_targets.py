@@ -3,7 +3,8 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   kmeans  - 8 Lloyd steps, k = 1024, 1.25e7 x 64 (h3_assign_p + deterministic update)
   moments - mean of 1e9 fp32, axis None / 0 / 1 (moments.hip, one kernel per call)
   gemm    - ht.matmul 8192^3 fp32 at precision highest (gemm_f32t) and high (gemm_h3t)
-  cdist   - one 32768 x 32768 x 128 distance tile (cdist_f16x3.hip)"""
+  cdist   - one 32768 x 32768 x 128 distance tile (cdist_f16x3.hip)
+  topk    - 8 nearest of 65536 x 128 queries among 1e6 points (spatial.cdist_topk -> h3_topk)"""
 import sys
 
 import torch
@@ -38,6 +39,11 @@ def main():
         x = torch.rand(32768, 128, device="cuda")
         for _ in range(3):
             ops.cdist(x, x)
+    elif which == "topk":
+        q = ht.random.rand(65536, 128, split=0)
+        y = ht.random.rand(1_000_000, 128, split=0)
+        for _ in range(3):
+            ht.spatial.cdist_topk(q, y, 8)
     torch.cuda.synchronize()
     print("done", which)
 

@@ -37,7 +37,7 @@ def main(root, out):
              "Produced by `tools/gpu_pmc_r03.sh` (three passes per workload: SQ issue / MFMA counters, "
              "FETCH_SIZE, WRITE_SIZE; `--kernel-trace` only besides the counters) and `tools/pmc_summary.py`. "
              "Workloads: `tools/microbench/pmc_targets.py`. Kernels under 20 us are omitted.", ""]
-    for w in ("kmeans", "moments", "gemm", "cdist"):
+    for w in ("kmeans", "moments", "gemm", "cdist", "topk"):
         fa = glob.glob(os.path.join(root, w + "_A", "*counter_collection.csv"))
         fb = glob.glob(os.path.join(root, w + "_B", "*counter_collection.csv"))
         fc = glob.glob(os.path.join(root, w + "_C", "*counter_collection.csv"))
