@@ -70,9 +70,11 @@ def main(root, out):
                 short(name), len(dA[name]), d * 1e6, clk, busy, vpm, wi, wa, rd, wr, tbs)))
         rows.sort(key=lambda r: -r[0])
         lines += [r for _, r in rows] + [""]
-    open(out, "w").write("\n".join(lines) + "\n")
+    if out:
+        open(out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc", sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_r03.md")
+    # the markdown file is written only when named (python tools/pmc_summary.py gpurun_out/pmc profiles/pmc_r03.md)
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc", sys.argv[2] if len(sys.argv) > 2 else None)
