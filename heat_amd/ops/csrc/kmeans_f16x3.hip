@@ -102,53 +102,85 @@ __global__ __launch_bounds__(256) void h3_cscale(const float* __restrict__ C, in
                                                  unsigned* __restrict__ vimg) {
   constexpr int G8 = FPAD / 8;  // lanes per centroid (divides 64)
   constexpr int CB = H3Cfg<FPAD>::CB;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int c = (int)(t / G8), g8 = (int)(t % G8);
-  const bool live = c < k;
-  float mx = 0.f, sq = 0.f;
+  // grid-stride over the kpad * G8 lanes (the loop bound is block-uniform, so every lane of a
+  // wave takes part in each step's shuffles); the two maxima are reduced per block and posted
+  // with ONE atomicMax pair per block - a pair per centroid serialised on two addresses (5.7 ms
+  // for 1e6 rows, the KNN training set, 90 GB/s)
+  const int64_t total = (int64_t)kpad * G8;
+  float bmx = 0.f, bu = 0.f;
+  for (int64_t t0 = (int64_t)blockIdx.x * 256; t0 < total; t0 += (int64_t)gridDim.x * 256) {
+    const int64_t t = t0 + threadIdx.x;
+    const int c = (int)(t / G8), g8 = (int)(t % G8);
+    const bool live = c < k;
+    float mx = 0.f, sq = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int fe = g8 * 8 + i;
-    const float x = (live && fe < f) ? C[(int64_t)c * ldc + fe] : 0.f;
-    mx = fmaxf(mx, fabsf(x));
-    sq = fmaf(x, x, sq);
-  }
+    for (int i = 0; i < 8; ++i) {
+      const int fe = g8 * 8 + i;
+      const float x = (live && fe < f) ? C[(int64_t)c * ldc + fe] : 0.f;
+      mx = fmaxf(mx, fabsf(x));
+      sq = fmaf(x, x, sq);
+    }
 #pragma unroll
-  for (int o = 1; o < G8; o <<= 1) {
-    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-    sq += __shfl_xor(sq, o, 64);
+    for (int o = 1; o < G8; o <<= 1) {
+      mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      sq += __shfl_xor(sq, o, 64);
+    }
+    if (g8 != 0 || c >= kpad) continue;
+    float* urc = ur + (int64_t)(c / CB) * 2 * CB + c % CB;
+    // rank-1 A fragment of the -s_c u_c term (see h3_assign_p): lane j of tile c/32 holds its three
+    // bf16 pieces in k-slots 0..2, lane j + 32 (k-slots 8..15) zeros
+    unsigned* vc = vimg + ((int64_t)(c / 32) * 64 + c % 32) * 2;
+    vc[64] = 0u;
+    vc[65] = 0u;
+    if (!live) {
+      urc[0] = __builtin_huge_valf();
+      urc[CB] = 1.f;
+      vc[0] = 0xFF80u;  // -inf, 0
+      vc[1] = 0u;
+      continue;
+    }
+    int e = 0;
+    if (mx > 0.f && mx < __builtin_huge_valf()) frexpf(mx, &e);
+    urc[0] = 0.5f * sq;
+    urc[CB] = ldexpf(1.f, e);
+    {
+      const float y = -ldexpf(0.5f * sq, -e);  // -s_c u_c, split into hi + mid + lo (24 bits)
+      const unsigned hi = h3_bf16_rn(y);
+      const float r1 = y - h3_bf16_f(hi);
+      const unsigned mid = h3_bf16_rn(r1);
+      const unsigned lo = h3_bf16_rn(r1 - h3_bf16_f(mid));
+      vc[0] = hi | (mid << 16);
+      vc[1] = lo;
+    }
+    if (mx > 0.f && mx < __builtin_huge_valf()) bmx = fmaxf(bmx, mx);
+    if (sq > 0.f && sq < __builtin_huge_valf()) bu = fmaxf(bu, 0.5f * sq);
   }
-  if (g8 != 0 || c >= kpad) return;
-  float* urc = ur + (int64_t)(c / CB) * 2 * CB + c % CB;
-  // rank-1 A fragment of the -s_c u_c term (see h3_assign_p): lane j of tile c/32 holds its three
-  // bf16 pieces in k-slots 0..2, lane j + 32 (k-slots 8..15) zeros
-  unsigned* vc = vimg + ((int64_t)(c / 32) * 64 + c % 32) * 2;
-  vc[64] = 0u;
-  vc[65] = 0u;
-  if (!live) {
-    urc[0] = __builtin_huge_valf();
-    urc[CB] = 1.f;
-    vc[0] = 0xFF80u;  // -inf, 0
-    vc[1] = 0u;
-    return;
+  // block maxima (non-negative, so 0 is the identity) -> one atomicMax per word per block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    bmx = fmaxf(bmx, __shfl_xor(bmx, o, 64));
+    bu = fmaxf(bu, __shfl_xor(bu, o, 64));
   }
-  int e = 0;
-  if (mx > 0.f && mx < __builtin_huge_valf()) frexpf(mx, &e);
-  urc[0] = 0.5f * sq;
-  urc[CB] = ldexpf(1.f, e);
-  {
-    const float y = -ldexpf(0.5f * sq, -e);  // -s_c u_c, split into hi + mid + lo (24 bits)
-    const unsigned hi = h3_bf16_rn(y);
-    const float r1 = y - h3_bf16_f(hi);
-    const unsigned mid = h3_bf16_rn(r1);
-    const unsigned lo = h3_bf16_rn(r1 - h3_bf16_f(mid));
-    vc[0] = hi | (mid << 16);
-    vc[1] = lo;
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wv] = bmx;
+    red[1][wv] = bu;
   }
-  if (mx > 0.f && mx < __builtin_huge_valf())
-    atomicMax(reinterpret_cast<unsigned int*>(meta + 1), __float_as_uint(mx));
-  if (sq > 0.f && sq < __builtin_huge_valf())
-    atomicMax(reinterpret_cast<unsigned int*>(meta + 2), __float_as_uint(0.5f * sq));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bmx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    bu = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    if (bmx > 0.f) atomicMax(reinterpret_cast<unsigned int*>(meta + 1), __float_as_uint(bmx));
+    if (bu > 0.f) atomicMax(reinterpret_cast<unsigned int*>(meta + 2), __float_as_uint(bu));
+  }
+}
+
+// Grid of h3_cscale: one lane per 8 features of each padded centroid, at most 1024 blocks (a
+// grid-stride loop covers the rest), so large point sets post few same-address atomics.
+static inline unsigned h3_cscale_grid(int64_t kpad, int g8) {
+  const int64_t b = (kpad * g8 + 255) / 256;
+  return (unsigned)(b < 1024 ? (b > 0 ? b : 1) : 1024);
 }
 
 template <int FPAD>
@@ -969,7 +1001,7 @@ HA_EXPORT int ha_h3_assign(const void* planes, const float* sx, int64_t n, int f
     constexpr int NPB = FP >= 128 ? 1 : 2, MINB = 2;  /* 2 chunk buffers (~66 KB) per WG: 2 WGs/CU */                                        \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     /* no memset of meta[1..2]: only h1_filter reads them (bench A/B: -12 us per step) */                  \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
     const size_t lds = 2 * ((size_t)KC::CHUNK_H * 2 + KC::CB * 8 + KC::CB * 16);                            \
@@ -1036,7 +1068,7 @@ HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_
     using KC = H3Cfg<FP, NPB>;                                                                              \
     using K1 = H3Cfg<FP, NPB1>;                                                                             \
     hipMemsetAsync(meta, 0, 4 * sizeof(float), s);                                                          \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
     const size_t lds1 = 2 * ((size_t)K1::CHUNK_H + K1::CB * 8);                                                   \
@@ -1100,7 +1132,7 @@ HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, 
   case FP: {                                                                                                 \
     using KC = H3Cfg<FP, 1>;                                                                                 \
     /* meta[1..2] (filter bound) unused: no memset */                                                           \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, m, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));          \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, m, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));          \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),   \
                        dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                \
     const size_t lds = (size_t)KC::CHUNK_H * 2 + KC::CB * 8;                                                 \
@@ -1166,7 +1198,7 @@ HA_EXPORT int ha_h3_assign_r(const void* planes, const float* sx, int64_t n, int
     constexpr int NPB = FP >= 128 ? 1 : 2;                                                                  \
     using KC = H3Cfg<FP, NPB>;                                                                              \
     /* meta[1..2] (filter bound) unused: no memset */                                                          \
-    hipLaunchKernelGGL(h3_cscale<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
+    hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, k, f, ldc, kpad, u, meta, (unsigned*)(meta + 4));         \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),  \
                        dim3(256), 0, s, C, k, f, ldc, kpad, image, u);                               \
     for (int ph = 0; ph < phases; ++ph) {                                                                   \
