@@ -22,6 +22,15 @@ from ..parallel.ring import ring_pass
 __all__ = ["KNeighborsClassifier"]
 
 
+def _smallest_k(vals: torch.Tensor, gidx: torch.Tensor, k: int) -> torch.Tensor:
+    """Positions (along dim 1) of the ``k`` smallest ``vals``, equal values ordered by global
+    training index ``gidx``: two stable sorts, so the pick does not depend on the visiting order of
+    the blocks (and thus not on the number of ranks)."""
+    o1 = torch.sort(gidx, dim=1, stable=True).indices
+    o2 = torch.sort(torch.gather(vals, 1, o1), dim=1, stable=True).indices
+    return torch.gather(o1, 1, o2[:, :k])
+
+
 class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
     """Majority vote of the ``n_neighbors`` nearest training samples (euclidean by default)."""
 
@@ -48,6 +57,15 @@ class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
         if y.split != x.split and x.comm.size > 1:
             # labels travel with their samples: y takes x's distribution
             y = ht.resplit(y, x.split if x.split == 0 else None)
+        if x.split == 0 and y.split == 0 and x.is_distributed():
+            xmap = x.create_lshape_map()
+            ymap = y.create_lshape_map()
+            if not torch.equal(xmap[:, 0], ymap[:, 0]):
+                # same split, different row blocks (e.g. an unbalanced x): move y's rows to x's
+                y = y.copy()
+                target = ymap.clone()
+                target[:, 0] = xmap[:, 0]
+                y.redistribute_(lshape_map=ymap, target_map=target)
         self.x = x
         self.n_samples_fit_ = x.gshape[0]
         if y.ndim == 1:
@@ -71,20 +89,28 @@ class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
                 d = distances.larray
                 kk = min(k, d.shape[1])
                 ylab = self.y.larray.to(torch.float32)
+                comm = distances.comm
+                col0 = sum(distances.split_counts()[: comm.rank])
+                if ylab.shape[0] != d.shape[1]:
+                    raise ValueError("distance columns ({}) and local labels ({}) are not aligned".format(
+                        d.shape[1], ylab.shape[0]))
                 if kk:
-                    vals, idx = torch.topk(d, kk, dim=1, largest=False)
+                    cols = torch.arange(d.shape[1], device=d.device).expand(d.shape[0], -1)
+                    idx = _smallest_k(d, cols, kk)
+                    vals = torch.gather(d, 1, idx)
                     cand_y = ylab[idx.reshape(-1).to(ylab.device)].reshape(d.shape[0], kk, -1)
                 else:
+                    idx = torch.zeros((d.shape[0], 0), dtype=torch.int64, device=d.device)
                     vals = d.new_zeros((d.shape[0], 0))
                     cand_y = ylab.new_zeros((d.shape[0], 0, ylab.shape[1]))
-                comm = distances.comm
                 all_v = comm.allgather_tensor(vals.to(torch.float64).contiguous(), 1)
+                all_i = comm.allgather_tensor((idx + col0).to(torch.int64).contiguous(), 1)
                 all_y = comm.allgather_tensor(cand_y.contiguous(), 1)
-                _, sel = torch.topk(all_v, k, dim=1, largest=False)
+                sel = _smallest_k(all_v, all_i, k)
                 votes = torch.gather(all_y, 1, sel.unsqueeze(-1).expand(-1, -1, all_y.shape[-1])).sum(1)
             else:
                 d = distances.larray
-                _, idx = torch.topk(d, k, dim=1, largest=False)
+                idx = _smallest_k(d, torch.arange(d.shape[1], device=d.device).expand(d.shape[0], -1), k)
                 ylab = self.y._gathered() if self.y.is_distributed() else self.y.larray
                 votes = ylab[idx.reshape(-1).to(ylab.device)].reshape(idx.shape[0], k, -1).sum(1)
             lab = torch.argmax(votes, dim=1)
@@ -96,31 +122,38 @@ class KNeighborsClassifier(ClassificationMixin, BaseEstimator):
         ylab = self.y.larray.to(torch.float32)
         nq = q.shape[0]
         best_d = torch.full((nq, k), float("inf"), dtype=torch.float32, device=q.device)
+        best_i = torch.full((nq, k), torch.iinfo(torch.int64).max, dtype=torch.int64, device=q.device)
         best_y = torch.zeros((nq, k, ylab.shape[1]), dtype=torch.float32, device=q.device)
         if train.is_distributed():
+            if ylab.shape[0] != tl.shape[0]:
+                raise ValueError("training rows ({}) and local labels ({}) are not aligned".format(
+                    tl.shape[0], ylab.shape[0]))
             packed = torch.cat([tl.float(), ylab], dim=1)
             counts = train.split_counts()
+            starts = [sum(counts[:r]) for r in range(len(counts))]
 
             def visit(block: torch.Tensor, src: int):
-                _merge(block[:, : tl.shape[1]], block[:, tl.shape[1]:])
+                _merge(block[:, : tl.shape[1]], block[:, tl.shape[1]:], starts[src])
 
-        def _merge(tb: torch.Tensor, yb: torch.Tensor):
-            nonlocal best_d, best_y
+        def _merge(tb: torch.Tensor, yb: torch.Tensor, row0: int):
+            nonlocal best_d, best_i, best_y
             if tb.shape[0] == 0 or nq == 0:
                 return
             # fused distance + running top-k kernel (no nq x nt matrix); exact distances of the picks
             kk = min(k, tb.shape[0])
             dv, di = ops.knn_topk(q.float(), tb.float(), kk)
             cand_d = torch.cat([best_d, dv], dim=1)
+            cand_i = torch.cat([best_i, di.to(torch.int64) + row0], dim=1)
             cand_y = torch.cat([best_y, yb[di.reshape(-1)].reshape(nq, kk, -1)], dim=1)
-            sel_d, sel = torch.topk(cand_d, k, dim=1, largest=False)
-            best_d = sel_d
+            sel = _smallest_k(cand_d, cand_i, k)   # ties by global training index
+            best_d = torch.gather(cand_d, 1, sel)
+            best_i = torch.gather(cand_i, 1, sel)
             best_y = torch.gather(cand_y, 1, sel.unsqueeze(2).expand(-1, -1, cand_y.shape[2]))
 
         if train.is_distributed():
             ring_pass(packed, visit, train.comm, counts)
         else:
-            _merge(tl.float(), ylab)
+            _merge(tl.float(), ylab, 0)
         votes = best_y.sum(1)
         lab = torch.argmax(votes, dim=1)
         self.classes_ = DNDarray(lab, (x.gshape[0],), ht.int64, x.split, x.device, x.comm, x.balanced)

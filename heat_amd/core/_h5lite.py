@@ -86,8 +86,11 @@ class H5Dataset:
                 n = len(raw) // es
                 body = np.frombuffer(raw, np.uint8, n * es).reshape(es, n).T.tobytes()
                 raw = body + raw[n * es:]
-            elif fid == 3:    # fletcher32: trailing 4-byte checksum
-                raw = raw[:-4]
+            elif fid == 3:    # fletcher32: trailing 4-byte little-endian checksum, verified
+                body, stored = raw[:-4], struct.unpack("<I", raw[-4:])[0]
+                if _fletcher32(body) != stored:
+                    raise IOError("HDF5 chunk of {!r} failed its fletcher32 checksum".format(self.path))
+                raw = body
             else:
                 raise NotImplementedError("HDF5 filter {} needs h5py".format(fid))
         return raw
@@ -753,17 +756,27 @@ def encode_chunk(block: np.ndarray, filters) -> bytes:
 
 
 def _fletcher32(data: bytes) -> int:
-    """HDF5's Fletcher-32 over 16-bit big-endian words (odd trailing byte padded)."""
-    if len(data) % 2:
-        data = data + b"\0"
-    w = np.frombuffer(data, dtype=">u2").astype(np.uint64)
+    """HDF5's Fletcher-32 (``H5_checksum_fletcher32``): 16-bit big-endian words in blocks of 360,
+    both sums folded with end-around carry ``(x & 0xffff) + (x >> 16)`` after every block (NOT
+    ``% 65535``: a nonzero multiple of 65535 stays 0xffff), an odd trailing byte as the high byte
+    of one more word, then a final fold."""
+    nw = len(data) // 2
+    w = np.frombuffer(data, dtype=">u2", count=nw).astype(np.uint64)
     s1 = s2 = 0
-    for i in range(0, len(w), 360):
-        blk = w[i: i + 360]
-        c1 = np.cumsum(blk) + s1
-        s2 = int((s2 + c1.sum()) % 65535)
-        s1 = int(c1[-1] % 65535)
-    return (s2 << 16) | s1
+    for i in range(0, nw, 360):
+        c1 = np.cumsum(w[i: i + 360]) + s1
+        s2 += int(c1.sum())
+        s1 = int(c1[-1])
+        s1 = (s1 & 0xFFFF) + (s1 >> 16)
+        s2 = (s2 & 0xFFFF) + (s2 >> 16)
+    if len(data) % 2:
+        s1 += data[-1] << 8
+        s2 += s1
+        s1 = (s1 & 0xFFFF) + (s1 >> 16)
+        s2 = (s2 & 0xFFFF) + (s2 >> 16)
+    s1 = (s1 & 0xFFFF) + (s1 >> 16)
+    s2 = (s2 & 0xFFFF) + (s2 >> 16)
+    return ((s2 << 16) | s1) & 0xFFFFFFFF
 
 
 def create_chunked_dataset(path: str, name: str, shape: Tuple[int, ...], dtype, chunks: Tuple[int, ...],

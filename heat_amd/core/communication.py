@@ -201,6 +201,17 @@ class Communication:
         raise NotImplementedError()
 
 
+def exchange_axis_bytes(send_shape, send_axis: int, scounts, recv_shape, recv_axis: int, rcounts, itemsize: int):
+    """Byte counts of the packed blocks of :meth:`MPICommunication.exchange_axis`: (to every rank,
+    from every rank). Block q of the send side is ``send.narrow(send_axis, ., scounts[q])`` packed
+    contiguously, block r of the receive side ``recv.narrow(recv_axis, ., rcounts[r])``."""
+    from ..ops import kernels as _k
+
+    so, _, sr = _k._rows_view(tuple(send_shape), send_axis)
+    ro, _, rr = _k._rows_view(tuple(recv_shape), recv_axis)
+    return ([so * int(c) * sr * itemsize for c in scounts], [ro * int(c) * rr * itemsize for c in rcounts])
+
+
 def _as_tensor(buf):
     from .dndarray import DNDarray
 
@@ -781,11 +792,8 @@ class MPICommunication(Communication):
             out = send.reshape(recv_shape) if tuple(send.shape) == recv_shape else send
             return None, lambda: out
         packed = _k.pack_blocks(send, send_axis, scounts)
-        so, _, sr = _k._rows_view(tuple(send.shape), send_axis)
-        ro, _, rr = _k._rows_view(recv_shape, recv_axis)
-        es = send.element_size()
-        in_b = [so * int(c) * sr * es for c in scounts]
-        out_b = [ro * int(c) * rr * es for c in rcounts]
+        in_b, out_b = exchange_axis_bytes(tuple(send.shape), send_axis, scounts, recv_shape, recv_axis, rcounts,
+                                          send.element_size())
         flat_out = torch.empty(int(np.prod(recv_shape)) if recv_shape else 1, dtype=send.dtype, device=send.device)
         src_b = packed.contiguous().view(torch.uint8) if packed.numel() else torch.empty(0, dtype=torch.uint8,
                                                                                            device=send.device)

@@ -23,7 +23,7 @@ import torch
 from . import devices, factories, types
 from .communication import MPI, sanitize_comm
 from .dndarray import DNDarray
-from . import _h5lite
+from . import _h5lite, _ncclassic as _ncc
 from .stride_tricks import sanitize_axis
 
 __all__ = ["load", "load_csv", "save", "save_csv", "load_npy", "save_npy", "supports_hdf5", "supports_netcdf",
@@ -386,32 +386,6 @@ DNDarray.save_hdf5 = lambda self, path, dataset, mode="w", **kwargs: save_hdf5(s
 
 
 # --------------------------------------------------------------------------------------------- netcdf
-def _netcdf3_header(variable: str, dims: List[str], shape, np_dtype: np.dtype) -> Tuple[bytes, int]:
-    """Classic netCDF (CDF-2, 64-bit offsets) header for ONE fixed-size variable; returns
-    (header bytes, data offset). Layout: magic, numrecs, dim_list, gatt_list, var_list."""
-    import struct
-
-    codes = {np.dtype("i1"): 1, np.dtype("S1"): 2, np.dtype("i2"): 3, np.dtype("i4"): 4, np.dtype("f4"): 5,
-             np.dtype("f8"): 6}
-    if np_dtype not in codes:
-        raise TypeError("netCDF classic has no {}".format(np_dtype))
-
-    def name(n: str) -> bytes:
-        raw = n.encode("utf-8")
-        return struct.pack(">i", len(raw)) + raw + b"\0" * ((-len(raw)) % 4)
-
-    h = b"CDF\x02" + struct.pack(">i", 0)
-    h += struct.pack(">ii", 0x0A, len(dims)) + b"".join(name(d) + struct.pack(">i", int(s)) for d, s in zip(dims, shape))
-    h += struct.pack(">ii", 0, 0)
-    vsize = int(np.prod(shape)) * np_dtype.itemsize
-    var = name(variable) + struct.pack(">i", len(dims)) + b"".join(struct.pack(">i", i) for i in range(len(dims)))
-    var += struct.pack(">ii", 0, 0) + struct.pack(">ii", codes[np_dtype], min(vsize + ((-vsize) % 4), 2 ** 31 - 1))
-    begin = len(h) + 8 + len(var) + 8
-    h += struct.pack(">ii", 0x0B, 1) + var + struct.pack(">q", begin)
-    assert len(h) == begin
-    return h, begin
-
-
 def load_netcdf(path: str, variable: str, dtype=types.float32, split: Optional[int] = None, device=None,
                 comm=None) -> DNDarray:
     """Load a netCDF variable (netCDF4 when installed; otherwise netCDF-4/HDF5 files through the
@@ -449,110 +423,17 @@ def _nc_read_local(path: str, variable: str, split, comm):
             split = sanitize_axis(gshape, split)
             local = np.asarray(data[_hyperslab(gshape, split, comm)])
     else:
-        from scipy.io import netcdf_file
-
-        with netcdf_file(path, "r", mmap=True) as handle:
-            data = handle.variables[variable].data
-            gshape = tuple(data.shape)
-            split = sanitize_axis(gshape, split)
-            local = np.array(data[_hyperslab(gshape, split, comm)])
-            del data  # the mmap must not be referenced when the file closes
+        # classic CDF-1 / CDF-2 / CDF-5: read this rank's hyperslab through a memory map
+        shape, dt, begin, recsize = _ncc.layout(_ncc.parse(path), variable)
+        gshape = tuple(shape)
+        split = sanitize_axis(gshape, split)
+        mm = _ncc.memmap(path, shape, dt, begin, recsize, mode="r")
+        local = np.array(mm[_hyperslab(gshape, split, comm)])
+        del mm
     return local, gshape, split
 
 
-_NC_TYPES = {1: np.dtype("i1"), 2: np.dtype("S1"), 3: np.dtype(">i2"), 4: np.dtype(">i4"), 5: np.dtype(">f4"),
-             6: np.dtype(">f8")}
 _NC_WRITE_MODES = ("w", "a", "r+")
-
-
-def _nc_classic_layout(path: str, variable: str):
-    """Parse the header of a classic netCDF file (CDF-1 / CDF-2) and return the data layout of
-    ``variable``: (shape with the current record count, big-endian dtype, begin offset, record
-    stride in bytes or None for a fixed-size variable, numrecs offset in the file)."""
-    import struct
-
-    with open(path, "rb") as f:
-        buf = f.read(1 << 16)
-        pos = [0]
-
-        def need(n):
-            nonlocal buf
-            while pos[0] + n > len(buf):
-                more = f.read(1 << 16)
-                if not more:
-                    raise ValueError("truncated netCDF header")
-                buf += more
-
-        def i4():
-            need(4)
-            v = struct.unpack(">i", buf[pos[0]: pos[0] + 4])[0]
-            pos[0] += 4
-            return v
-
-        def i8():
-            need(8)
-            v = struct.unpack(">q", buf[pos[0]: pos[0] + 8])[0]
-            pos[0] += 8
-            return v
-
-        def name():
-            n = i4()
-            need(n + (-n) % 4)
-            v = buf[pos[0]: pos[0] + n].decode("utf-8")
-            pos[0] += n + (-n) % 4
-            return v
-
-        def skip_atts():
-            tag, n = i4(), i4()
-            for _ in range(n if tag else 0):
-                name()
-                t, cnt = i4(), i4()
-                size = cnt * _NC_TYPES[t].itemsize
-                need(size + (-size) % 4)
-                pos[0] += size + (-size) % 4
-
-        need(4)
-        if buf[:3] != b"CDF" or buf[3] not in (1, 2):
-            raise ValueError("{} is not a classic netCDF file".format(path))
-        off64 = buf[3] == 2
-        pos[0] = 4
-        numrecs_at = 4
-        numrecs = i4()
-        tag, nd = i4(), i4()
-        dims = [(name(), i4()) for _ in range(nd if tag else 0)]
-        skip_atts()
-        tag, nv = i4(), i4()
-        vars_ = {}
-        for _ in range(nv if tag else 0):
-            vn = name()
-            ndv = i4()
-            dimids = [i4() for _ in range(ndv)]
-            skip_atts()
-            t, vsize = i4(), i4()
-            begin = i8() if off64 else i4()
-            vars_[vn] = (dimids, t, vsize, begin)
-    if variable not in vars_:
-        raise KeyError(variable)
-    dimids, t, vsize, begin = vars_[variable]
-    is_rec = bool(dimids) and dims[dimids[0]][1] == 0
-    recsize = sum(v[2] for v in vars_.values() if v[0] and dims[v[0][0]][1] == 0)
-    if sum(1 for v in vars_.values() if v[0] and dims[v[0][0]][1] == 0) == 1:
-        recsize = vsize  # a single record variable is not padded per record
-    shape = tuple(numrecs if (k == 0 and is_rec) else dims[d][1] for k, d in enumerate(dimids))
-    return shape, _NC_TYPES[t], begin, (recsize if is_rec else None), numrecs_at
-
-
-def _nc_memmap(path: str, shape, dtype, begin: int, recsize: Optional[int]):
-    """Writable strided view of a classic variable's data (records at ``recsize`` strides)."""
-    if recsize is None:
-        return np.memmap(path, dtype=dtype, mode="r+", offset=begin, shape=shape)
-    nrec = shape[0]
-    inner = int(np.prod(shape[1:])) if len(shape) > 1 else 1
-    if nrec == 0:
-        return np.zeros(shape, dtype=dtype)
-    raw = np.memmap(path, dtype=np.uint8, mode="r+", offset=begin, shape=((nrec - 1) * recsize + inner * dtype.itemsize,))
-    strides = (recsize,) + tuple(int(np.prod(shape[k + 1:])) * dtype.itemsize for k in range(1, len(shape)))
-    return np.ndarray(shape, dtype=dtype, buffer=raw, strides=strides)
 
 
 def _normalize_file_slices(file_slices, ndim: int) -> tuple:
@@ -572,8 +453,9 @@ def save_netcdf(data: DNDarray, path: str, variable: str, mode: str = "w", dimen
     data is written to, e.g. a record range of an existing unlimited variable).
 
     With netCDF4: rank 0 defines dimensions / the variable, then the ranks write their slabs in
-    turn. Without it: a classic netCDF (CDF-2) file; rank 0 defines the structure (new file, or an
-    added dimension / variable in an existing file through ``scipy.io.netcdf_file``), grows the
+    turn. Without it: a classic netCDF file (CDF-2, or CDF-5 when a variable needs int64 / unsigned /
+    bool storage - never a lossy cast; ``_ncclassic``); rank 0 defines the structure (new file, or an
+    added dimension / variable in an existing file, rewritten with its data), grows the
     record count of an unlimited variable to what ``file_slices`` addresses, and EVERY rank then
     writes its slab in place through a memory map of the variable's data (record variables as a
     strided view) - parallel, no gather. Classic files allow one unlimited dimension, the first of a
@@ -631,27 +513,22 @@ def save_netcdf(data: DNDarray, path: str, variable: str, mode: str = "w", dimen
             comm.Barrier()
         _exception_barrier(comm, exc)
         return
-    np_dtype = np.dtype(local.dtype)
-    if np_dtype == np.dtype("i8"):
-        np_dtype = np.dtype("i4")
-    elif np_dtype == np.dtype("bool") or np_dtype == np.dtype("u1"):
-        np_dtype = np.dtype("i1")
-    elif np_dtype == np.dtype("f2"):
-        np_dtype = np.dtype("f4")
+    # lossless storage type (int64 / unsigned / bool need CDF-5; complex raises)
+    nc_type = _ncc.nc_type_for(local.dtype)
     layout = None
     # rank 0 may truncate / restructure the file: every rank must be done with earlier reads of it
     comm.Barrier()
     if comm.rank == 0:
         try:
-            layout = _nc_define_classic(path, variable, mode, dimension_names, data.gshape, np_dtype, is_unlimited,
+            layout = _nc_define_classic(path, variable, mode, dimension_names, data.gshape, nc_type, is_unlimited,
                                         key)
         except Exception as e:
             exc = e
     _exception_barrier(comm, exc)
-    shape, dt, begin, recsize, _ = comm.bcast(layout, root=0)
+    shape, dt, begin, recsize = comm.bcast(layout, root=0)
     try:
         if (data.is_distributed() or comm.rank == 0) and local.size:
-            mm = _nc_memmap(path, shape, dt, begin, recsize)
+            mm = _ncc.memmap(path, shape, dt, begin, recsize)
             full = _file_region(shape, key, data.gshape, recsize is not None)
             mm[_sub_region(full, data, lsl)] = local.astype(dt)
             if isinstance(mm, np.memmap):
@@ -704,37 +581,17 @@ def _sub_region(full, data: DNDarray, lsl) -> tuple:
     return tuple(key)
 
 
-def _nc_define_classic(path, variable, mode, dims, gshape, np_dtype, is_unlimited, key):
+def _nc_define_classic(path, variable, mode, dims, gshape, nc_type, is_unlimited, key):
     """Rank 0: create / extend the classic file so that ``variable`` exists and holds the region
-    ``key`` addresses; returns its data layout."""
-    import os
-
+    ``key`` addresses; returns its data layout (shape, dtype, begin, record stride)."""
     exists = os.path.exists(path)
-    if mode == "w" or not exists:
-        if mode == "r+" and not exists:
-            raise FileNotFoundError(path)
-        if not is_unlimited:
-            header, begin = _netcdf3_header(variable, dims, gshape, np_dtype)
-            nbytes = int(np.prod(gshape)) * np_dtype.itemsize
-            with open(path, "wb") as f:
-                f.write(header)
-                f.truncate(begin + nbytes + ((-nbytes) % 4))
-            return _nc_classic_layout(path, variable)
-        if os.path.exists(path):
-            os.unlink(path)
-    from scipy.io import netcdf_file
-
-    with netcdf_file(path, "a" if os.path.exists(path) else "w", version=2, mmap=False) as h:
-        if variable not in h.variables:
-            for i, (name, size) in enumerate(zip(dims, gshape)):
-                if name not in h.dimensions:
-                    h.createDimension(name, None if (is_unlimited and i == 0) else size)
-            v = h.createVariable(variable, np_dtype.newbyteorder("="), tuple(dims))
-            if dims and h.dimensions[dims[0]] is None:
-                # one zero record, so the header carries the record size (scipy writes vsize from data)
-                v[0] = np.zeros(tuple(gshape[1:]), dtype=np_dtype.newbyteorder("="))
-    shape, dt, begin, recsize, nr_at = _nc_classic_layout(path, variable)
-    if recsize is not None:
+    if mode == "r+" and not exists:
+        raise FileNotFoundError(path)
+    h = _ncc.parse(path) if (exists and mode != "w") else None
+    if h is None or h.var(variable) is None:
+        h = _ncc.write_with_variable(path, h, variable, list(dims), gshape, nc_type, is_unlimited)
+    v = h.var(variable)
+    if h.is_record(v):
         # grow the record count to what the write addresses (zero-filled records)
         k0 = key[0]
         need = gshape[0]
@@ -744,18 +601,8 @@ def _nc_define_classic(path, variable, mode, dims, gshape, np_dtype, is_unlimite
             need = start + step * (gshape[0] - 1) + 1 if gshape[0] else start
         elif isinstance(k0, (int, np.integer)):
             need = int(k0) + 1
-        if need > shape[0]:
-            import struct
-
-            with open(path, "r+b") as f:
-                f.seek(nr_at)
-                f.write(struct.pack(">i", int(need)))
-                end = begin + need * recsize
-                f.seek(0, 2)
-                if f.tell() < end:
-                    f.truncate(end + (-end) % 4)
-            shape, dt, begin, recsize, nr_at = _nc_classic_layout(path, variable)
-    return shape, dt, begin, recsize, nr_at
+        h = _ncc.grow_records(path, h, need)
+    return _ncc.layout(h, variable)
 
 
 DNDarray.save_netcdf = lambda self, path, variable, mode="w", **kwargs: save_netcdf(self, path, variable, mode, **kwargs)

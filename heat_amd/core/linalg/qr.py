@@ -251,9 +251,17 @@ def _qr_complete(a: DNDarray, dtype, calc_q: bool) -> QR:
     d = torch.sign(torch.diagonal(R))
     d = torch.where(d == 0, torch.ones_like(d), d)
     R = d.unsqueeze(1) * R
-    if m > kmax:
-        R = torch.cat([R, R.new_zeros((m - kmax, n))], 0)
-    Rd = factories.array(R, split=a.split, device=a.device, comm=comm, dtype=dtype)
+    # R is m x n with zero rows past kmax: build only this rank's block of it (a replicated
+    # m x n tensor would be as large as the whole input on every rank)
+    off, lshape, _ = comm.chunk((m, n), a.split)
+    Rl = R.new_zeros(lshape)
+    if a.split == 1:
+        Rl[:kmax] = R[:, off: off + lshape[1]]
+    else:
+        lo, hi = off, min(off + lshape[0], kmax)
+        if hi > lo:
+            Rl[: hi - lo] = R[lo:hi]
+    Rd = DNDarray(Rl, (m, n), dtype, a.split, a.device, comm, True)
     if not calc_q:
         return QR(None, Rd)
     Q = torch.zeros((m_r, m), dtype=tt, device=local.device)

@@ -131,6 +131,28 @@ def _fill_torch(e0: int, n: int, counter: int, key: int, bits: int, dist: str, l
     return _kundu(u) if dist == "normal" else u
 
 
+_KUNDU_TABLE_DEVICES = set()
+
+
+def _ensure_kundu_table(L, tdev) -> None:
+    """Upload (once per device) the host-computed Kundu values for u within 2^-5 of 1, where the
+    device's fast transform defers to them (``ops/csrc/threefry.hip``): computed with THIS module's
+    torch formula, so the device matches the host path exactly where rounding decides the value."""
+    import ctypes
+
+    idx = tdev.index if tdev.index is not None else torch.cuda.current_device()
+    if idx in _KUNDU_TABLE_DEVICES:
+        return
+    count = L.ha_threefry_kundu_table_size()
+    v23 = 8388607 - torch.arange(count, dtype=torch.int64)
+    tab = _kundu(v23.to(torch.float32) * (1.0 / 8388608.0)).to(torch.float32).contiguous()
+    with torch.cuda.device(idx):
+        rc = L.ha_threefry_set_kundu_table(ctypes.c_void_p(tab.data_ptr()), count)
+    if rc != 0:
+        raise RuntimeError("uploading the Kundu table failed (code {})".format(rc))
+    _KUNDU_TABLE_DEVICES.add(idx)
+
+
 def _kundu(values: torch.Tensor) -> torch.Tensor:
     inner = 1 - values ** 0.0775
     tiny = torch.finfo(inner.dtype).tiny
@@ -173,6 +195,8 @@ def _generate(shape, dtype, split, device, comm, dist: str, low: int = 0, span: 
             import ctypes
 
             L = lib()
+            if bits == 32 and dist == "normal":
+                _ensure_kundu_table(L, tdev)
             rc = L.ha_threefry_fill(ctypes.c_void_p(out.data_ptr()), e0, n, counter & _M64, (counter >> 64) & _M64,
                                     __seed & _M64, bits, _DIST[dist], float(low), float(span),
                                     ctypes.c_void_p(stream_ptr(tdev)))

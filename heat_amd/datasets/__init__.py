@@ -3,12 +3,13 @@ The reference's data fixtures (``heat/datasets/iris.{csv,h5,nc}``, ``diabetes.h5
 train/test CSVs) and synthetic generators.
 
 The fixture files are not shipped in this repository. :func:`fixture_path` finds them in
-``$HEAT_DATASETS_DIR``, ``heat_amd/datasets/data`` or a Heat checkout (``/root/reference/heat/datasets``)
+``$HEAT_DATASETS_DIR`` (e.g. a Heat checkout's ``heat/datasets``) or ``heat_amd/datasets/data``
 and :func:`load_fixture` reads one in parallel through ``ht.load`` (CSV / HDF5 / NetCDF, split as
 asked). :func:`iris` and :func:`diabetes` return the real fixture when one is found
 (``synthetic=False``, the default) and otherwise a deterministic stand-in of the same shape and
 character (3 Gaussian classes of 50 x 4 with the class means / spreads of Fisher's iris
-measurements; a 442 x 10 linear-regression problem), identical on every rank for any process count.
+measurements; a 442 x 11 linear-regression problem whose first column is the intercept, like the
+fixture), identical on every rank for any process count.
 """
 from __future__ import annotations
 
@@ -43,7 +44,6 @@ def _search_dirs():
     env = os.environ.get("HEAT_DATASETS_DIR")
     dirs = [env] if env else []
     dirs.append(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data"))
-    dirs.append("/root/reference/heat/datasets")
     return dirs
 
 
@@ -108,13 +108,13 @@ def diabetes(split: Optional[int] = 0, device=None, comm=None, seed: int = 0,
              synthetic: bool = False) -> Tuple[DNDarray, DNDarray]:
     """442 x 11 features (first column = 1 for the Lasso intercept) and a (442, 1) target column:
     the reference's ``diabetes.h5`` (datasets ``x`` and ``y``) when available, else a synthetic
-    problem of the same layout (442 x 10)."""
+    problem of the same layout (442 x 11, column 0 the intercept)."""
     if not synthetic and fixture_path("diabetes.h5") is not None:
         X = load_fixture("diabetes.h5", "x", split=split, device=device, comm=comm)
         y = load_fixture("diabetes.h5", "y", split=split if split in (None, 0) else None, device=device, comm=comm)
         return X, ht.reshape(y, (-1, 1), new_split=y.split)
     X, y = make_regression(442, 10, noise=0.5, seed=seed, as_numpy=True)
-    X[:, 0] = 1.0
+    X = np.concatenate([np.ones((442, 1), np.float32), X], axis=1)
     return ht.array(X, split=split, device=device, comm=comm), ht.array(y, split=split, device=device, comm=comm)
 
 

@@ -24,10 +24,24 @@ from .. import optim
 __all__ = ["DataParallel", "DataParallelMultiGPU"]
 
 
+class _Done:
+    """Completed request (world of one)."""
+
+    def Wait(self) -> None:
+        pass
+
+
 class _Bucket:
     def __init__(self, params: List[torch.nn.Parameter]):
         self.params = params
         self.ready = 0
+        self.reported = set()
+        self.flat = None
+        self.req = None
+
+    def reset(self) -> None:
+        self.ready = 0
+        self.reported = set()
         self.flat = None
         self.req = None
 
@@ -89,50 +103,97 @@ class DataParallel(tnn.Module):
                 self._bucket_of[id(p)] = bi
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in params]
         self._pending = False
+        self._callback_queued = False
 
     # ---------------------------------------------------------------- gradient synchronisation
+    def _fire(self, b: _Bucket) -> None:
+        """Launch the (async) all-reduce of one bucket. Parameters that produced no gradient on
+        this rank contribute zeros, so a bucket is never left waiting for a gradient that will not
+        come (reference: per-parameter hooks, ``nn/data_parallel.py:223-278``, average exactly the
+        parameters that received a gradient)."""
+        grads = [q.grad.reshape(-1) if (id(q) in b.reported and q.grad is not None)
+                 else torch.zeros(q.numel(), device=q.device, dtype=q.dtype) for q in b.params]
+        flat = torch.cat(grads).to(self.grad_dtype)  # a copy: a zero_grad() before the deferred
+        flat.mul_(1.0 / self.comm.size)              # update cannot erase it
+        b.flat = flat
+        b.req = self.comm.Iallreduce(MPI.IN_PLACE, flat, MPI.SUM) if self.comm.is_distributed() else _Done()
+
+    def _on_backward_end(self) -> None:
+        """Queued on the autograd engine by the first gradient hook of a backward pass: buckets
+        with a parameter that received no gradient are flushed here, in bucket order (the same on
+        every rank as long as every rank uses the same parameters - the reference's and DDP's
+        contract), while the gradients are still in place."""
+        self._callback_queued = False
+        for b in self._buckets:
+            if b.req is None and b.reported:
+                self._fire(b)
+
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
-        if not self.comm.is_distributed() or not self.module.training:
+        if not self.module.training:
             return
+        if not (self.comm.is_distributed() or not self.blocking_parameter_updates):
+            return  # world of one, blocking: the local gradient is the average
         b = self._buckets[self._bucket_of[id(p)]]
+        self._pending = True
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._on_backward_end)
+        if id(p) in b.reported:
+            # second backward before the update (gradient accumulation): the flush in
+            # _finish_gradient_sync re-sends the accumulated gradient
+            if b.req is not None:
+                b.req.Wait()
+                b.req, b.flat = None, None
+            return
+        b.reported.add(id(p))
         b.ready += 1
         if b.ready == len(b.params):
-            grads = [q.grad.reshape(-1) if q.grad is not None else torch.zeros(q.numel(), device=q.device,
-                                                                              dtype=q.dtype) for q in b.params]
-            flat = torch.cat(grads).to(self.grad_dtype)
-            flat.mul_(1.0 / self.comm.size)
-            b.flat = flat
-            b.req = self.comm.Iallreduce(MPI.IN_PLACE, flat, MPI.SUM)
-            b.ready = 0
-            self._pending = True
+            self._fire(b)
 
     @torch.no_grad()
-    def _finish_gradient_sync(self) -> None:
+    def _finish_gradient_sync(self, inplace: bool = True) -> None:
         if not self._pending:
             return
+        # normally done at the end of backward already (_on_backward_end)
+        for b in self._buckets:
+            if b.req is None and b.reported:
+                self._fire(b)
         for b in self._buckets:
             if b.req is None:
+                b.reset()
                 continue
             b.req.Wait()
             off = 0
             for q in b.params:
                 n = q.numel()
-                g = b.flat[off: off + n].reshape(q.shape).to(q.dtype)
-                if q.grad is None:
-                    q.grad = g.clone()
-                else:
-                    q.grad.copy_(g)
+                if id(q) in b.reported:
+                    g = b.flat[off: off + n].reshape(q.shape).to(q.dtype)
+                    if q.grad is None or not inplace:
+                        q.grad = g.clone()
+                    else:
+                        q.grad.copy_(g)
+                # a parameter without a gradient keeps grad None (the optimizer skips it, as in
+                # the reference where no hook fires for it)
                 off += n
-            b.req = None
-            b.flat = None
+            b.reset()
         self._pending = False
 
     def _deferred_update(self) -> None:
-        self._finish_gradient_sync()
+        """Non-blocking mode: apply the previous step's averaged gradients and optimizer step at
+        the start of the next forward. The ``.grad`` the user left (usually None after
+        ``zero_grad()``) is restored afterwards, so the coming backward does not accumulate onto
+        the previous step's average (the reference's hooks likewise keep the averaged gradient
+        out of the local accumulation, ``nn/data_parallel.py:255-276``)."""
+        if not self._pending and not any(o.update_next for o in self._dp_optimizers):
+            return
+        stash = [(q, q.grad) for q in self.module.parameters()]
+        self._finish_gradient_sync(inplace=False)
         for o in self._dp_optimizers:
             if o.update_next:
                 o.torch_optimizer.step()
                 o.update_next = False
+        for q, g in stash:
+            q.grad = g
 
     def __setattr__(self, name: str, value: Any) -> None:
         # leaving training mode finalises a pending (non-blocking) update, like the reference

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 import threading
 
 import torch
@@ -60,9 +61,18 @@ def lib():
             if _build.needs_build():
                 try:
                     path = _build.build()
-                except Exception as e:  # no hipcc on this machine: use a prebuilt library if present
-                    if not os.path.exists(_build.LIBPATH):
+                except Exception as e:
+                    # a prebuilt library exists but is OLDER than the sources: using it may call a
+                    # changed C signature with the old ABI. Say so loudly (naming what failed), and
+                    # refuse under HEAT_STRICT_BUILD=1.
+                    if not os.path.exists(_build.LIBPATH) or os.environ.get("HEAT_STRICT_BUILD") == "1":
                         raise
+                    stale = [os.path.basename(s) for s in _build.stale_sources()]
+                    warnings.warn("heat_amd: rebuilding the native kernels failed ({}); loading the STALE "
+                                  "library {} (older than {}). Kernels whose C signature changed may be "
+                                  "called with the wrong ABI.".format(str(e).strip()[:2000], _build.LIBPATH,
+                                                                       ", ".join(stale) or "the build script"),
+                                  RuntimeWarning, stacklevel=2)
             handle = ctypes.CDLL(path)
             sigs = dict(_SIGNATURES)
             try:

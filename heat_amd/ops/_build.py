@@ -52,11 +52,16 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found; the native kernels need ROCm's hipcc")
 
 
-def needs_build() -> bool:
+def stale_sources() -> list:
+    """Sources / headers (and this script) newer than the built library."""
     if not os.path.exists(LIBPATH):
-        return True
+        return sources() + headers()
     t = os.path.getmtime(LIBPATH)
-    return any(os.path.getmtime(s) > t for s in sources() + headers() + [__file__])
+    return [s for s in sources() + headers() + [__file__] if os.path.getmtime(s) > t]
+
+
+def needs_build() -> bool:
+    return bool(stale_sources())
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -86,7 +91,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     except subprocess.CalledProcessError as e:
         os.unlink(tmp)
         msg = e.stderr.decode() if e.stderr else ""
-        raise RuntimeError("building the native kernels failed:\n" + msg) from e
+        src = next((a for a in e.cmd if str(a).endswith(".hip")), None)
+        where = " ({})".format(os.path.basename(src)) if src else ""
+        raise RuntimeError("building the native kernels failed{}:\n{}".format(where, msg)) from e
     finally:
         shutil.rmtree(objdir, ignore_errors=True)
     os.replace(tmp, LIBPATH)

@@ -150,11 +150,22 @@ HA_EXPORT int ha_comm_alltoallv(void* comm, int nranks, int rank, const void* se
           hipSuccess)
     return HA_LAUNCH;
   if (g_rccl.GroupStart() != 0) return HA_LAUNCH;
+  // every enqueue is checked; the group is always closed (an open group would swallow the next
+  // collective), and the first failure is returned as 100 + the RCCL code
+  rcclResult first = 0;
   for (int k = 1; k < nranks; ++k) {
     // pairwise schedule: at step k send to rank+k, receive from rank-k (every link busy both ways)
     const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
-    if (send_bytes[to] > 0) g_rccl.Send(sb + send_off[to], (size_t)send_bytes[to], kUint8, to, comm, s);
-    if (recv_bytes[from] > 0) g_rccl.Recv(rb + recv_off[from], (size_t)recv_bytes[from], kUint8, from, comm, s);
+    if (send_bytes[to] > 0) {
+      const rcclResult r = g_rccl.Send(sb + send_off[to], (size_t)send_bytes[to], kUint8, to, comm, s);
+      if (r != 0 && first == 0) first = r;
+    }
+    if (recv_bytes[from] > 0) {
+      const rcclResult r = g_rccl.Recv(rb + recv_off[from], (size_t)recv_bytes[from], kUint8, from, comm, s);
+      if (r != 0 && first == 0) first = r;
+    }
   }
-  return g_rccl.GroupEnd() == 0 ? HA_OK : HA_LAUNCH;
+  const rcclResult e = g_rccl.GroupEnd();
+  if (first != 0) return 100 + first;
+  return e == 0 ? HA_OK : 100 + e;
 }

@@ -58,6 +58,28 @@ __device__ __forceinline__ float kundu_f(float u) {
   return (logf(-logf(inner + tiny) + tiny) - 1.0821f) * (1.0f / 0.3807f);
 }
 
+// Fast single-precision Kundu transform. u^0.0775 = exp2(0.0775 log2 u) and the two logs go
+// through the hardware v_log_f32 / v_exp_f32 (~1 ulp) instead of the precise powf / logf (tens of
+// instructions each), which held randn at 0.75 TB/s. The transform amplifies an error of w = u^0.0775
+// by 1 / (1 - w): where 1 - u < 2^-5 the value comes from a table (2^18 entries, 1 MB, L2-resident;
+// u only takes the values k 2^-23) that the HOST computes with its own torch formula and uploads
+// once per device (ha_threefry_set_kundu_table), so the result equals the host path exactly where
+// the rounding of u^0.0775 decides it, and within a few ulp elsewhere.
+constexpr int KUNDU_TAB_BITS = 18;
+__device__ float g_kundu_tab[1 << KUNDU_TAB_BITS];  // [i] = kundu(u) at u = (2^23 - 1 - i) 2^-23
+static bool g_tab_ready[64] = {};
+
+__device__ __forceinline__ float kundu_fast(uint32_t v23) {
+  const float u = (float)v23 * (1.0f / 8388608.0f);
+  const float ln2 = 0.693147180559945f, tiny = 1.17549435e-38f;
+  const float w = __builtin_amdgcn_exp2f(0.0775f * __builtin_amdgcn_logf(u));  // u = 0: exp2(-inf) = 0
+  const float l1 = -ln2 * __builtin_amdgcn_logf(1.f - w + tiny);
+  float r = (ln2 * __builtin_amdgcn_logf(l1 + tiny) - 1.0821f) * (1.0f / 0.3807f);
+  const uint32_t mi = 8388607u - v23;  // 2^23 (1 - u) - 1
+  if (mi < (1u << KUNDU_TAB_BITS)) r = g_kundu_tab[mi];
+  return r;
+}
+
 __device__ __forceinline__ double kundu_d(double u) {
   const double inner = 1.0 - pow(u, 0.0775);
   const double tiny = 2.2250738585072014e-308;
@@ -88,8 +110,8 @@ __global__ __launch_bounds__(256) void tf_fill32(void* __restrict__ out, int64_t
         if (r < 0) r += span;
         reinterpret_cast<int32_t*>(out)[i] = (int32_t)(r + low);
       } else {
-        const float u = (float)(v & 0x7FFFFFu) * (1.0f / 8388608.0f);
-        reinterpret_cast<float*>(out)[i] = dist == DIST_NORMAL ? kundu_f(u) : u;
+        const uint32_t v23 = v & 0x7FFFFFu;
+        reinterpret_cast<float*>(out)[i] = dist == DIST_NORMAL ? kundu_fast(v23) : (float)v23 * (1.0f / 8388608.0f);
       }
     }
   }
@@ -129,6 +151,19 @@ __global__ __launch_bounds__(256) void tf_fill64(void* __restrict__ out, int64_t
 
 }  // namespace
 
+HA_EXPORT int ha_threefry_kundu_table_size() { return 1 << KUNDU_TAB_BITS; }
+
+// host_tab: ha_threefry_kundu_table_size() floats, [i] = kundu((2^23 - 1 - i) 2^-23), for the
+// current device (synchronous copy)
+HA_EXPORT int ha_threefry_set_kundu_table(const float* host_tab, int count) {
+  if (!host_tab || count != (1 << KUNDU_TAB_BITS)) return HA_BAD_ARG;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return HA_LAUNCH;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_kundu_tab), host_tab, sizeof(float) * count) != hipSuccess) return HA_LAUNCH;
+  g_tab_ready[dev] = true;
+  return HA_OK;
+}
+
 // bits: 32 or 64. For bits == 32 only counter_lo (the counter mod 2^64) is used.
 HA_EXPORT int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counter_lo, uint64_t counter_hi, uint64_t seed,
                                int bits, int dist, double low, double span, void* stream) {
@@ -137,6 +172,10 @@ HA_EXPORT int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counte
   int64_t blocks = (pairs + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipStream_t s = (hipStream_t)stream;
+  if (bits == 32 && dist == DIST_NORMAL) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_tab_ready[dev]) return HA_UNSUPPORTED;
+  }
   if (bits == 32) {
     hipLaunchKernelGGL(tf_fill32, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo,
                        (uint32_t)(seed & 0x7FFFFFFFull), dist, (int64_t)low, (int64_t)span);

@@ -205,6 +205,29 @@ def kmeans_assign(X: torch.Tensor, C: torch.Tensor, want_mind: bool = True,
 kmeans_assign.last_rechecked = None
 
 
+def _lex_key(d: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """int64 keys ordering non-negative float32 distances, equal distances by index: the float
+    bits of d >= 0 are monotone as integers, so (bits << 32) | idx sorts lexicographically."""
+    bits = (d.float() + 0.0).contiguous().view(torch.int32).to(torch.int64)   # + 0.0: -0.0 -> +0.0
+    return (bits << 32) | (idx.to(torch.int64) & 0xFFFFFFFF)
+
+
+def _lex_split(key: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    d = (key >> 32).to(torch.int32).view(torch.float32)
+    i = (key & 0xFFFFFFFF)
+    return d, torch.where(i == 0xFFFFFFFF, torch.full_like(i, -1), i)
+
+
+def _topk_lex(d: torch.Tensor, idx: Optional[torch.Tensor], k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """k smallest distances per row with ties ordered by (global) index - the same answer for any
+    blocking of the candidates, hence for any number of ranks."""
+    if idx is None:
+        idx = torch.arange(d.shape[1], device=d.device).expand(d.shape[0], -1)
+    key = _lex_key(d, idx)
+    key = torch.topk(key, k, dim=1, largest=False).values if k < key.shape[1] else torch.sort(key, dim=1).values
+    return _lex_split(key)
+
+
 def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPoints] = None,
              exact_distances: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
     """The ``k`` nearest rows of ``T`` for every row of ``Q``: (squared distances [nq, k] ascending,
@@ -240,15 +263,14 @@ def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPo
         else:
             dist = dist.permute(1, 0, 2).reshape(nq, splits * k)
             idx = idx.permute(1, 0, 2).reshape(nq, splits * k)
-            dist, sel = torch.topk(dist, k, dim=1, largest=False)
-            idx = torch.gather(idx, 1, sel).long()
+            dist, idx = _topk_lex(dist, idx, k)
     else:
         kk = min(k, nt)
         step = max(1, (1 << 28) // max(nt, 1))
         ds, ids = [], []
         for q0 in range(0, nq, step):
             d = cdist(Q[q0: q0 + step].float(), T.float(), "sqeuclidean", exact=True)
-            dv, di = torch.topk(d, kk, dim=1, largest=False)
+            dv, di = _topk_lex(d, None, kk)   # equal distances ordered by index
             ds.append(dv)
             ids.append(di)
         dist, idx = torch.cat(ds), torch.cat(ids)
@@ -263,9 +285,9 @@ def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPo
             nb = T[ib.clamp(min=0)].float()
             d = ((Q[q0: q0 + step].float().unsqueeze(1) - nb) ** 2).sum(-1)
             d = torch.where(ib >= 0, d, torch.full_like(d, float("inf")))
-            d, order = torch.sort(d, dim=1)
+            d, i = _topk_lex(d, ib, k)
             dist[q0: q0 + step] = d
-            idx[q0: q0 + step] = torch.gather(ib, 1, order)
+            idx[q0: q0 + step] = i
     return dist, idx
 
 

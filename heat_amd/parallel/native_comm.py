@@ -20,12 +20,58 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-__all__ = ["NativeComm", "enabled", "rccl_path"]
+__all__ = ["NativeComm", "enabled", "rccl_path", "allgatherv_plan", "alltoallv_plan", "simulate_alltoallv"]
 
 # ncclDataType_t / ncclRedOp_t codes
 _DT = {torch.int8: 0, torch.uint8: 1, torch.bool: 1, torch.int32: 2, torch.int64: 4, torch.float16: 6,
        torch.float32: 7, torch.float64: 8, torch.bfloat16: 9}
 _OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+
+
+# ------------------------------------------------------------------ byte plans (pure, CPU-testable)
+def allgatherv_plan(counts: Sequence[int], rank: int, row_bytes: int):
+    """Arguments of ``ha_comm_alltoallv`` for an all-gather of unequal row blocks: this rank sends
+    its whole block (``counts[rank]`` rows, offset 0) to every peer and receives rank q's block at
+    the byte offset of q's rows in the concatenation. Returns int64 arrays (sb, so, rb, ro)."""
+    size = len(counts)
+    own = int(counts[rank]) * int(row_bytes)
+    sb = np.full(size, own, dtype=np.int64)
+    so = np.zeros(size, dtype=np.int64)
+    rb = np.asarray([int(c) * int(row_bytes) for c in counts], dtype=np.int64)
+    ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.int64) if size else np.zeros(0, np.int64)
+    return sb, so, rb, ro
+
+
+def alltoallv_plan(send_bytes: Sequence[int], recv_bytes: Sequence[int]):
+    """Arguments of ``ha_comm_alltoallv`` for blocks stored back to back in rank order on both
+    sides. Returns int64 arrays (sb, so, rb, ro)."""
+    sb = np.asarray(send_bytes, dtype=np.int64)
+    rb = np.asarray(recv_bytes, dtype=np.int64)
+    so = np.concatenate([[0], np.cumsum(sb)[:-1]]).astype(np.int64) if sb.size else np.zeros(0, np.int64)
+    ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.int64) if rb.size else np.zeros(0, np.int64)
+    return sb, so, rb, ro
+
+
+def simulate_alltoallv(sends, plans, recv_sizes):
+    """Host model of ``ha_comm_alltoallv`` run by every rank at once (``ops/csrc/comm.hip``):
+    rank r's ``sends[r]`` (uint8 array) and ``plans[r]`` = (sb, so, rb, ro); returns every rank's
+    receive buffer (``recv_sizes[r]`` bytes). Raises where the real exchange would fail or hang: a
+    local block whose send and receive sizes differ (HA_BAD_ARG), or a send of rank r to q whose
+    size differs from the receive q posted for r (mismatched RCCL p2p)."""
+    size = len(sends)
+    out = [np.zeros(int(n), dtype=np.uint8) for n in recv_sizes]
+    for r in range(size):
+        sb, so, rb, ro = plans[r]
+        if sb[r] != rb[r]:
+            raise ValueError("rank {}: local block sends {} bytes, receives {}".format(r, sb[r], rb[r]))
+        for q in range(size):
+            qsb, qso, qrb, qro = plans[q]
+            if qsb[r] != rb[q]:
+                raise ValueError("rank {} expects {} bytes from {}, which sends {}".format(r, rb[q], q, qsb[r]))
+            if rb[q] < 0 or ro[q] + rb[q] > out[r].size or qso[r] + qsb[r] > sends[q].size:
+                raise ValueError("rank {}: block from {} out of bounds".format(r, q))
+            out[r][ro[q]: ro[q] + rb[q]] = sends[q][qso[r]: qso[r] + qsb[r]]
+    return out
 
 
 def enabled() -> bool:
@@ -116,11 +162,7 @@ class NativeComm:
 
         row = int(np.prod(moved.shape[1:])) * moved.element_size()
         out = torch.empty((sum(counts),) + tuple(moved.shape[1:]), dtype=moved.dtype, device=moved.device)
-        own = counts[self.rank] * row
-        sb = np.full(self.size, own, dtype=np.int64)
-        so = np.zeros(self.size, dtype=np.int64)
-        rb = np.asarray([c * row for c in counts], dtype=np.int64)
-        ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.int64)
+        sb, so, rb, ro = allgatherv_plan(counts, self.rank, row)
         p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
         check(self.L.ha_comm_alltoallv(self.handle, self.size, self.rank, ctypes.c_void_p(moved.data_ptr()), p(sb),
                                        p(so), ctypes.c_void_p(out.data_ptr()), p(rb), p(ro), self._stream(moved)),
@@ -140,10 +182,7 @@ class NativeComm:
         """Personalised exchange of raw bytes (blocks back to back in rank order on both sides)."""
         from ..ops import check
 
-        sb = np.asarray(send_bytes, dtype=np.int64)
-        rb = np.asarray(recv_bytes, dtype=np.int64)
-        so = np.concatenate([[0], np.cumsum(sb)[:-1]]).astype(np.int64)
-        ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.int64)
+        sb, so, rb, ro = alltoallv_plan(send_bytes, recv_bytes)
         p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
         ref = recv if recv.numel() else send
         check(self.L.ha_comm_alltoallv(self.handle, self.size, self.rank, ctypes.c_void_p(send.data_ptr()), p(sb),

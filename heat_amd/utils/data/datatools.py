@@ -51,6 +51,11 @@ class DataLoader:
         return self.DataLoader.__iter__()
 
     def __len__(self) -> int:
+        if isinstance(self.dataset, partial_dataset.PartialH5Dataset):
+            # batches per epoch over the rank's share (len(dataset) is the whole file)
+            bs = self.DataLoader.batch_size
+            n = self.dataset.lcl_full_sz
+            return n // bs if self.DataLoader.drop_last else -(-n // bs)
         return len(self.DataLoader)
 
     def _full_dataset_shuffle_iter(self):

@@ -1,8 +1,25 @@
 """
 Streaming HDF5 datasets (reference ``heat/utils/data/partial_dataset.py``: ``PartialH5Dataset`` 32,
 ``PartialH5DataLoaderIter`` 224): only a window of the file is resident; a background thread
-loads the next window while the current one is consumed. Uses ``h5py`` when installed, the
+reads the next windows while the current one is consumed. Uses ``h5py`` when installed, the
 built-in HDF5 reader (``heat_amd.core._h5lite``) otherwise.
+
+Semantics kept from the reference:
+
+* every rank owns ``total_size // comm.size`` consecutive rows (``partial_dataset.py:111-114``);
+* ``validate_set=True`` or ``initial_load > lcl_full_sz`` makes the WHOLE file resident on every
+  rank and the iterator a plain shuffled pass over it (``:116-124``);
+* ``len(dataset)`` is ``total_size`` (``:182-186``);
+* an epoch visits every row of the rank's share exactly once, in random order, whatever the speed
+  of the loader relative to the consumer (the reference replaces consumed indices under a
+  condition variable, ``:188-221, 324-359``).
+
+Design here: the share is cut into windows (``initial_load`` rows, then ``load_length`` rows,
+then the remainder). The loader thread reads windows ahead into a bounded queue (two windows of
+look-ahead); the iterator shuffles each window, fetches items through ``dataset[i]`` (so a
+user-overridden ``__getitem__`` and the transforms apply), carries a partial batch over into the
+next window, and BLOCKS on the queue when the next window is not loaded yet. After the last
+window the loader pre-reads the first window of the next epoch.
 """
 from __future__ import annotations
 
@@ -28,6 +45,8 @@ def _open(path: str):
 
 __all__ = ["PartialH5Dataset", "PartialH5DataLoaderIter", "queue_thread"]
 
+_END = object()
+
 
 def queue_thread(q: queue.Queue) -> None:
     """Worker loop of the loader threads: run ``func(*args)`` (or a bare callable) per queue item."""
@@ -44,43 +63,92 @@ def queue_thread(q: queue.Queue) -> None:
 
 class PartialH5Dataset(torch_data.Dataset):
     """Window over this rank's share of HDF5 datasets (``dataset_names``), ``initial_load`` rows
-    resident, ``load_length`` rows fetched per background load."""
+    resident at construction, ``load_length`` rows per background read.
+
+    Parameters follow the reference: ``file``, ``comm``, ``dataset_names``, ``transforms`` (one
+    callable or ``None`` per item returned by ``__getitem__``), ``use_gpu``, ``validate_set``,
+    ``initial_load``, ``load_length``. ``__getitem__`` indexes the RESIDENT rows (subclass it for
+    custom items, as in the reference where it must be overridden).
+    """
 
     def __init__(self, file: str, comm=MPI_WORLD, dataset_names: Union[str, List[str]] = "data",
                  transforms: List[Callable] = None, use_gpu: bool = True, validate_set: bool = False,
                  initial_load: int = 7000, load_length: int = 1000):
+        super().__init__()
         self.ishuffle = False
         self.file = file
         self.comm = comm
         self.transforms = transforms if isinstance(transforms, (list, tuple)) else [transforms]
         self.gpu = use_gpu and torch.cuda.is_available()
+        self.torch_device = torch.device("cuda", torch.cuda.current_device()) if self.gpu else torch.device("cpu")
         self.validate_set = validate_set
         self.dataset_names = [dataset_names] if isinstance(dataset_names, str) else list(dataset_names)
+        if initial_load < 1 or load_length < 1:
+            raise ValueError("initial_load and load_length must be positive, got {} and {}".format(
+                initial_load, load_length))
         with _open(file) as f:
-            self.total_size = f[self.dataset_names[0]].shape[0]
+            sizes = [f[n].shape[0] for n in self.dataset_names]
+        if len(set(sizes)) != 1:
+            raise ValueError("all datasets in {} must be the same length, got {}".format(file, sizes))
+        self.total_size = sizes[0]
         self.lcl_full_sz = self.total_size // comm.size
         self.local_data_start = self.lcl_full_sz * comm.rank
         self.local_data_end = self.local_data_start + self.lcl_full_sz
-        self.load_initial = min(initial_load, self.lcl_full_sz)
-        self.load_len = load_length
-        self.loads_remaining = max(0, (self.lcl_full_sz - self.load_initial) // max(1, load_length))
-        self._f = _open(file)
-        self.next_start = self.local_data_start + self.load_initial
-        for name in self.dataset_names:
-            arr = torch.tensor(self._f[name][self.local_data_start: self.next_start])
-            setattr(self, name, arr.cuda() if self.gpu else arr)
-        self.length = self.load_initial
+        if validate_set or initial_load > self.lcl_full_sz:
+            # whole file resident on every rank (validation sets; reference :116-124)
+            self.partial_dataset = False
+            self.lcl_full_sz = self.total_size
+            self.local_data_start, self.local_data_end = 0, self.total_size
+            self.load_initial = self.total_size
+            self.load_len = 0
+        else:
+            self.partial_dataset = True
+            self.load_initial = initial_load
+            self.load_len = load_length
+        self.windows = self._windows()
+        self.loads_needed = max(0, len(self.windows) - 1)
+        self.loads_remaining = self.loads_needed
+        self._load_lock = threading.Lock()
+        lo, hi = self.windows[0] if self.windows else (self.local_data_start, self.local_data_start)
+        self._set_resident(self._read(lo, hi), lo)
         self.load_thread = None
-        self.io_queue = queue.Queue()
+        self.io_queue = None
+        self._next_first = None
+
+    # ------------------------------------------------------------------ windows and reads
+    def _windows(self):
+        """(start, stop) row ranges of the rank's share: the initial window, then ``load_len``
+        rows each, the last one holding the remainder (no row is left out)."""
+        start, end = self.local_data_start, self.local_data_end
+        if start >= end:
+            return []
+        out = [(start, min(end, start + self.load_initial))]
+        pos = out[0][1]
+        while pos < end:
+            out.append((pos, min(end, pos + self.load_len)))
+            pos = out[-1][1]
+        return out
+
+    def _read(self, lo: int, hi: int) -> List[torch.Tensor]:
+        with self._load_lock, _open(self.file) as f:
+            return [torch.as_tensor(f[n][lo:hi]) for n in self.dataset_names]
+
+    def _set_resident(self, chunk: List[torch.Tensor], start: int) -> None:
+        for n, c in zip(self.dataset_names, chunk):
+            setattr(self, n, c.to(self.torch_device) if self.gpu else c)
+        self.resident_start = start
+        self.length = int(chunk[0].shape[0]) if chunk else 0
 
     def Shuffle(self):
-        pass
+        """Not implemented for partial datasets (reference returns ``NotImplementedError``)."""
+        return NotImplementedError
 
     def Ishuffle(self):
-        pass
+        """Not implemented for partial datasets (reference returns ``NotImplementedError``)."""
+        return NotImplementedError
 
     def __len__(self) -> int:
-        return self.length
+        return self.total_size
 
     def __getitem__(self, index):
         items = [getattr(self, n)[index] for n in self.dataset_names]
@@ -88,43 +156,96 @@ class PartialH5Dataset(torch_data.Dataset):
             items = [t(x) if t is not None else x for t, x in zip(self.transforms, items)]
         return items[0] if len(items) == 1 else tuple(items)
 
-    def thread_replace_converted_batches(self):
-        """Background loader: read the next window and queue it."""
-        while self.loads_remaining > 0:
-            end = min(self.next_start + self.load_len, self.local_data_end)
-            chunk = [torch.tensor(self._f[n][self.next_start: end]) for n in self.dataset_names]
-            self.io_queue.put(chunk)
-            self.next_start = end
-            self.loads_remaining -= 1
+    def thread_replace_converted_batches(self, out: "queue.Queue", windows) -> None:
+        """Background loader: read ``windows`` in order into ``out`` (bounded, so at most two
+        windows are held ahead), then the end marker, then pre-read the first window of the next
+        epoch into ``self._next_first``."""
+        try:
+            for lo, hi in windows:
+                out.put((lo, self._read(lo, hi)))
+                self.loads_remaining -= 1
+        except BaseException as e:  # surfaced in the consumer
+            out.put(("error", e))
+            return
+        out.put(_END)
+        lo, hi = self.windows[0]
+        self._next_first = (lo, self._read(lo, hi))
 
 
 class PartialH5DataLoaderIter:
-    """Iterator for :class:`PartialH5Dataset`: consumes resident rows while the next window loads."""
+    """Iterator for :class:`PartialH5Dataset`: one epoch over every row of the rank's share, in
+    random order per window, with the next windows loading in the background."""
 
     def __init__(self, loader):
         self.loader = loader
-        self.dataset = loader.dataset
-        self._it = iter(loader.DataLoader)
-        if self.dataset.loads_remaining > 0 and self.dataset.load_thread is None:
-            self.dataset.load_thread = threading.Thread(target=self.dataset.thread_replace_converted_batches,
-                                                        daemon=True)
-            self.dataset.load_thread.start()
+        self.dataset = ds = loader.dataset
+        dl = loader.DataLoader
+        self.batch_size = dl.batch_size
+        self.drop_last = dl.drop_last
+        self._collate = dl.collate_fn
+        n = ds.lcl_full_sz
+        self.length = n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+        self._num_yielded = 0
+        self._carry = []
+        self._win = 0
+        self._order = []
+        self._pos = 0
+        ds.loads_remaining = ds.loads_needed
+        if ds.windows and ds.resident_start != ds.windows[0][0]:
+            if ds.load_thread is not None:
+                ds.load_thread.join()  # it ends with the pre-read of this window
+            first = getattr(ds, "_next_first", None)
+            lo, hi = ds.windows[0]
+            ds._set_resident(first[1] if first is not None else ds._read(lo, hi), lo)
+        ds._next_first = None
+        self._queue = None
+        if ds.partial_dataset and len(ds.windows) > 1:
+            self._queue = queue.Queue(maxsize=2)
+            ds.io_queue = self._queue
+            ds.load_thread = threading.Thread(target=ds.thread_replace_converted_batches,
+                                              args=(self._queue, ds.windows[1:]), daemon=True)
+            ds.load_thread.start()
+        self._start_window()
+
+    def _start_window(self) -> None:
+        self._order = torch.randperm(self.dataset.length).tolist() if self.dataset.length else []
+        self._pos = 0
+
+    def _advance_window(self) -> bool:
+        """Swap in the next window, waiting for the loader if it is behind. False at epoch end."""
+        if self._queue is None:
+            return False
+        item = self._queue.get()  # blocks: a slow loader delays the batch, it never drops rows
+        if item is _END:
+            self._queue = None
+            return False
+        if item[0] == "error":
+            raise item[1]
+        lo, chunk = item
+        self.dataset._set_resident(chunk, lo)
+        self._start_window()
+        return True
 
     def __len__(self):
-        return len(self.loader)
+        return self.length
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        try:
-            return next(self._it)
-        except StopIteration:
-            if not self.dataset.io_queue.empty():
-                chunk = self.dataset.io_queue.get()
-                for n, c in zip(self.dataset.dataset_names, chunk):
-                    setattr(self.dataset, n, c.cuda() if self.dataset.gpu else c)
-                self.dataset.length = chunk[0].shape[0]
-                self._it = iter(self.loader.DataLoader)
-                return next(self._it)
-            raise
+        if self._num_yielded >= self.length:
+            raise StopIteration
+        items = self._carry
+        while len(items) < self.batch_size:
+            if self._pos >= len(self._order):
+                if not self._advance_window():
+                    break
+                continue
+            take = self._order[self._pos: self._pos + self.batch_size - len(items)]
+            self._pos += len(take)
+            items.extend(self.dataset[i] for i in take)
+        self._carry = []
+        if not items or (len(items) < self.batch_size and self.drop_last):
+            raise StopIteration
+        self._num_yielded += 1
+        return self._collate(items)

@@ -5,12 +5,12 @@ All checks of one (module, world size) run in ONE multi-rank job (interpreter st
 the per-check runs); a failing check is re-run alone in a fresh job to report a clean traceback."""
 import pytest
 
-from . import dist_checks, dist_checks_edge, oracle_checks, random_checks, vcoll_checks
+from . import dist_checks, dist_checks_edge, dl_io_checks, oracle_checks, random_checks, vcoll_checks
 from ._dist import run_distributed, run_distributed_batch
 
 MODULES = {"tests.dist_checks": dist_checks, "tests.dist_checks_edge": dist_checks_edge,
            "tests.vcoll_checks": vcoll_checks, "tests.random_checks": random_checks,
-           "tests.oracle_checks": oracle_checks}
+           "tests.oracle_checks": oracle_checks, "tests.dl_io_checks": dl_io_checks}
 CASES = [(m, n) for m, mod in MODULES.items() for n in dir(mod) if n.startswith("check_")
          and getattr(getattr(mod, n), "__module__", m) == m]
 _BATCH = {}

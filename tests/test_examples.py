@@ -38,18 +38,24 @@ def test_datasets():
     km = ht.cluster.KMeans(n_clusters=3, init="kmeans++", random_state=1).fit(X)
     assert km.cluster_centers_.shape == (3, 4)
     Xd, yd = ht.datasets.diabetes(synthetic=True)
-    assert Xd.shape == (442, 10) and yd.shape == (442, 1)
+    assert Xd.shape == (442, 11) and yd.shape == (442, 1)   # same layout as the fixture
+    assert np.all(Xd.numpy()[:, 0] == 1.0)
     Xs, ys = ht.datasets.iris(synthetic=True)
     assert Xs.shape == (150, 4) and np.bincount(ys.numpy()).tolist() == [50, 50, 50]
 
 
-def test_dataset_fixtures():
+def test_dataset_fixtures(monkeypatch):
     """The reference fixtures (when a Heat checkout or $HEAT_DATASETS_DIR provides them) load through
     every format with the same values, on every split axis; iris() / diabetes() return them."""
     import numpy as np
     import pytest
     import heat_amd as ht
 
+    import os
+
+    ref_dir = "/root/reference/heat/datasets"   # a Heat checkout, opted in through the env var
+    if not os.environ.get("HEAT_DATASETS_DIR") and os.path.isdir(ref_dir):
+        monkeypatch.setenv("HEAT_DATASETS_DIR", ref_dir)
     if ht.datasets.fixture_path("iris.csv") is None:
         pytest.skip("reference fixtures not available")
     ref = np.loadtxt(ht.datasets.fixture_path("iris.csv"), delimiter=";", dtype=np.float32)

@@ -523,6 +523,29 @@ def test_threefry_bit_exact():
     assert torch.allclose(a.larray, b.larray.cpu(), rtol=1e-4, atol=1e-4)
 
 
+def test_randn_fast_transform_parity_and_distribution():
+    """The hardware-log/exp Kundu transform (+ precise table near u = 1) stays within the host
+    parity bound on EVERY one of 1e7 samples, and the sample moments / KS statistic match the
+    host path."""
+    import heat_amd as ht
+
+    _dev()
+    n = 10_000_000
+    ht.random.set_state(("Threefry", 2024, 77))
+    a = ht.random.randn(n, device="cpu").larray.double()
+    ht.random.set_state(("Threefry", 2024, 77))
+    b = ht.random.randn(n, device="gpu").larray.cpu().double()
+    err = ((a - b).abs() / (1 + a.abs())).max().item()
+    assert err < 1e-4, err
+    assert abs(b.mean().item() - a.mean().item()) < 1e-6
+    assert abs(b.var().item() / a.var().item() - 1) < 1e-5
+    # two-sample KS statistic between host and device samples (identical up to rounding)
+    sa, sb = torch.sort(a).values, torch.sort(b).values
+    grid = torch.linspace(-5, 5, 2001, dtype=torch.float64)
+    ks = (torch.searchsorted(sa, grid).double() - torch.searchsorted(sb, grid).double()).abs().max().item() / n
+    assert ks < 1e-5, ks
+
+
 def test_kmeans_fit_gpu(gpu):
     import heat_amd as ht
 

@@ -170,3 +170,45 @@ def test_householder_partial_contracts():
         assert part % nb == 0 and 1 <= blocks <= max(1, -(-m // 32))
         gb = -(-blocks // copies)                       # blocks per group of the fixed-order tree
         assert -(-blocks // gb) <= copies               # every group has an accumulator copy
+
+
+def test_stale_library_after_failed_rebuild_warns(tmp_path, monkeypatch):
+    """A rebuild that fails while an older library exists loads it with a loud warning that
+    names the failing source; HEAT_STRICT_BUILD=1 refuses instead."""
+    import os
+    import shutil
+    import warnings
+
+    import pytest
+
+    from heat_amd.ops import _build
+
+    real = _build.LIBPATH
+    if not os.path.exists(real):
+        pytest.skip("native library not built")
+    libdir = tmp_path / "_lib"
+    libdir.mkdir()
+    stale = libdir / "libheat_amd_kernels.so"
+    shutil.copy(real, stale)
+    bad = tmp_path / "broken_kernel.hip"
+    bad.write_text("#include <hip/hip_runtime.h>\n__global__ void k() { this is not C++; }\n")
+    os.utime(stale, (1, 1))  # older than every source
+    monkeypatch.setattr(_build, "LIBDIR", str(libdir))
+    monkeypatch.setattr(_build, "LIBPATH", str(stale))
+    monkeypatch.setattr(_build, "sources", lambda: [str(bad)])
+    monkeypatch.setattr(_build, "headers", lambda: [])
+    saved = ops._lib
+    monkeypatch.setattr(ops, "_lib", None)
+    try:
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            handle = ops.lib()
+        msgs = [str(w.message) for w in rec if issubclass(w.category, RuntimeWarning)]
+        assert handle is not None
+        assert any("STALE" in m and "broken_kernel.hip" in m for m in msgs), msgs
+        monkeypatch.setattr(ops, "_lib", None)
+        monkeypatch.setenv("HEAT_STRICT_BUILD", "1")
+        with pytest.raises(RuntimeError, match="broken_kernel.hip"):
+            ops.lib()
+    finally:
+        ops._lib = saved

@@ -121,3 +121,66 @@ def check_exchange_empty_ranks_statistics():
     assert np.allclose(ht.var(x, axis=0).numpy(), a.var(0), atol=1e-6)
     assert np.allclose(ht.max(x).item(), a.max())
     assert int(ht.argmin(x).item()) == int(a.argmin())
+
+
+def check_native_comm_byte_plans():
+    """The byte counts / offsets the native RCCL communicator hands to ``ha_comm_alltoallv``
+    (``parallel/native_comm.py``), run through a host model of that grouped send/receive, give
+    exactly the gloo results of ``allgather_tensor`` and ``exchange_axis`` - uneven blocks, empty
+    ranks, every axis (the native path itself needs several GPUs; its arithmetic does not)."""
+    from heat_amd.core.communication import exchange_axis_bytes
+    from heat_amd.ops import kernels as K
+    from heat_amd.parallel import native_comm as nc
+
+    comm = ht.MPI_WORLD
+    p, me = comm.size, comm.rank
+
+    def raw(t):
+        t = t.contiguous()
+        return t.view(torch.uint8).numpy().reshape(-1) if t.numel() else np.zeros(0, np.uint8)
+
+    # all-gather of unequal row blocks (some ranks empty)
+    counts = [(3 * r + 1) % 4 for r in range(p)]
+    block = torch.arange(counts[me] * 5, dtype=torch.float64).reshape(counts[me], 5) + 1000 * me
+    real = comm.allgather_tensor(block, 0, counts)
+    plan = nc.allgatherv_plan(counts, me, 5 * 8)
+    sims = nc.simulate_alltoallv(comm.allgather(raw(block)), comm.allgather(plan), [sum(counts) * 40] * p)
+    assert np.array_equal(sims[me].view(np.float64).reshape(-1, 5), real.numpy())
+
+    # personalised exchanges along every axis pair of a 3-D array with uneven counts
+    shape = (7, 2 * p + 1, 5)
+    g = np.arange(np.prod(shape), dtype=np.int32).reshape(shape)
+    for split in range(3):
+        for target in range(3):
+            if split == target:
+                continue
+            scounts = comm.counts_displs_shape(shape, target)[0]
+            rcounts = comm.counts_displs_shape(shape, split)[0]
+            lo = sum(rcounts[:me])
+            send = torch.from_numpy(np.ascontiguousarray(np.take(g, range(lo, lo + rcounts[me]), axis=split)))
+            recv_shape = list(shape)
+            recv_shape[target] = scounts[me]
+            real = comm.exchange_axis(send, target, scounts, tuple(recv_shape), split, rcounts)
+            in_b, out_b = exchange_axis_bytes(tuple(send.shape), target, scounts, tuple(recv_shape), split, rcounts,
+                                              send.element_size())
+            packed = K.pack_blocks(send, target, scounts)
+            plans = comm.allgather(nc.alltoallv_plan(in_b, out_b))
+            sends = comm.allgather(raw(packed))
+            sizes = comm.allgather(int(sum(out_b)))
+            sim = nc.simulate_alltoallv(sends, plans, sizes)[me]
+            got = K.unpack_blocks(torch.from_numpy(sim.view(np.int32).copy()), tuple(recv_shape), split, rcounts)
+            assert torch.equal(got, real), (split, target)
+            t0 = sum(scounts[:me])
+            assert np.array_equal(real.numpy(), np.take(g, range(t0, t0 + scounts[me]), axis=target))
+
+    # a mismatched plan is caught (the real exchange would hang): rank 0 announces one byte more
+    if p > 1:
+        bad = [list(nc.alltoallv_plan([4] * p, [4] * p)) for _ in range(p)]
+        bad[0][0] = bad[0][0].copy()
+        bad[0][0][1] += 1
+        try:
+            nc.simulate_alltoallv([np.zeros(4 * p + 1, np.uint8)] * p, bad, [4 * p] * p)
+        except ValueError:
+            pass
+        else:
+            raise AssertionError("mismatched send/receive sizes not detected")

@@ -51,6 +51,44 @@ void run_p(const _Float16* P, const float2* A, int64_t n, float* C, const float*
                        1.f, run);
   });
   printf("f=%d cdist_p no-store %.3f ms  %4.0f TF fp16\n", f, t, tf / t * 1e3);
+  CHECK(hipFuncSetAttribute((const void*)cdist_p<0, KS, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  CHECK(hipMemset(C, 0, n * n * 4));
+  t = timeit([&] {
+    hipLaunchKernelGGL((cdist_p<0, KS, 2>), dim3((unsigned)(per_xcd * 8)), dim3(256), lds, 0, P, A, n, P, A, n, C, n,
+                       1.f, run);
+  });
+  printf("f=%d cdist_p edge-path %.3f ms  %5.0f GB/s out  relerr %.1e\n", f, t, gb / t * 1e3, check(C, h, n, f));
+}
+
+// write-bandwidth references: a sequential 16-byte non-temporal fill of the same bytes, and the
+// same bytes written in cdist_p's pattern (128 x 128 tiles, 8 rows x 128 B per store instruction)
+__global__ __launch_bounds__(256) void fill_seq(floatx4* C, int64_t n4) {
+  const floatx4 v = {1.f, 2.f, 3.f, 4.f};
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    __builtin_nontemporal_store(v, C + i);
+}
+__global__ __launch_bounds__(256) void fill_tiles(float* C, int64_t n, int run) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31, t = j & 3;
+  const int64_t panels = n / 128, tiles_n = n / 128, runs = (tiles_n + run - 1) / run;
+  const int64_t total = panels * runs, per_xcd = (total + 7) / 8, b = blockIdx.x;
+  const int64_t tt = (b % 8) * per_xcd + b / 8;
+  if (tt >= total) return;
+  const int64_t rp = tt % panels, cr = tt / panels, row0 = rp * 128;
+  const floatx4 v = {1.f, 2.f, 3.f, 4.f};
+  for (int64_t c = cr * run; c < (cr + 1) * run && c < tiles_n; ++c) {
+    float* p = C + (row0 + 4 * h + t) * n + c * 128 + wave * 32 + (j >> 2) * 4;
+    for (int k = 0; k < 16; ++k) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p + (int64_t)8 * k * n));
+  }
+}
+
+void run_fill(float* C, int64_t n) {
+  const double gb = n * n * 4 / 1e9;
+  float t = timeit([&] { hipLaunchKernelGGL(fill_seq, dim3(256 * 8), dim3(256), 0, 0, (floatx4*)C, n * n / 4); });
+  printf("fill sequential     %.3f ms  %5.0f GB/s\n", t, gb / t * 1e3);
+  const int run = cdist_run(n, n);
+  const int64_t per_xcd = ((n / TM) * ((n / TN + run - 1) / run) + 7) / 8;
+  t = timeit([&] { hipLaunchKernelGGL(fill_tiles, dim3((unsigned)(per_xcd * 8)), dim3(256), 0, 0, C, n, run); });
+  printf("fill cdist pattern  %.3f ms  %5.0f GB/s\n", t, gb / t * 1e3);
 }
 
 int main() {
@@ -73,6 +111,7 @@ int main() {
     if (fpad == 128) run_p<8>(P, A, n, C, h, f);
     if (fpad == 64) run_p<4>(P, A, n, C, h, f);
     if (fpad == 32) run_p<2>(P, A, n, C, h, f);
+    if (f == 128) run_fill(C, n);
     CHECK(hipFree(X)); CHECK(hipFree(C)); CHECK(hipFree(P)); CHECK(hipFree(A)); free(h);
   }
   return 0;
