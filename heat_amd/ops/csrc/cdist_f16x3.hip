@@ -117,20 +117,7 @@ __device__ __forceinline__ void store_blocks(const floatx16 (&acc)[NU], const fl
 }
 
 // ------------------------------------------------------------------ panel-resident kernel, fpad <= 128
-// ABL (timing ablation in tools/microbench only): 1 = no stores, 2 = every tile through the edge
-// path (the round-3 loop: one loop with a run-time interior / edge branch)
-//
-// Store/wait structure. gfx950 counts loads AND stores in one vmcnt, and store acknowledgements may
-// overtake earlier loads, so the compiler cannot let stores stay in flight while it waits for a
-// load issued before them: every such wait (vmcnt(k) with k = loads issued since) in effect also
-// drains the stores. The round-3 loop prefetched the next tile's Y fragments during the MFMAs and
-// only consumed them after this tile's 64 stores, so every wave drained all of its output at the
-// top of every tile (4.4 ms for a 65536^2 x 128 tile whose MFMAs alone take 2.7 ms and whose output
-// alone streams in 3.3 ms). Now the epilogue first computes all 64 outputs, then waits for the
-// prefetched loads (vmcnt(0): they had the MFMA block and the epilogue math to land), then issues
-// the stores: no later wait covers them until the end of the NEXT tile's MFMA block, so they drain
-// under those MFMAs. Interior tiles run in their own loop with never-skipped stores, the first
-// one peeled; the rare edge tiles (last row panel, last column tile) run after it.
+// ABL (timing ablation in tools/microbench only): 1 = no stores
 template <int MODE, int KS, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void cdist_p(const _Float16* __restrict__ PX, const float2* __restrict__ AX,
                                                   int64_t m, const _Float16* __restrict__ PY,
@@ -180,13 +167,10 @@ __global__ __launch_bounds__(256, 2) void cdist_p(const _Float16* __restrict__ P
   }
   float2 ya = AY[c_begin * TN + wave * 32 + j];
   __syncthreads();
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
 
-  auto step = [&](int64_t c, auto edge) {
+  for (int64_t c = c_begin; c < c_end; ++c) {
     const bool more = c + 1 < c_end;
     const int64_t cn = more ? c + 1 : c;  // the last tile re-reads itself: no branches around loads
-    const float2 yc = ya;
-    ya = AY[cn * TN + wave * 32 + j];
     // the X fragments are loop-invariant; an opaque per-iteration base keeps the compiler from
     // hoisting all of them (4 x KS x 2 x 4 VGPRs) out of the loop
     int xoff = lane * 8;
@@ -209,7 +193,8 @@ __global__ __launch_bounds__(256, 2) void cdist_p(const _Float16* __restrict__ P
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[u], 0, 0, 0);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    const float2 yc = ya;
+    ya = AY[cn * TN + wave * 32 + j];
     const int64_t col = c * TN + wave * 32 + j;
     if (ABL == 1) {
       float s = 0.f;
@@ -218,52 +203,41 @@ __global__ __launch_bounds__(256, 2) void cdist_p(const _Float16* __restrict__ P
 #pragma unroll
         for (int r = 0; r < 16; ++r) s += acc[u][r];
       if (s == 1234.5f) C[col] = s;  // keep the MFMAs alive
-      return;
+      continue;
     }
     // epilogue. Row values come from LDS through the laundered base (hoisting them would pin
     // 128 VGPRs), and the store address is a wave-uniform row pointer (SGPRs, bumped 8 rows at a
-    // time) plus one 32-bit per-lane byte offset, so no 64-bit per-store addresses are kept. Each
-    // store instruction writes 2 rows x 32 columns = two whole 128-byte lines.
+    // time) plus one 32-bit per-lane byte offset, so no 64-bit per-store addresses are kept.
     const float ynv = yc.x, m2isy = -2.f * yc.y;
     const float* rv = rowv + (xoff >> 3) - lane + 4 * h;  // == rowv + 4h, opaque to LICM
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
     int64_t ld4 = ldc * 4;
     asm volatile("" : "+s"(ld4));  // per-iteration, so the row offsets are not hoisted into spilled SGPRs
     char* p = reinterpret_cast<char*>(C + row0 * ldc + c * TN + wv * 32);
     const uint32_t lb = (uint32_t)(4 * h * ld4 + j * 4);
+    const bool interior = row0 + TM <= m && (c + 1) * TN <= n;
     int rows_left = (int)((m - row0 < TM ? m - row0 : TM) - 4 * h);
     asm volatile("" : "+v"(rows_left));  // keep the 64 row predicates out of the loop preheader
+    auto tile_out = [&](auto edge) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 4; ++u) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = u * 32 + (r & 3) + 8 * (r >> 2);  // + 4h
-        acc[u][r] = epi<MODE>(fmaxf(fmaf(m2isy * rv[128 + rl], acc[u][r], rv[rl] + ynv), 0.f), scale);
-      }
-    // the next tile's loads are complete before the first store is issued (see above)
-    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-    __builtin_amdgcn_sched_barrier(0);
+        for (int q = 0; q < 4; ++q) {
+          const int rl = u * 32 + 8 * q;  // + 4h + rr
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int rl = u * 32 + 8 * q;  // + 4h + rr
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          float* dst = reinterpret_cast<float*>(p + rr * ld4 + lb);
-          if (!decltype(edge)::value || (col < n && rl + rr < rows_left))
-            __builtin_nontemporal_store(acc[u][4 * q + rr], dst);
+          for (int rr = 0; rr < 4; ++rr) {
+            const float d2 = fmaxf(fmaf(m2isy * rv[128 + rl + rr], acc[u][4 * q + rr], rv[rl + rr] + ynv), 0.f);
+            const float o = epi<MODE>(d2, scale);
+            float* dst = reinterpret_cast<float*>(p + rr * ld4 + lb);
+            if (!decltype(edge)::value || (col < n && rl + rr < rows_left)) __builtin_nontemporal_store(o, dst);
+          }
+          p += 8 * ld4;
         }
-        p += 8 * ld4;
       }
-    }
-  };
-
-  int64_t c = c_begin;
-  const int64_t full_n = n / TN;  // column tiles without an edge
-  const int64_t c_int = ABL == 2 || row0 + TM > m ? c_begin : (c_end < full_n ? c_end : full_n);
-  if (c < c_int) step(c++, std::false_type{});  // peeled: the loop header sees only interior epilogues
-  for (; c < c_int; ++c) step(c, std::false_type{});
-  for (; c < c_end; ++c) step(c, std::true_type{});
+    };
+    if (interior) tile_out(std::false_type{});
+    else tile_out(std::true_type{});
+  }
 }
 
 // ---------------------------------------------------------------------- LDS-staged tile kernel, any fpad

@@ -51,13 +51,6 @@ void run_p(const _Float16* P, const float2* A, int64_t n, float* C, const float*
                        1.f, run);
   });
   printf("f=%d cdist_p no-store %.3f ms  %4.0f TF fp16\n", f, t, tf / t * 1e3);
-  CHECK(hipFuncSetAttribute((const void*)cdist_p<0, KS, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  CHECK(hipMemset(C, 0, n * n * 4));
-  t = timeit([&] {
-    hipLaunchKernelGGL((cdist_p<0, KS, 2>), dim3((unsigned)(per_xcd * 8)), dim3(256), lds, 0, P, A, n, P, A, n, C, n,
-                       1.f, run);
-  });
-  printf("f=%d cdist_p edge-path %.3f ms  %5.0f GB/s out  relerr %.1e\n", f, t, gb / t * 1e3, check(C, h, n, f));
 }
 
 // write-bandwidth references: a sequential 16-byte non-temporal fill of the same bytes, and the
