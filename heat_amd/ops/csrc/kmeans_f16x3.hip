@@ -763,6 +763,190 @@ __global__ __launch_bounds__(256, 2) void h3_topk(const _Float16* __restrict__ p
   }
 }
 
+// Pipelined top-k ("p"): the assignment kernel's structure (h3_assign_p) with a top-k epilogue.
+//  * the -s_x s_c u_c term rides in the accumulator as one rank-1 bf16 MFMA per tile, so a score
+//    is ONE multiply (acc * r_c) instead of an FMA + a multiply with two LDS vectors per tile;
+//  * ping-pong accumulators: the scores / tile maximum / threshold test of tile t-1 are VALU issued
+//    in the MFMA gaps of tile t (sched_group_barrier interleave);
+//  * the rare insertion (a tile value beating a lane's KN-th best) runs after the tile's MFMAs,
+//    only when some lane of the wave needs it (__any), from the 16 stashed scores;
+//  * two LDS chunk buffers (the last tile's epilogue reads the previous buffer's r values).
+// Round 3's h3_topk ran at 50 % MFMA-busy with 4.7 VALU per MFMA (profiles/pmc_r03.md).
+template <int FPAD, int KN, int NPB_>
+__global__ __launch_bounds__(256, 2) void h3_topk_p(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+                                                    int64_t n, const _Float16* __restrict__ image,
+                                                    const float* __restrict__ u, const float* __restrict__ meta,
+                                                    int nchunks, int cps, int kout, float* __restrict__ dist,
+                                                    int* __restrict__ idx) {
+  using K = H3Cfg<FPAD, NPB_>;
+  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+
+  halfx8 bhi[NPB][KS], blo[NPB][KS];
+  bf16x8 bsx[NPB];
+  float sx[NPB], xsq[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const int64_t pi = pbase + pb * 32 + j;
+    const int64_t row = pi < n ? pi : n - 1;
+    const _Float16* pr = planes + row * (2 * FPAD) + h * F2;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bhi[pb][ks] = *reinterpret_cast<const halfx8*>(pr + 8 * ks);
+      blo[pb][ks] = *reinterpret_cast<const halfx8*>(pr + FPAD + 8 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = (float)bhi[pb][ks][i] + (float)blo[pb][ks][i];
+        q = fmaf(xv, xv, q);
+      }
+    }
+    sx[pb] = sxv[row];
+    xsq[pb] = q;
+    const unsigned sb = __float_as_uint(sx[pb]) >> 16;  // s_x: a power of two, exact in bf16
+    const u32x4 bw = {h ? 0u : (sb | (sb << 16)), h ? 0u : sb, 0u, 0u};
+    bsx[pb] = __builtin_bit_cast(bf16x8, bw);
+  }
+  float tv[NPB][KN];
+  int ti[NPB][KN];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+    for (int s = 0; s < KN; ++s) {
+      tv[pb][s] = -__builtin_huge_valf();
+      ti[pb][s] = -1;
+    }
+  const int ch0 = blockIdx.y * cps;
+  const int ch1 = ch0 + cps < nchunks ? ch0 + cps : nchunks;
+  dist += (int64_t)blockIdx.y * n * kout;
+  idx += (int64_t)blockIdx.y * n * kout;
+
+  constexpr int PIECES = CHUNK_H * 2 / 1024;
+  constexpr int VPIECES = CB * 16 / 1024;
+  constexpr int BUF = CHUNK_H * 2 + CB * 8 + CB * 16;
+  const unsigned* vimg = reinterpret_cast<const unsigned*>(meta + 4);
+  floatx16 acc[2][NPB];
+  float w[NPB][16];
+  bool need = false;
+  const float* pu = nullptr;
+  int ptile = -1;
+  // scores of the pending tile, its maximum against each lane's current KN-th best (no branch)
+  auto epilogue = [&](const floatx16 (&ac)[NPB], const float* pu_) {
+    floatx4 cr[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[pb][q] = ac[pb][q] * cr[q >> 2][q & 3];
+      float m = w[pb][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) m = fmaxf(m, w[pb][r]);
+      need |= m > tv[pb][KN - 1];
+    }
+  };
+  auto insert = [&](int tile) {
+    if (__builtin_amdgcn_ballot_w64(need) == 0ull) return;  // wave-uniform: usually nobody
+    const int tbase = tile * 32 + 4 * h;
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (w[pb][r] > tv[pb][KN - 1]) topk_insert<KN>(tv[pb], ti[pb], w[pb][r], tbase + (r & 3) + 8 * (r >> 2));
+    need = false;
+  };
+  for (int ch = ch0; ch < ch1; ++ch) {
+    {
+      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+      unsigned char* dst = smem + (ch & 1) * BUF;
+#pragma unroll
+      for (int pc = wave; pc < PIECES; pc += 4)
+        __builtin_amdgcn_global_load_lds(src + pc * 1024,
+                                         (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, 0, 0);
+      if (wave == 0 && lane < CB / 2)  // u and r of the chunk (adjacent)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H * 2), 16, 0, 0);
+#pragma unroll
+      for (int pc = wave; pc < VPIECES; pc += 4)  // rank-1 fragments of the chunk's tiles
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(vimg) + (int64_t)ch * CB * 16 + pc * 1024 + lane * 16,
+                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H * 2 + CB * 8 + pc * 1024),
+                                         16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+    const unsigned char* buf = smem + (ch & 1) * BUF;
+    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
+    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H * 2);
+    const unsigned* vb = reinterpret_cast<const unsigned*>(buf + CHUNK_H * 2 + CB * 8);
+#pragma unroll
+    for (int cb = 0; cb < CB / 32; ++cb) {
+      const int cur = cb & 1;  // CB/32 is even: ping-pong slot is compile-time
+#pragma unroll
+      for (int pb = 0; pb < NPB; ++pb) acc[cur][pb] = (floatx16)(0.f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const _Float16* a = img + (((cb * KS + ks) * 2) * 64 + lane) * 8;
+        const halfx8 ahi = *reinterpret_cast<const halfx8*>(a);
+        const halfx8 alo = *reinterpret_cast<const halfx8*>(a + 64 * 8);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) {
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo[pb][ks], acc[cur][pb], 0, 0, 0);
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+        }
+      }
+      {
+        const uint2 vv = *reinterpret_cast<const uint2*>(vb + (cb * 64 + lane) * 2);
+        const u32x4 aw = {vv.x, vv.y, 0u, 0u};
+        const bf16x8 av = __builtin_bit_cast(bf16x8, aw);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb)
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bsx[pb], acc[cur][pb], 0, 0, 0);
+      }
+      if (ptile >= 0) epilogue(acc[cur ^ 1], pu);
+#pragma unroll
+      for (int i = 0; i < (3 * KS + 1) * NPB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to 4 VALU
+      }
+      if (ptile >= 0) insert(ptile);
+      ptile = ch * (CB / 32) + cb;
+      pu = ub + cb * 32;
+    }
+    __syncthreads();  // every wave is done with the buffer before the chunk after next is staged
+  }
+  if (ptile >= 0) {
+    epilogue(acc[((CB / 32) - 1) & 1], pu);
+    insert(ptile);
+  }
+  // merge the partner half's list (disjoint candidates) into lane half 0
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+#pragma unroll
+    for (int s = 0; s < KN; ++s) {
+      const float ov = __shfl_xor(tv[pb][s], 32, 64);
+      const int oi = __shfl_xor(ti[pb][s], 32, 64);
+      if (h == 0 && ov > tv[pb][KN - 1]) topk_insert<KN>(tv[pb], ti[pb], ov, oi);
+    }
+    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
+    const int64_t pi = pbase + pb * 32 + j;
+    if (h == 0 && pi < n) {
+      const float isx = 1.f / sx[pb];
+#pragma unroll
+      for (int s = 0; s < KN; ++s)
+        if (s < kout) {
+          const bool ok = ti[pb][s] >= 0;
+          dist[pi * kout + s] = ok ? fmaxf(xs * isx * isx - 2.f * tv[pb][s] * isx, 0.f) : __builtin_huge_valf();
+          idx[pi * kout + s] = ti[pb][s];
+        }
+    }
+  }
+}
+
 // Resident-centroid assignment ("r"): ONE workgroup per CU (NW waves) stages up to RC centroid
 // chunks into LDS once (128 KB: 512 centroids at f = 64) and its waves then stream point blocks
 // through them with no further barrier or staging; per-wave point blocks are independent. k above
@@ -1121,13 +1305,28 @@ HA_EXPORT int ha_h3_topk(const void* planes, const float* sx, int64_t n, int f, 
   hipStream_t s = (hipStream_t)stream;
   const int cb = fpad >= 128 ? 64 : 128;
   const int kpad = (m + cb - 1) / cb * cb;
+  // HEAT_H3_TOPK_V1=1: the round-3 kernel (A/B)
+  static const bool v1 = getenv("HEAT_H3_TOPK_V1") && getenv("HEAT_H3_TOPK_V1")[0] == '1';
   _Float16* image = (_Float16*)workspace;
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
   float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
 #define HA_TK_LAUNCH(FP, KN)                                                                                 \
-  hipLaunchKernelGGL((h3_topk<FP, KN>), dim3(blocks, splits), dim3(256), lds, s, p, sx, n, image, u, meta,      \
-                     kpad / KC::CB, (kpad / KC::CB + splits - 1) / splits, kout, dist, idx)
+  do {                                                                                                       \
+  if (v1) {                                                                                                  \
+    hipLaunchKernelGGL((h3_topk<FP, KN>), dim3(blocks, splits), dim3(256), lds, s, p, sx, n, image, u, meta,    \
+                       kpad / KC::CB, (kpad / KC::CB + splits - 1) / splits, kout, dist, idx);              \
+  } else {                                                                                                   \
+    constexpr int NPBT = FP >= 128 ? 1 : 2;                                                                  \
+    using KP = H3Cfg<FP, NPBT>;                                                                              \
+    const size_t ldsp = 2 * ((size_t)KP::CHUNK_H * 2 + KP::CB * 8 + KP::CB * 16);                           \
+    const unsigned bp = (unsigned)((n + KP::PTS_PER_WG - 1) / KP::PTS_PER_WG);                               \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h3_topk_p<FP, KN, NPBT>),                               \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsp);                              \
+    hipLaunchKernelGGL((h3_topk_p<FP, KN, NPBT>), dim3(bp, splits), dim3(256), ldsp, s, p, sx, n, image, u,   \
+                       meta, kpad / KC::CB, (kpad / KC::CB + splits - 1) / splits, kout, dist, idx);        \
+  }                                                                                                          \
+  } while (0)
 #define HA_TK(FP)                                                                                            \
   case FP: {                                                                                                 \
     using KC = H3Cfg<FP, 1>;                                                                                 \

@@ -89,6 +89,7 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
         raise TypeError("X must be a DNDarray")
     if len(X.shape) > 2:
         raise NotImplementedError("Only 2D data matrices are currently supported")
+    symmetric = Y is None
     if Y is None:
         Y = X
     if not isinstance(Y, DNDarray):
@@ -118,7 +119,11 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
         return DNDarray(_local(metric, x, y, sigma).to(tt), (m, n), dtype, 1, X.device, comm, Y.balanced)
     counts, displs = Y.counts_displs()
     ybytes = n * Y.gshape[1] * y.element_size()
-    if ybytes <= _ALLGATHER_BYTES:
+    if symmetric and ybytes > _allgather_bytes():
+        out = torch.empty((x.shape[0], n), dtype=tt, device=x.device)
+        _symmetric_half_ring(x, out, counts, displs, comm, lambda a, b: _local(metric, a, b, sigma).to(tt))
+        return DNDarray(out, (m, n), dtype, 0, X.device, comm, X.balanced)
+    if ybytes <= _allgather_bytes():
         yfull = comm.allgather_tensor(y.contiguous(), 0, counts)
         res = _local(metric, x, yfull, sigma).to(tt)
         return DNDarray(res, (m, n), dtype, 0, X.device, comm, X.balanced)
@@ -134,6 +139,63 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
 
     ring_pass(y, tile, comm, counts)
     return DNDarray(out, (m, n), dtype, 0, X.device, comm, X.balanced)
+
+
+def _allgather_bytes() -> int:
+    """Largest operand (bytes) that is all-gathered instead of streamed around the ring
+    (``HEAT_CDIST_ALLGATHER_BYTES`` overrides, e.g. to exercise the ring paths in small tests)."""
+    import os
+
+    v = os.environ.get("HEAT_CDIST_ALLGATHER_BYTES")
+    return int(v) if v else _ALLGATHER_BYTES
+
+
+def _symmetric_half_ring(x: torch.Tensor, out: torch.Tensor, counts, displs, comm, tile) -> None:
+    """``cdist(X)`` with X split 0 on p ranks in ceil((p-1)/2) + 1 steps instead of p (reference
+    ``spatial/distance.py:237, 265-362``): d(X_r, X_q) = d(X_q, X_r)^T, so every off-diagonal tile
+    pair is computed ONCE. At step s every rank receives the block of rank r - s, computes the
+    tile (r, r - s), keeps it and sends its transpose back to r - s, which stores it as its tile
+    (r - s, r); for even p the last step (partners r and r + p/2) is computed by the lower half
+    only. Per step: one block exchange and one tile exchange, each a batched send/receive pair."""
+    import torch.distributed as dist
+
+    from ..parallel import staging as _SD
+
+    p, r = comm.size, comm.rank
+    out[:, displs[r]: displs[r] + counts[r]] = tile(x, x)
+    rest = tuple(x.shape[1:])
+    xs = x.contiguous()
+
+    def exchange(send, dst, recv_shape, src):
+        recv = None if src is None else torch.empty(recv_shape, dtype=xs.dtype, device=xs.device)
+        ops = []
+        if send is not None:
+            ops.append(dist.P2POp(dist.isend, send.contiguous(), comm._g(dst), comm.group))
+        if src is not None:
+            ops.append(dist.P2POp(dist.irecv, recv, comm._g(src), comm.group))
+        for w in _SD.batch_isend_irecv(ops):
+            w.wait()
+        return recv
+
+    for s_ in range(1, p // 2 + 1):
+        dst, src = (r + s_) % p, (r - s_) % p
+        if p % 2 == 0 and s_ == p // 2:
+            q = dst  # == src: partners r and r + p/2
+            if r < p // 2:   # computes the pair's tile
+                blk = exchange(None, None, (counts[q],) + rest, q)
+                t = tile(xs, blk)
+                out[:, displs[q]: displs[q] + counts[q]] = t
+                exchange(t.t(), q, None, None)
+            else:            # sends its block, receives the mirrored tile
+                exchange(xs, q, None, None)
+                got = exchange(None, None, (counts[r], counts[q]), q)
+                out[:, displs[q]: displs[q] + counts[q]] = got
+            continue
+        blk = exchange(xs, dst, (counts[src],) + rest, src)
+        t = tile(xs, blk)
+        out[:, displs[src]: displs[src] + counts[src]] = t
+        got = exchange(t.t(), src, (counts[r], counts[dst]), dst)
+        out[:, displs[dst]: displs[dst] + counts[dst]] = got
 
 
 def _dist_callable(X: DNDarray, Y: Optional[DNDarray], fn: Callable) -> DNDarray:

@@ -583,3 +583,36 @@ def check_kmeans_bit_reproducible():
         d = ((pts.astype(np.float64)[:, None, :] - c[None]) ** 2).sum(-1)
         best = d.min(1)
         assert np.all(d[np.arange(len(pts)), lab] <= best * (1 + 1e-5) + 1e-4)
+
+
+def check_cdist_symmetric_half_ring():
+    """cdist(X) / rbf(X) / manhattan(X) with X split 0 and no Y through the half ring (every
+    off-diagonal tile computed once, its transpose sent back; reference spatial/distance.py:265-362)
+    equal the NumPy distance matrix, for uneven blocks and every p (odd and even last step)."""
+    import os
+
+    from scipy.spatial.distance import cdist as sp_cdist
+
+    comm = ht.MPI_WORLD
+    rng = np.random.default_rng(5)
+    old = os.environ.get("HEAT_CDIST_ALLGATHER_BYTES")
+    os.environ["HEAT_CDIST_ALLGATHER_BYTES"] = "0"      # force the ring paths
+    try:
+        for n in (3 * comm.size + 2, 2 * comm.size - 1):
+            a = rng.standard_normal((n, 5)).astype(np.float64)
+            X = ht.array(a, split=0)
+            ref = sp_cdist(a, a)
+            d = ht.spatial.cdist(X)
+            assert d.split == 0 and d.shape == (n, n)
+            np.testing.assert_allclose(d.numpy(), ref, atol=1e-9)
+            np.testing.assert_allclose(ht.spatial.cdist(X, X).numpy(), ref, atol=1e-9)   # full ring
+            np.testing.assert_allclose(ht.spatial.rbf(X, sigma=1.5).numpy(), np.exp(-ref ** 2 / (2 * 1.5 ** 2)),
+                                       atol=1e-9)
+            np.testing.assert_allclose(ht.spatial.manhattan(X).numpy(), sp_cdist(a, a, "cityblock"), atol=1e-9)
+            d32 = ht.spatial.cdist(ht.array(a.astype(np.float32), split=0), quadratic_expansion=True)
+            np.testing.assert_allclose(d32.numpy(), ref, atol=2e-3)
+    finally:
+        if old is None:
+            os.environ.pop("HEAT_CDIST_ALLGATHER_BYTES", None)
+        else:
+            os.environ["HEAT_CDIST_ALLGATHER_BYTES"] = old
