@@ -170,6 +170,11 @@ def main():
         cfg = {"model": "cdist_topk euclidean n={} f={} k={} float32 split=0".format(n, f, args.topk),
                "global_batch": n, "seq_len": f, "parallelism": "dp{}".format(n_gpus)}
         extra["flop_convention"] = "2*n*n*f (the distance GEMM of the quadratic expansion)"
+        from heat_amd.ops import kernels as _k
+
+        st = _k._KNN_STATS
+        extra["certified_queries"] = st["queries"]
+        extra["certified_rechecked_fraction"] = st["rechecked"] / st["queries"] if st["queries"] else None
         extra.update(validate_knn(x, d, idx, comm))
         scaling = "strong"
     else:

@@ -228,15 +228,85 @@ def _topk_lex(d: torch.Tensor, idx: Optional[torch.Tensor], k: int) -> Tuple[tor
     return _lex_split(key)
 
 
+_KNN_CERTIFIED = os.environ.get("HEAT_KNN_CERTIFIED", "1") != "0"
+_KNN_KP = 16  # candidates per query of the certified one-term pass
+
+
+def _knn_exact_select(Q: torch.Tensor, T: torch.Tensor, idx: torch.Tensor, k: int):
+    """Exact (difference-form) squared distances of the candidate rows ``idx`` [nq, c] (-1 =
+    none), the k smallest per query, equal distances ordered by index."""
+    nq, c = idx.shape
+    f = Q.shape[1]
+    dist = torch.empty((nq, k), dtype=torch.float32, device=Q.device)
+    out_i = torch.empty((nq, k), dtype=torch.int64, device=Q.device)
+    step = max(1, (1 << 26) // (c * f))
+    for q0 in range(0, nq, step):
+        ib = idx[q0: q0 + step]
+        nb = T[ib.clamp(min=0)].float()
+        d = ((Q[q0: q0 + step].float().unsqueeze(1) - nb) ** 2).sum(-1)
+        d = torch.where(ib >= 0, d, torch.full_like(d, float("inf")))
+        dv, di = _topk_lex(d, ib, k)
+        dist[q0: q0 + step] = dv
+        out_i[q0: q0 + step] = di
+    return dist, out_i
+
+
+def _knn_certified(Q, T, Tc, k, packed, ws, exact_distances: bool = True):
+    """k <= 8 nearest rows of T through the certified one-term kernel (``h1_topk``: 1 fp16 MFMA
+    per k-step instead of 3, a rigorous error bound per query): 16 candidates per query, the
+    queries whose candidates are not certified to contain the true k nearest re-run through the
+    3-term kernel, then every candidate list is rescored exactly."""
+    L = lib()
+    nq, f = Q.shape
+    nt = T.shape[0]
+    dev = Q.device
+    kp = _KNN_KP
+    st = ctypes.c_void_p(stream_ptr(dev))
+    dist = torch.empty((nq, kp), dtype=torch.float32, device=dev)
+    idx = torch.empty((nq, kp), dtype=torch.int32, device=dev)
+    cert = torch.empty(nq, dtype=torch.uint8, device=dev)
+    check(L.ha_h1_topk(_ptr(packed.planes), _ptr(packed.sx), nq, f, _ptr(Tc), nt, Tc.stride(0), _ptr(ws), k, kp,
+                       _ptr(dist), _ptr(idx), _ptr(cert), st), "ha_h1_topk")
+    unc = torch.nonzero(cert == 0).flatten()
+    _KNN_STATS["queries"] += nq
+    _KNN_STATS["rechecked"] += int(unc.numel())
+    if unc.numel():
+        pl = packed.planes.index_select(0, unc).contiguous()
+        sxu = packed.sx.index_select(0, unc).contiguous()
+        nu = int(unc.numel())
+        qblocks = (nu + 127) // 128
+        splits = max(1, min(L.ha_h3_topk_chunks(nt, f) // 4, (4 * num_cus(dev) + qblocks - 1) // qblocks))
+        d3 = torch.empty((splits, nu, kp), dtype=torch.float32, device=dev)
+        i3 = torch.empty((splits, nu, kp), dtype=torch.int32, device=dev)
+        check(L.ha_h3_topk(_ptr(pl), _ptr(sxu), nu, f, _ptr(Tc), nt, Tc.stride(0), _ptr(ws), kp, splits, _ptr(d3),
+                           _ptr(i3), st), "ha_h3_topk")
+        if splits == 1:
+            i3 = i3[0].long()
+        else:
+            _, i3 = _topk_lex(d3.permute(1, 0, 2).reshape(nu, splits * kp), i3.permute(1, 0, 2).reshape(nu, splits * kp),
+                              kp)
+        idx = idx.long()
+        idx[unc] = i3
+    else:
+        idx = idx.long()
+    # the k nearest are certified to be AMONG the candidates, not ranked: always rescore exactly
+    return _knn_exact_select(Q, T, idx, k)
+
+
+_KNN_STATS = {"queries": 0, "rechecked": 0}
+
+
 def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPoints] = None,
              exact_distances: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
     """The ``k`` nearest rows of ``T`` for every row of ``Q``: (squared distances [nq, k] ascending,
     int64 row indices [nq, k]; +inf / -1 where T has fewer than k rows).
 
     Device fp32 with k <= 16 and f <= 128: ONE fused kernel (fp16x3 MFMA scores + a running top-k
-    per point in registers, ``csrc/kmeans_f16x3.hip: h3_topk``), no nq x nt distance matrix. The
-    selected neighbours' distances are then recomputed exactly (difference form) and re-sorted
-    (``exact_distances``). Otherwise: distance tiles + torch.topk, in query blocks."""
+    per point in registers, ``csrc/kmeans_f16x3.hip: h3_topk_p``), no nq x nt distance matrix;
+    for k <= 8 (and enough queries to fill the GPU) the certified one-term pass first
+    (``h1_topk``, :func:`_knn_certified`). The selected neighbours' distances are then recomputed
+    exactly (difference form) and re-sorted (``exact_distances``). Otherwise: distance tiles +
+    torch.topk, in query blocks."""
     nq, f = Q.shape
     nt = T.shape[0]
     dev = Q.device
@@ -254,6 +324,8 @@ def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPo
         # (>= 4 waves of 128 queries per CU overall) and merge the partial lists
         qblocks = (nq + 127) // 128
         splits = max(1, min(L.ha_h3_topk_chunks(nt, f) // 4, (4 * num_cus(dev) + qblocks - 1) // qblocks))
+        if splits == 1 and k <= 8 and _KNN_CERTIFIED and hasattr(L, "ha_h1_topk"):
+            return _knn_certified(Q, T, Tc, k, packed, ws, exact_distances)
         dist = torch.empty((splits, nq, k), dtype=torch.float32, device=dev)
         idx = torch.empty((splits, nq, k), dtype=torch.int32, device=dev)
         check(L.ha_h3_topk(_ptr(packed.planes), _ptr(packed.sx), nq, f, _ptr(Tc), nt, Tc.stride(0), _ptr(ws), k,
@@ -279,15 +351,7 @@ def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPo
             idx = torch.cat([idx, torch.full((nq, k - kk), -1, dtype=torch.int64, device=dev)], 1)
         return dist, idx
     if exact_distances:
-        step = max(1, (1 << 26) // (k * f))
-        for q0 in range(0, nq, step):
-            ib = idx[q0: q0 + step]
-            nb = T[ib.clamp(min=0)].float()
-            d = ((Q[q0: q0 + step].float().unsqueeze(1) - nb) ** 2).sum(-1)
-            d = torch.where(ib >= 0, d, torch.full_like(d, float("inf")))
-            d, i = _topk_lex(d, ib, k)
-            dist[q0: q0 + step] = d
-            idx[q0: q0 + step] = i
+        return _knn_exact_select(Q, T, idx, k)
     return dist, idx
 
 

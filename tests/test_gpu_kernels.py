@@ -877,3 +877,44 @@ def test_kmeans_assign_small_k(n, f, k):
     lab2, _ = ops.kmeans_assign(Xs, C[:, : Xs.shape[1]].contiguous())
     d2 = torch.cdist(Xs.double(), C[:, : Xs.shape[1]].double()) ** 2
     assert (lab2.long() == d2.argmin(1)).float().mean() > 0.9999
+
+
+@pytest.mark.parametrize("f", [128, 64, 18])
+def test_knn_certified_one_term(f):
+    """The certified one-term pass (h1_topk: 16 candidates per query from hi.hi scores + a rigorous
+    bound, uncertain queries re-run through the 3-term kernel, exact rescoring) gives the exact
+    fp64 k nearest neighbours, including on duplicated training rows (exact ties: the uncertain
+    path must run) and near-duplicate queries."""
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(f)
+    nq, nt, k = 140_000, 20_000, 8          # enough query blocks for the single-split path
+    Q = torch.randn(nq, f, generator=g).to(dev)
+    T = torch.randn(nt, f, generator=g).to(dev)
+    T[:600] = T[600:1200]                                   # exact duplicates -> ties
+    Q[:3000] = T[:3000] + 1e-3 * torch.randn(3000, f, generator=g).to(dev)
+    # 20 training rows of exactly equal norm (sign flips of one vector) nearest to 100 zero queries:
+    # more exact ties than candidates, so those queries cannot be certified and take the 3-term path
+    base = 0.05 * torch.randn(f, generator=g)
+    flips = torch.where(torch.rand(20, f, generator=g) < 0.5, -1.0, 1.0)
+    T[1200:1220] = (flips * base).to(dev)
+    Q[3000:3100] = 0.0
+    before = dict(K._KNN_STATS)
+    dist, idx = ops.knn_topk(Q, T, k)
+    assert K._KNN_STATS["queries"] - before["queries"] == nq          # the certified path ran
+    rechecked = K._KNN_STATS["rechecked"] - before["rechecked"]
+    assert 100 <= rechecked < nq // 2, rechecked
+    sel = torch.cat([torch.arange(3100), torch.randint(3100, nq, (3000,), generator=g)]).to(dev)
+    d = torch.cdist(Q[sel].double(), T.double()) ** 2
+    # reference order: distance, then index (stable sort over ascending indices)
+    rd, ri = torch.sort(d, dim=1, stable=True)
+    rd, ri = rd[:, :k], ri[:, :k]
+    assert torch.allclose(dist[sel].double(), rd, rtol=1e-5, atol=1e-5)
+    # the reported indices sit at the reported distances; index sets equal wherever the k-th
+    # distance is not tied with the (k+1)-th
+    assert torch.allclose(d.gather(1, idx[sel]), dist[sel].double(), rtol=1e-5, atol=1e-5)
+    clear = (torch.sort(d, dim=1).values[:, k] - rd[:, -1]) > 1e-4 * rd[:, -1].clamp(min=1)
+    same = (torch.sort(idx[sel], 1).values == torch.sort(ri, 1).values).all(1)
+    assert bool(same[clear].all()), int((~same[clear]).sum())

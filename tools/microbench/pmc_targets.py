@@ -5,6 +5,7 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   gemm    - ht.matmul 8192^3 fp32 at precision highest (gemm_f32t) and high (gemm_h3t)
   cdist   - one 32768 x 32768 x 128 distance tile (cdist_f16x3.hip)
   topk    - 8 nearest of 65536 x 128 queries among 1e6 points (spatial.cdist_topk -> h3_topk)
+  knn     - the bench.py knn step: 8 nearest of all 1e6 x 128 rows among themselves (certified h1_topk)
   randn   - 8e8 standard normals and 8e8 uniforms, fp32 (threefry.hip: tf_fill32, 3.2 GB each)"""
 import sys
 
@@ -45,6 +46,9 @@ def main():
         y = ht.random.rand(1_000_000, 128, split=0)
         for _ in range(3):
             ht.spatial.cdist_topk(q, y, 8)
+    elif which == "knn":
+        x = ht.random.rand(1_000_000, 128, split=0)
+        ht.spatial.cdist_topk(x, x, 8)
     elif which == "randn":
         for _ in range(3):
             ht.random.randn(1_000_000, 800, split=0)
