@@ -2,10 +2,14 @@
 K-Means (Lloyd's algorithm) (reference ``heat/cluster/kmeans.py``: ``KMeans`` 13,
 ``_update_centroids`` 73-100, ``fit`` 102-139).
 
-Per iteration and rank: ONE fused assign kernel (fp32 MFMA distances + running argmin), ONE
-update kernel (LDS-privatised per-cluster sums and counts, one pass over the local points) and
-ONE all-reduce of the packed (k*f sums + k counts) over RCCL - instead of the reference's k full
-passes over the data and 2k all-reduces + k broadcasts.
+Per iteration and rank: ONE fused assign kernel (distances as a 3-term fp16 split on the FP16
+matrix cores, ~fp32-GEMM accuracy, plus a running argmax of the score; the points' fp16 planes are
+packed once per fit - ``ops/csrc/kmeans_f16x3.hip``; a certified one-term filter with a 3-term
+re-check where it pays; k <= 16 a single fused VALU/MFMA pass, ``kmeans_smallk.hip``; the exact
+f32-MFMA kernel under ``precision="exact"``), ONE deterministic update (counting sort of the
+labels, fixed-order per-cluster sums and counts - ``kmeans.hip``: no float atomics, bit-reproducible
+runs) and ONE all-reduce of the packed (k*f sums + k counts) over RCCL - instead of the reference's
+k full passes over the data and 2k all-reduces + k broadcasts.
 """
 from __future__ import annotations
 

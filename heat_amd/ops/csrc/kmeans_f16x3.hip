@@ -962,7 +962,11 @@ __device__ __forceinline__ void topk_insert_ev(float (&tv)[KP], int (&ti)[KP], f
   topk_insert<KP>(tv, ti, v, id);
 }
 
-template <int FPAD, int KP, int KN, int NPB_>
+// KH: list length per lane half (each half sees half of the rows of C); the two half lists are
+// merged into the output list of KP = 2 KH. A short per-half list halves the cost of an insertion
+// and makes insertions rarer (the per-half threshold is its KH-th best): the insertions, not the
+// MFMAs, bound this kernel (8.7 VALU per MFMA at KH = 16).
+template <int FPAD, int KH, int KN, int NPB_>
 __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
@@ -1005,13 +1009,14 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     const u32x4 bw = {h ? 0u : (sb | (sb << 16)), h ? 0u : sb, 0u, 0u};
     bsx[pb] = __builtin_bit_cast(bf16x8, bw);
   }
-  float tv[NPB][KP], rej[NPB];
-  int ti[NPB][KP];
+  constexpr int KP = 2 * KH;
+  float tv[NPB][KH], rej[NPB];
+  int ti[NPB][KH];
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
     rej[pb] = NINF;
 #pragma unroll
-    for (int s2 = 0; s2 < KP; ++s2) {
+    for (int s2 = 0; s2 < KH; ++s2) {
       tv[pb][s2] = NINF;
       ti[pb][s2] = -1;
     }
@@ -1037,7 +1042,7 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
       float m = w[pb][0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) m = fmaxf(m, w[pb][r]);
-      const bool nd = m > tv[pb][KP - 1];
+      const bool nd = m > tv[pb][KH - 1];
       rej[pb] = nd ? rej[pb] : fmaxf(rej[pb], m);  // the whole tile is let go
       need |= nd;
     }
@@ -1049,8 +1054,8 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     for (int pb = 0; pb < NPB; ++pb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        if (w[pb][r] > tv[pb][KP - 1])
-          topk_insert_ev<KP>(tv[pb], ti[pb], w[pb][r], tbase + (r & 3) + 8 * (r >> 2), rej[pb]);
+        if (w[pb][r] > tv[pb][KH - 1])
+          topk_insert_ev<KH>(tv[pb], ti[pb], w[pb][r], tbase + (r & 3) + 8 * (r >> 2), rej[pb]);
         else
           rej[pb] = fmaxf(rej[pb], w[pb][r]);
       }
@@ -1119,16 +1124,22 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
   const float cmax = sqrtf(2.f * umax);
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
-    // merge the partner half's list; every value the merge lets go raises rej
-    float orj = __shfl_xor(rej[pb], 32, 64);
+    // the two half lists (disjoint candidates) side by side in one list of KP = 2 KH
+    float mv[KP];
+    int mi[KP];
 #pragma unroll
-    for (int s2 = 0; s2 < KP; ++s2) {
+    for (int s2 = 0; s2 < KH; ++s2) {
+      mv[s2] = tv[pb][s2];
+      mi[s2] = ti[pb][s2];
+      mv[KH + s2] = NINF;
+      mi[KH + s2] = -1;
+    }
+    const float orj = __shfl_xor(rej[pb], 32, 64);
+#pragma unroll
+    for (int s2 = 0; s2 < KH; ++s2) {
       const float ov = __shfl_xor(tv[pb][s2], 32, 64);
       const int oi = __shfl_xor(ti[pb][s2], 32, 64);
-      if (h == 0) {
-        if (ov > tv[pb][KP - 1]) topk_insert_ev<KP>(tv[pb], ti[pb], ov, oi, rej[pb]);
-        else orj = fmaxf(orj, ov);
-      }
+      if (h == 0 && ov > mv[KP - 1]) topk_insert<KP>(mv, mi, ov, oi);
     }
     rej[pb] = fmaxf(rej[pb], orj);
     const float xn = sqrtf(hsq[pb] + __shfl_xor(hsq[pb], 32, 64)) * (1.f + 0x1p-10f);
@@ -1140,11 +1151,11 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
       const float isx = 1.f / sx[pb];
 #pragma unroll
       for (int s2 = 0; s2 < KP; ++s2) {
-        const bool ok = ti[pb][s2] >= 0;
-        dist[pi * KP + s2] = ok ? fmaxf(xs * isx * isx - 2.f * tv[pb][s2] * isx, 0.f) : __builtin_huge_valf();
-        idx[pi * KP + s2] = ti[pb][s2];
+        const bool ok = mi[s2] >= 0;
+        dist[pi * KP + s2] = ok ? fmaxf(xs * isx * isx - 2.f * mv[s2] * isx, 0.f) : __builtin_huge_valf();
+        idx[pi * KP + s2] = mi[s2];
       }
-      cert[pi] = (ti[pb][KN - 1] >= 0 && rej[pb] < tv[pb][KN - 1] - 2.f * E) ? 1 : 0;
+      cert[pi] = (mi[KN - 1] >= 0 && rej[pb] < mv[KN - 1] - 2.f * E) ? 1 : 0;
     }
   }
 }
@@ -1504,9 +1515,9 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   // the error bound needs max |c| and max u (atomicMax into zeroed words)
   if (hipMemsetAsync(meta, 0, 16, s) != hipSuccess) return HA_LAUNCH;
 #define HA_H1TK_KN(FP, KN)                                                                                     \
-  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KN, NPBT>),                                 \
+  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 8, KN, NPBT>),                                  \
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                    \
-  hipLaunchKernelGGL((h1_topk<FP, 16, KN, NPBT>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,      \
+  hipLaunchKernelGGL((h1_topk<FP, 8, KN, NPBT>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,      \
                      kpad / KC::CB, dist, idx, cert)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
