@@ -86,33 +86,46 @@ __device__ __forceinline__ double kundu_d(double u) {
   return (log(-log(inner + tiny) + tiny) - 1.0821) * (1.0 / 0.3807);
 }
 
-// out: local block of n elements; global element index of out[0] is e0.
+template <int DIST>
+__device__ __forceinline__ void tf_convert32(uint32_t v, void* out, int64_t i, int64_t low, int64_t span) {
+  if constexpr (DIST == DIST_INT) {
+    int32_t sv = (int32_t)v;
+    int32_t a = sv < 0 ? (int32_t)(0u - (uint32_t)sv) : sv;  // torch abs (wraps at INT_MIN)
+    int64_t r = (int64_t)a % span;
+    if (r < 0) r += span;
+    reinterpret_cast<int32_t*>(out)[i] = (int32_t)(r + low);
+  } else {
+    const uint32_t v23 = v & 0x7FFFFFu;
+    reinterpret_cast<float*>(out)[i] = DIST == DIST_NORMAL ? kundu_fast(v23) : (float)v23 * (1.0f / 8388608.0f);
+  }
+}
+
+// out: local block of n elements; global element index of out[0] is e0. One counter pair per
+// thread per grid-stride step; a pair whose two elements are both in range and 8-byte aligned
+// (e0 even) is written with one 8-byte store. DIST is a template parameter so each launch is one
+// straight-line loop (the run-time switch kept the 64-bit modulo of the integer path in every
+// iteration's code).
+template <int DIST>
 __global__ __launch_bounds__(256) void tf_fill32(void* __restrict__ out, int64_t e0, int64_t n, uint64_t counter_lo,
-                                                 uint32_t key, int dist, int64_t low, int64_t span) {
+                                                 uint32_t key, int64_t low, int64_t span) {
   const int64_t p0 = e0 >> 1;
   const int64_t p1 = (e0 + n + 1) >> 1;
+  const bool even = (e0 & 1) == 0;
   for (int64_t p = p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < p1;
        p += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t V = counter_lo + (uint64_t)p;
     uint32_t x0 = (uint32_t)(V >> 32), x1 = (uint32_t)V;
     tf32(x0, x1, key);
-    const uint32_t comp[2] = {x0, x1};
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int64_t e = 2 * p + c;
-      const int64_t i = e - e0;
-      if (i < 0 || i >= n) continue;
-      const uint32_t v = comp[c];
-      if (dist == DIST_INT) {
-        int32_t s = (int32_t)v;
-        int32_t a = s < 0 ? (int32_t)(0u - (uint32_t)s) : s;  // torch abs (wraps at INT_MIN)
-        int64_t r = (int64_t)a % span;
-        if (r < 0) r += span;
-        reinterpret_cast<int32_t*>(out)[i] = (int32_t)(r + low);
-      } else {
-        const uint32_t v23 = v & 0x7FFFFFu;
-        reinterpret_cast<float*>(out)[i] = dist == DIST_NORMAL ? kundu_fast(v23) : (float)v23 * (1.0f / 8388608.0f);
-      }
+    const int64_t i = 2 * p - e0;
+    if (DIST != DIST_INT && even && i >= 0 && i + 1 < n) {
+      float2 o;
+      const uint32_t a = x0 & 0x7FFFFFu, b = x1 & 0x7FFFFFu;
+      o.x = DIST == DIST_NORMAL ? kundu_fast(a) : (float)a * (1.0f / 8388608.0f);
+      o.y = DIST == DIST_NORMAL ? kundu_fast(b) : (float)b * (1.0f / 8388608.0f);
+      *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + i) = o;
+    } else {
+      if (i >= 0 && i < n) tf_convert32<DIST>(x0, out, i, low, span);
+      if (i + 1 >= 0 && i + 1 < n) tf_convert32<DIST>(x1, out, i + 1, low, span);
     }
   }
 }
@@ -177,8 +190,16 @@ HA_EXPORT int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counte
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_tab_ready[dev]) return HA_UNSUPPORTED;
   }
   if (bits == 32) {
-    hipLaunchKernelGGL(tf_fill32, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo,
-                       (uint32_t)(seed & 0x7FFFFFFFull), dist, (int64_t)low, (int64_t)span);
+    const uint32_t key = (uint32_t)(seed & 0x7FFFFFFFull);
+    if (dist == DIST_NORMAL)
+      hipLaunchKernelGGL(tf_fill32<DIST_NORMAL>, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo, key,
+                         (int64_t)low, (int64_t)span);
+    else if (dist == DIST_INT)
+      hipLaunchKernelGGL(tf_fill32<DIST_INT>, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo, key,
+                         (int64_t)low, (int64_t)span);
+    else
+      hipLaunchKernelGGL(tf_fill32<DIST_UNIFORM>, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo, key,
+                         (int64_t)low, (int64_t)span);
   } else if (bits == 64) {
     hipLaunchKernelGGL(tf_fill64, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo, counter_hi, seed,
                        dist, (int64_t)low, (int64_t)span);
