@@ -64,147 +64,15 @@ __global__ void km_pack_centroids(const float* __restrict__ C, int k, int f, int
   }
 }
 
-template <int FPAD>
-__global__ __launch_bounds__(256, 2) void km_assign(const float* __restrict__ X, int64_t n, int f, int64_t ldx,
-                                                   const float* __restrict__ frag,
-                                                   const float* __restrict__ cnorm, int nchunks,
-                                                   int* __restrict__ labels, float* __restrict__ mind) {
-  using K = KMCfg<FPAD>;
-  constexpr int F2 = K::F2, S4 = K::S4, CB = K::CB, NPB = K::NPB, CHUNK = K::CHUNK;
-  constexpr int BUF = CHUNK + CB;                 // packed centroids + their norms
-  constexpr int STG = CHUNK / 4 / 256;            // float4 staged per thread per chunk
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
-
-  // ---- B fragments: this lane's half row of its points, kept in registers for all centroids
-  float xb[NPB][F2];
-  float xsq[NPB];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    int64_t row = pbase + pb * 32 + j;
-    row = row < n ? row : n - 1;
-    const float* xr = X + row * ldx + h * F2;
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < S4; ++q) {
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (h * F2 + 4 * q < f) v = *reinterpret_cast<const floatx4*>(xr + 4 * q);
-      xb[pb][4 * q + 0] = v[0];
-      xb[pb][4 * q + 1] = v[1];
-      xb[pb][4 * q + 2] = v[2];
-      xb[pb][4 * q + 3] = v[3];
-      s = fmaf(v[0], v[0], s);
-      s = fmaf(v[1], v[1], s);
-      s = fmaf(v[2], v[2], s);
-      s = fmaf(v[3], v[3], s);
-    }
-    xsq[pb] = s;
-  }
-
-  float best[NPB];
-  int bidx[NPB];
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    best[pb] = __builtin_huge_valf();
-    bidx[pb] = 0;
-  }
-
-  // ---- stage chunk 0
-  {
-    const floatx4* src = reinterpret_cast<const floatx4*>(frag);
-    floatx4* dst = reinterpret_cast<floatx4*>(smem);
-#pragma unroll
-    for (int i = 0; i < STG; ++i) dst[tid + 256 * i] = src[tid + 256 * i];
-    if (tid < CB / 4)
-      reinterpret_cast<floatx4*>(smem + CHUNK)[tid] = reinterpret_cast<const floatx4*>(cnorm)[tid];
-  }
-  __syncthreads();
-
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const bool more = ch + 1 < nchunks;
-    // issue the next chunk's loads early (register staging, written after compute)
-    floatx4 stg[STG];
-    floatx4 stn = {0.f, 0.f, 0.f, 0.f};
-    if (more) {
-      const floatx4* src = reinterpret_cast<const floatx4*>(frag + (int64_t)(ch + 1) * CHUNK);
-#pragma unroll
-      for (int i = 0; i < STG; ++i) stg[i] = src[tid + 256 * i];
-      if (tid < CB / 4) stn = reinterpret_cast<const floatx4*>(cnorm + (ch + 1) * CB)[tid];
-    }
-    const float* buf = smem + (ch & 1) * BUF;
-#pragma unroll 1
-    for (int cb = 0; cb < CB / 32; ++cb) {
-      floatx16 acc[NPB];
-#pragma unroll
-      for (int pb = 0; pb < NPB; ++pb) acc[pb] = (floatx16)(0.f);
-#pragma unroll
-      for (int s4 = 0; s4 < S4; ++s4) {
-        const floatx4 a = *reinterpret_cast<const floatx4*>(buf + ((cb * S4 + s4) * 64 + lane) * 4);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-#pragma unroll
-          for (int pb = 0; pb < NPB; ++pb)
-            acc[pb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], xb[pb][4 * s4 + t], acc[pb], 0, 0, 0);
-        }
-      }
-      // epilogue: d = |c|^2 - 2 x.c ; accumulator row = (reg&3) + 8*(reg>>2) + 4*h
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const floatx4 cn = *reinterpret_cast<const floatx4*>(buf + CHUNK + cb * 32 + 8 * g + 4 * h);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int cidx = ch * CB + cb * 32 + 8 * g + 4 * h + t;
-#pragma unroll
-          for (int pb = 0; pb < NPB; ++pb) {
-            const float d = fmaf(-2.f, acc[pb][4 * g + t], cn[t]);
-            if (d < best[pb]) {
-              best[pb] = d;
-              bidx[pb] = cidx;
-            }
-          }
-        }
-      }
-    }
-    if (more) {
-      floatx4* dst = reinterpret_cast<floatx4*>(smem + ((ch + 1) & 1) * BUF);
-#pragma unroll
-      for (int i = 0; i < STG; ++i) dst[tid + 256 * i] = stg[i];
-      if (tid < CB / 4) reinterpret_cast<floatx4*>(smem + ((ch + 1) & 1) * BUF + CHUNK)[tid] = stn;
-    }
-    __syncthreads();
-  }
-
-  // ---- merge the two half-waves (same point, disjoint centroid rows) and write
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    const float ob = __shfl_xor(best[pb], 32, 64);
-    const int oi = __shfl_xor(bidx[pb], 32, 64);
-    const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
-    if (ob < best[pb] || (ob == best[pb] && oi < bidx[pb])) {
-      best[pb] = ob;
-      bidx[pb] = oi;
-    }
-    const int64_t row = pbase + pb * 32 + j;
-    if (h == 0 && row < n) {
-      labels[row] = bidx[pb];
-      if (mind) mind[row] = fmaxf(best[pb] + xs, 0.f);
-    }
-  }
-}
-
-// Pipelined exact assignment (the default): km_assign's math with the structure of the fp16x3
-// kernel (kmeans_f16x3.hip: h3_assign_p) -
+// Exact assignment with the structure of the fp16x3 kernel (kmeans_f16x3.hip: h3_assign_p) -
 //  * the packed centroid chunks are staged by LDS-DMA (global_load_lds_dwordx4, lane-linear 1 KB
-//    pieces) into two LDS buffers instead of through registers (frees 32 VGPRs and the VALU/LDS
-//    writes of the register staging);
+//    pieces) into two LDS buffers (no register staging);
 //  * the tiles of a chunk are unrolled with ping-pong accumulators: the argmin epilogue of tile
-//    t-1 is issued in the MFMA gaps of tile t (sched_group_barrier), where km_assign drained the
-//    MFMA pipe and ran it between the tiles.
-// Numerics are identical to km_assign (the same fmaf chain per product, the same compare order).
+//    t-1 is issued in the MFMA gaps of tile t (sched_group_barrier).
+// Measured against round 3's register-staged, unpipelined kernel (bench.py exact path, k = 1024,
+// 1.25e7 x 64): 13.37 vs 13.38 ms (122 TFLOP/s either way, ~85 % of gemm_f32t's rate): the exact
+// assignment is bound by the f32 MFMA rate, not by its staging or epilogue. Kept for its lower
+// register use (193 VGPRs at FPAD 64) and the shared structure with the fp16x3 kernel.
 template <int FPAD>
 __global__ __launch_bounds__(256, 2) void km_assign_p(const float* __restrict__ X, int64_t n, int f, int64_t ldx,
                                                      const float* __restrict__ frag,
@@ -346,8 +214,6 @@ HA_EXPORT int ha_km_assign(const float* X, int64_t n, int f, int64_t ldx, const 
   int fpad, kpad;
   if (ha_km_workspace_floats(k, f, &fpad, &kpad) < 0) return HA_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  // HEAT_KM_ASSIGN_V1=1: the round-3 (register-staged, unpipelined) kernel, for A/B
-  static const bool v1 = getenv("HEAT_KM_ASSIGN_V1") && getenv("HEAT_KM_ASSIGN_V1")[0] == '1';
   float* frag = workspace;
   float* cnorm = workspace + (int64_t)kpad * fpad;
   const int64_t packthreads = (int64_t)kpad * (fpad / 4) > kpad ? (int64_t)kpad * (fpad / 4) : kpad;
@@ -360,15 +226,9 @@ HA_EXPORT int ha_km_assign(const float* X, int64_t n, int f, int64_t ldx, const 
     const int nchunks = kpad / KC::CB;                                                                  \
     const int64_t nwg = (n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG;                                      \
     const size_t lds = 2 * (size_t)(KC::CHUNK + KC::CB) * sizeof(float);                               \
-    if (v1) {                                                                                           \
-      hipFuncSetAttribute((const void*)km_assign<FP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-      hipLaunchKernelGGL(km_assign<FP>, dim3((unsigned)nwg), dim3(256), lds, s, X, n, f, ldx, frag, cnorm, \
-                         nchunks, labels, mind);                                                        \
-    } else {                                                                                            \
-      hipFuncSetAttribute((const void*)km_assign_p<FP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-      hipLaunchKernelGGL(km_assign_p<FP>, dim3((unsigned)nwg), dim3(256), lds, s, X, n, f, ldx, frag, cnorm, \
-                         nchunks, labels, mind);                                                        \
-    }                                                                                                   \
+    hipFuncSetAttribute((const void*)km_assign_p<FP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    hipLaunchKernelGGL(km_assign_p<FP>, dim3((unsigned)nwg), dim3(256), lds, s, X, n, f, ldx, frag, cnorm, \
+                       nchunks, labels, mind);                                                          \
     break;                                                                                              \
   }
   switch (fpad) {

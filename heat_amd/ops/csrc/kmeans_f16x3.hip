@@ -963,9 +963,12 @@ __device__ __forceinline__ void topk_insert_ev(float (&tv)[KP], int (&ti)[KP], f
 }
 
 // KH: list length per lane half (each half sees half of the rows of C); the two half lists are
-// merged into the output list of KP = 2 KH. A short per-half list halves the cost of an insertion
-// and makes insertions rarer (the per-half threshold is its KH-th best): the insertions, not the
-// MFMAs, bound this kernel (8.7 VALU per MFMA at KH = 16).
+// merged into the output list of 16. Measured (bench knn, 1e6 x 1e6 x 128): KH = 16 -> 373 ms +
+// 10.8 % of the queries re-checked (81 ms); KH = 8 -> 350 ms but 32.7 % re-checked (222 ms).
+// The insertions, not the MFMAs, bound this kernel (7-9 VALU per MFMA): a lane whose tile beats
+// its threshold makes the whole wave run the insertion. Parking such tiles in LDS and draining
+// them for all lanes together (2 parked tiles per lane) was 5x SLOWER: a drain runs the union of
+// the lanes' insertion positions, so batching sparse, uncorrelated insertions does not pay.
 template <int FPAD, int KH, int KN, int NPB_>
 __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
@@ -1009,7 +1012,7 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     const u32x4 bw = {h ? 0u : (sb | (sb << 16)), h ? 0u : sb, 0u, 0u};
     bsx[pb] = __builtin_bit_cast(bf16x8, bw);
   }
-  constexpr int KP = 2 * KH;
+  constexpr int KO = 16;  // output candidates per point
   float tv[NPB][KH], rej[NPB];
   int ti[NPB][KH];
 #pragma unroll
@@ -1124,22 +1127,26 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
   const float cmax = sqrtf(2.f * umax);
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
-    // the two half lists (disjoint candidates) side by side in one list of KP = 2 KH
-    float mv[KP];
-    int mi[KP];
+    // merge the two half lists (disjoint candidates) into the output list of KO: whatever the
+    // merge lets go raises rej
+    float mv[KO];
+    int mi[KO];
 #pragma unroll
-    for (int s2 = 0; s2 < KH; ++s2) {
-      mv[s2] = tv[pb][s2];
-      mi[s2] = ti[pb][s2];
-      mv[KH + s2] = NINF;
-      mi[KH + s2] = -1;
+    for (int s2 = 0; s2 < KO; ++s2) {
+      mv[s2] = s2 < KH ? tv[pb][s2 < KH ? s2 : 0] : NINF;
+      mi[s2] = s2 < KH ? ti[pb][s2 < KH ? s2 : 0] : -1;
     }
-    const float orj = __shfl_xor(rej[pb], 32, 64);
+#pragma unroll
+    for (int s2 = KO; s2 < KH; ++s2) rej[pb] = fmaxf(rej[pb], tv[pb][s2]);
+    float orj = __shfl_xor(rej[pb], 32, 64);
 #pragma unroll
     for (int s2 = 0; s2 < KH; ++s2) {
       const float ov = __shfl_xor(tv[pb][s2], 32, 64);
       const int oi = __shfl_xor(ti[pb][s2], 32, 64);
-      if (h == 0 && ov > mv[KP - 1]) topk_insert<KP>(mv, mi, ov, oi);
+      if (h == 0) {
+        if (ov > mv[KO - 1]) topk_insert_ev<KO>(mv, mi, ov, oi, rej[pb]);
+        else orj = fmaxf(orj, ov);
+      }
     }
     rej[pb] = fmaxf(rej[pb], orj);
     const float xn = sqrtf(hsq[pb] + __shfl_xor(hsq[pb], 32, 64)) * (1.f + 0x1p-10f);
@@ -1150,10 +1157,10 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     if (h == 0 && pi < n) {
       const float isx = 1.f / sx[pb];
 #pragma unroll
-      for (int s2 = 0; s2 < KP; ++s2) {
+      for (int s2 = 0; s2 < KO; ++s2) {
         const bool ok = mi[s2] >= 0;
-        dist[pi * KP + s2] = ok ? fmaxf(xs * isx * isx - 2.f * mv[s2] * isx, 0.f) : __builtin_huge_valf();
-        idx[pi * KP + s2] = mi[s2];
+        dist[pi * KO + s2] = ok ? fmaxf(xs * isx * isx - 2.f * mv[s2] * isx, 0.f) : __builtin_huge_valf();
+        idx[pi * KO + s2] = mi[s2];
       }
       cert[pi] = (mi[KN - 1] >= 0 && rej[pb] < mv[KN - 1] - 2.f * E) ? 1 : 0;
     }
@@ -1515,9 +1522,9 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   // the error bound needs max |c| and max u (atomicMax into zeroed words)
   if (hipMemsetAsync(meta, 0, 16, s) != hipSuccess) return HA_LAUNCH;
 #define HA_H1TK_KN(FP, KN)                                                                                     \
-  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 8, KN, NPBT>),                                  \
+  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KN, NPBT>),                                 \
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                    \
-  hipLaunchKernelGGL((h1_topk<FP, 8, KN, NPBT>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,      \
+  hipLaunchKernelGGL((h1_topk<FP, 16, KN, NPBT>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,      \
                      kpad / KC::CB, dist, idx, cert)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \

@@ -70,14 +70,18 @@ __device__ float g_kundu_tab[1 << KUNDU_TAB_BITS];  // [i] = kundu(u) at u = (2^
 static bool g_tab_ready[64] = {};
 
 __device__ __forceinline__ float kundu_fast(uint32_t v23) {
+  // the table value is loaded for EVERY element (lanes outside the table read entry 0, one line
+  // shared by the wave): a branch around the load put its latency on the path of ~86 % of the
+  // waves (3 % of lanes need it) and held randn at 2.5 TB/s
+  const uint32_t mi = 8388607u - v23;  // 2^23 (1 - u) - 1
+  const bool in_tab = mi < (1u << KUNDU_TAB_BITS);
+  const float tabv = g_kundu_tab[in_tab ? mi : 0u];
   const float u = (float)v23 * (1.0f / 8388608.0f);
   const float ln2 = 0.693147180559945f, tiny = 1.17549435e-38f;
   const float w = __builtin_amdgcn_exp2f(0.0775f * __builtin_amdgcn_logf(u));  // u = 0: exp2(-inf) = 0
   const float l1 = -ln2 * __builtin_amdgcn_logf(1.f - w + tiny);
-  float r = (ln2 * __builtin_amdgcn_logf(l1 + tiny) - 1.0821f) * (1.0f / 0.3807f);
-  const uint32_t mi = 8388607u - v23;  // 2^23 (1 - u) - 1
-  if (mi < (1u << KUNDU_TAB_BITS)) r = g_kundu_tab[mi];
-  return r;
+  const float r = (ln2 * __builtin_amdgcn_logf(l1 + tiny) - 1.0821f) * (1.0f / 0.3807f);
+  return in_tab ? tabv : r;
 }
 
 __device__ __forceinline__ double kundu_d(double u) {
