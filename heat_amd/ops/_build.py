@@ -64,29 +64,54 @@ def needs_build() -> bool:
     return bool(stale_sources())
 
 
+OBJDIR = os.path.join(LIBDIR, "obj")  # per-source object cache (git- and gpurun-ignored)
+
+
+def _stale_objects(objs, flags) -> list:
+    """Indices of the sources whose cached object is missing or older than the source, a header
+    or this script, or was compiled with other flags."""
+    stamp = os.path.join(OBJDIR, "flags.txt")
+    same_flags = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
+    dep_t = max([os.path.getmtime(h) for h in headers()] + [os.path.getmtime(__file__)])
+    out = []
+    for i, (src, obj) in enumerate(zip(sources(), objs)):
+        if not same_flags or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), dep_t):
+            out.append(i)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile all kernels into one shared library (atomic replace). Returns the library path."""
+    """Compile the kernels into one shared library (atomic replace) and return its path. Sources
+    whose cached object is current are not recompiled unless ``force``."""
     if not force and not needs_build():
         return LIBPATH
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(OBJDIR, exist_ok=True)
     fd, tmp = tempfile.mkstemp(suffix=".so", dir=LIBDIR)
     os.close(fd)
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result",
              "-I" + CSRC]
-    objdir = tempfile.mkdtemp(prefix="ha_obj_")
 
     def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, capture_output=not verbose)
 
-    # one hipcc per source in parallel (the template-heavy kernel files dominate a serial build)
-    objs = [os.path.join(objdir, os.path.basename(src) + ".o") for src in sources()]
-    jobs = max(1, min(len(objs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    # one hipcc per stale source in parallel (the template-heavy kernel files dominate a serial build)
+    objs = [os.path.join(OBJDIR, os.path.basename(src) + ".o") for src in sources()]
+    todo = list(range(len(objs))) if force else _stale_objects(objs, flags)
+    jobs = max(1, min(max(len(todo), 1), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    srcs = sources()
+
+    def compile_one(i):
+        part = objs[i] + ".part"
+        run([hipcc()] + flags + file_flags(srcs[i]) + ["-c", srcs[i], "-o", part])
+        os.replace(part, objs[i])
+
     try:
         with ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(lambda so: run([hipcc()] + flags + file_flags(so[0]) + ["-c", so[0], "-o", so[1]]),
-                        zip(sources(), objs)))
+            list(ex.map(compile_one, todo))
+        with open(os.path.join(OBJDIR, "flags.txt"), "w") as f:
+            f.write(" ".join(flags))
         run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-ldl", "-o", tmp])
     except subprocess.CalledProcessError as e:
         os.unlink(tmp)
@@ -94,8 +119,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
         src = next((a for a in e.cmd if str(a).endswith(".hip")), None)
         where = " ({})".format(os.path.basename(src)) if src else ""
         raise RuntimeError("building the native kernels failed{}:\n{}".format(where, msg)) from e
-    finally:
-        shutil.rmtree(objdir, ignore_errors=True)
     os.replace(tmp, LIBPATH)
     return LIBPATH
 

@@ -14,6 +14,11 @@
 // column j + 1 from the rows it has just updated - so a panel of NB columns is NB launches, each one
 // pass over the panel's rows, with fp64 accumulation of every dot product.
 //
+// The step also writes column j of Y = V^T V (for larft) from the same sums, so the panel needs no
+// separate V^T V pass. The host factors each panel in a compact m x NB copy (row pitch NB: the 32
+// passes stream contiguous rows instead of one 128-byte segment per 16 KB matrix row) - `coff` is
+// the panel's first column within a row of A, k0 its global column.
+//
 // Layout: A row-major (lda), rows of this rank = global rows [g0, g0 + m). 8 lanes own one row (4
 // consecutive panel columns each: 16- or 32-byte accesses, a row segment per 8 lanes), 32 rows per
 // 256-thread block, grid-stride over the rows; block partial sums go through LDS, then a
@@ -139,9 +144,10 @@ __global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64
 // next column's S / rowd into Sout (nullptr for the panel's last column).
 template <typename T>
 __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int64_t lda, int64_t g0, int64_t k0,
-                                               int ncols, int j, const double* __restrict__ Sin,
+                                               int64_t coff, int ncols, int j, const double* __restrict__ Sin,
                                                double* __restrict__ Sout, T* __restrict__ tau,
-                                               double* __restrict__ part, unsigned* __restrict__ cnt) {
+                                               double* __restrict__ Y, double* __restrict__ part,
+                                               unsigned* __restrict__ cnt) {
   __shared__ double red[32 * HH_NB];
   __shared__ double sin_[HH_SLEN];
   hh_gather_s(Sin, sin_);
@@ -167,13 +173,22 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
     w[c] = (col > j && col < ncols) ? rd + scale * (sin_[col] - alpha * rd) : 0.0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) tau[j] = (T)tauv;
+  if (Y && blockIdx.x == 0 && threadIdx.x <= j) {
+    // column j of Y = V^T V (the larft input) from the same global sums: v_j = e_d + scale x below
+    // row d, so for c < j  Y[c][j] = v_c[d] + scale (S[c] - alpha v_c[d])  (v_c[d] = rowd[c]) -
+    // the same expression as w_c; Y[j][j] = 1 + scale^2 sig
+    const int c = threadIdx.x;
+    const double rd = sin_[HH_NB + c];
+    Y[c * ncols + j] = c < j ? rd + scale * (sin_[c] - alpha * rd) : 1.0 + scale * scale * sig;
+  }
   const int jl = j & 3, jq = j >> 2;              // lane group slot holding column j
+  const bool wr = 4 * q + 3 >= j;  // columns < j are read (sums), never changed: no store
   const int j1 = j + 1, j1l = j1 & 3, j1q = j1 >> 2;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t i = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3); i < m; i += (int64_t)gridDim.x * 32) {
     const int64_t g = g0 + i;
     if (g < d) continue;  // rows above the diagonal: untouched (the group is uniform in g)
-    T* row = A + i * lda + k0 + 4 * q;
+    T* row = A + i * lda + coff + 4 * q;
     Vec4<T> a = hh_load4(row, nh);
     if (g == d) {
       // the owner writes the R row: beta on the diagonal, rowd[c] - tau w_c right of it
@@ -183,7 +198,7 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
         if (col == j) a.v[c] = (T)beta;
         else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * w[c]);
       }
-      hh_store4(row, a, nh);
+      if (wr) hh_store4(row, a, nh);
       continue;
     }
     // g > d: v_g = x_g / (alpha - beta), A[g][c] -= tau v_g w_c
@@ -195,7 +210,7 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
       if (col == j) a.v[c] = (T)v;
       else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * v * w[c]);
     }
-    hh_store4(row, a, nh);
+    if (wr) hh_store4(row, a, nh);
     if (Sout) {
       // next column's sums over rows g >= d + 1 (all rows handled here), row d + 1's values
       const double x1 = (double)__shfl(a.v[j1l], (threadIdx.x & ~7) + j1q, 64);
@@ -349,17 +364,20 @@ HA_EXPORT int ha_hh_colsums(const void* A, int dtype, int64_t m, int64_t lda, in
 
 // Reflector j of the panel (see the header); Sout (zeroed, 2 NB doubles) receives column j + 1's
 // partial sums unless it is null.
-HA_EXPORT int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols, int j,
-                         const double* Sin, double* Sout, void* tau, double* part, unsigned* cnt, void* stream) {
-  if (ncols <= 0 || ncols > HH_NB || j < 0 || j >= ncols || m < 0) return HA_BAD_ARG;
+// coff: the panel's first column within a row of A (k0 for the matrix itself, 0 for a compact
+// panel copy); Y (nullable, ncols x ncols fp64 row-major): receives column j of V^T V.
+HA_EXPORT int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int64_t coff, int ncols,
+                         int j, const double* Sin, double* Sout, void* tau, double* Y, double* part, unsigned* cnt,
+                         void* stream) {
+  if (ncols <= 0 || ncols > HH_NB || j < 0 || j >= ncols || m < 0 || coff < 0) return HA_BAD_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int grid = hh_grid(m);
   if (dtype == 0)
-    hipLaunchKernelGGL(hh_step<float>, dim3(grid), dim3(256), 0, s, (float*)A, m, lda, g0, k0, ncols, j, Sin, Sout,
-                       (float*)tau, part, cnt);
+    hipLaunchKernelGGL(hh_step<float>, dim3(grid), dim3(256), 0, s, (float*)A, m, lda, g0, k0, coff, ncols, j, Sin,
+                       Sout, (float*)tau, Y, part, cnt);
   else
-    hipLaunchKernelGGL(hh_step<double>, dim3(grid), dim3(256), 0, s, (double*)A, m, lda, g0, k0, ncols, j, Sin, Sout,
-                       (double*)tau, part, cnt);
+    hipLaunchKernelGGL(hh_step<double>, dim3(grid), dim3(256), 0, s, (double*)A, m, lda, g0, k0, coff, ncols, j, Sin,
+                       Sout, (double*)tau, Y, part, cnt);
   return ha_launch_status();
 }
 

@@ -16,6 +16,8 @@
 // Numerics: every product and sum in fp64.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
@@ -308,13 +310,227 @@ __global__ __launch_bounds__(256) void vtc64(const T* __restrict__ V, int64_t ld
     }
 }
 
-// W[e] (+)= sum over splits s = 0, 1, ... of P[s][e], in split order.
-__global__ __launch_bounds__(256) void vtc64_sum(const double* __restrict__ P, int64_t splits, int64_t plane,
-                                                 double* __restrict__ W, int accumulate) {
+// vtc64d: the fp32 form of vtc64 with the operands staged by LDS-DMA (global_load_lds, no
+// register staging) into a 4-stage ring: one barrier per 16-row stage, the DMA of stage t + 3
+// issued right after it, so three stages (~3 x 1.7 us of MFMA work) cover a load's latency - the
+// register-staged kernel prefetched one stage ahead and ran at ~70 % of the fp64 MFMA rate.
+// Stage image of one operand: 8 pieces of 1 KB (one DMA instruction each: lanes 0-31 k-row kk,
+// lanes 32-63 k-row kk + 4, 4 columns per lane), pieces 1088 bytes apart, k-rows paired
+// {0,4} {1,5} {2,6} {3,7} {8,12} ... so the 4 k-rows x 16 columns of one fragment read fall in
+// 64 distinct banks. Rows past the chunk end are clamped in the DMA and zeroed in LDS.
+constexpr int VD_NST = 4, VD_PIECE = 1088, VD_OP = 8 * VD_PIECE, VD_STAGE = 2 * VD_OP;
+
+__device__ __forceinline__ int vd_off(int kk, int col) {
+  return ((kk & 3) + 4 * (kk >> 3)) * VD_PIECE + ((kk >> 2) & 1) * 512 + col * 4;
+}
+
+template <int N>
+__device__ __forceinline__ void vd_wait_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(256, 2) void vtc64d(const float* __restrict__ V, int64_t ldv, const float* __restrict__ C,
+                                                 int64_t ldc, int64_t m, int64_t nc, int64_t N, int64_t chunk,
+                                                 double* __restrict__ P) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[VD_NST * VD_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.y * VT_T, j0 = (int64_t)blockIdx.x * VT_T;
+  const int64_t r0 = (int64_t)blockIdx.z * chunk;
+  const int64_t r1 = r0 + chunk < m ? r0 + chunk : m;
+  const int nst = r1 > r0 ? (int)((r1 - r0 + VT_BK - 1) / VT_BK) : 0;
+  const int wm = wave >> 1, wn = wave & 1;
+  // this lane's DMA sources: pieces p = 2 wave + e of each operand
+  const int cl = (lane & 31) * 4;
+  int kkp[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = 2 * wave + e;
+    kkp[e] = (p & 3) + 8 * (p >> 2) + 4 * (lane >> 5);
+  }
+  const int64_t vcol = i0 + cl + 4 <= nc ? i0 + cl : nc - 4;  // columns past nc / N only feed
+  const int64_t ccol = j0 + cl + 4 <= N ? j0 + cl : N - 4;     // outputs that are never stored
+  auto issue = [&](int t) {
+    unsigned char* dst = smem + (t % VD_NST) * VD_STAGE;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = 2 * wave + e;
+      int64_t g = r0 + (int64_t)t * VT_BK + kkp[e];
+      g = g < r1 ? g : r1 - 1;
+      __builtin_amdgcn_global_load_lds(V + g * ldv + vcol, (__attribute__((address_space(3))) void*)(dst + p * VD_PIECE),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(C + g * ldc + ccol,
+                                       (__attribute__((address_space(3))) void*)(dst + VD_OP + p * VD_PIECE), 16, 0, 0);
+    }
+  };
+  doublex4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (doublex4)(0.0);
+  for (int t = 0; t < VD_NST - 1 && t < nst; ++t) issue(t);
+  for (int t = 0; t < nst; ++t) {
+    const int ahead = nst - 1 - t;  // stages issued after t (at most 2)
+    if (ahead >= 2) vd_wait_barrier<8>();
+    else if (ahead == 1) vd_wait_barrier<4>();
+    else vd_wait_barrier<0>();
+    unsigned char* b = smem + (t % VD_NST) * VD_STAGE;
+    if (r0 + (int64_t)(t + 1) * VT_BK > r1) {
+      // tail stage: zero this wave's k-rows past the chunk end (its own DMA has landed)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int p = 2 * wave + e;
+        if (r0 + (int64_t)t * VT_BK + kkp[e] >= r1) {
+          *reinterpret_cast<floatx4*>(b + p * VD_PIECE + lane * 16) = (floatx4)(0.f);
+          *reinterpret_cast<floatx4*>(b + VD_OP + p * VD_PIECE + lane * 16) = (floatx4)(0.f);
+        }
+      }
+      vd_wait_barrier<0>();
+    }
+    if (t + VD_NST - 1 < nst) issue(t + VD_NST - 1);
+#pragma unroll
+    for (int ks = 0; ks < VT_BK; ks += 4) {
+      const int kk = ks + (lane >> 4);
+      double a[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = (double)*reinterpret_cast<const float*>(b + vd_off(kk, wm * 64 + i * 16 + (lane & 15)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bv[j] = (double)*reinterpret_cast<const float*>(b + VD_OP + vd_off(kk, wn * 64 + j * 16 + (lane & 15)));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  double* Pz = P + (int64_t)blockIdx.z * nc * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gj = j0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t gi = i0 + wm * 64 + i * 16 + (lane >> 4) + 4 * g;
+        if (gi < nc && gj < N) Pz[gi * N + gj] = acc[i][j][g];
+      }
+    }
+}
+
+// vtc32: W = V^T C for a narrow V (nc <= 32: the 32-column panels of the Householder QR, whose
+// inner updates were on the fp64 VALU kernel hh_vtc at ~0.5 TB/s). Tile 32 x 256 per workgroup
+// (wave w: all 32 rows x columns 64 w .. 64 w + 63 = 2 x 4 v_mfma_f64_16x16x4_f64 blocks); the MFMA
+// operands are loaded straight from global memory (lane (k = lane >> 4, c = lane & 15): V[g][16 i + c]
+// and C[g][j0 + 16 j + c], rows g = r + k), 8 k-steps (32 rows) per batch so 48 loads are in flight
+// per lane, two waves per SIMD. Split-K partials as vtc64.
+__global__ __launch_bounds__(256, 2) void vtc32(const float* __restrict__ V, int64_t ldv, const float* __restrict__ C,
+                                             int64_t ldc, int64_t m, int64_t nc, int64_t N, int64_t chunk,
+                                             double* __restrict__ P) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kr = lane >> 4, cc = lane & 15;
+  const int64_t j0 = (int64_t)blockIdx.x * 256 + wave * 64;
+  const int64_t r0 = (int64_t)blockIdx.z * chunk;
+  const int64_t r1 = r0 + chunk < m ? r0 + chunk : m;
+  bool vok[2], cok[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) vok[i] = 16 * i + cc < nc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cok[j] = j0 + 16 * j + cc < N;
+  doublex4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (doublex4)(0.0);
+  // out-of-range rows / columns: clamped addresses, the loaded value replaced by 0
+  int vcol[2];
+  int64_t ccol[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) vcol[i] = vok[i] ? 16 * i + cc : 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ccol[j] = cok[j] ? j0 + 16 * j + cc : 0;
+  for (int64_t r = r0; r < r1; r += 32) {
+    float va[8][2], cv[8][4];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int64_t g0 = r + 4 * s + kr;
+      const bool ok = g0 < r1;
+      const int64_t g = ok ? g0 : r1 - 1;
+      const float* vr = V + g * ldv;
+      const float* cr = C + g * ldc;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float x = vr[vcol[i]];
+        va[s][i] = ok && vok[i] ? x : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = cr[ccol[j]];
+        cv[s][j] = ok && cok[j] ? x : 0.f;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)va[s][i], (double)cv[s][j], acc[i][j], 0, 0, 0);
+  }
+  double* Pz = P + (int64_t)blockIdx.z * nc * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gj = j0 + 16 * j + cc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t gi = 16 * i + kr + 4 * g;
+        if (gi < nc && gj < N) Pz[gi * N + gj] = acc[i][j][g];
+      }
+    }
+}
+
+// W[e] (+)= sum over z = 0, 1, ... < count of P[z stride + e], in z order (8 loads in flight).
+__global__ __launch_bounds__(256) void vtc64_sum(const double* __restrict__ P, int64_t count, int64_t stride,
+                                                 int64_t plane, double* __restrict__ W, int accumulate) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < plane; e += (int64_t)gridDim.x * 256) {
     double s = accumulate ? W[e] : 0.0;
-    for (int64_t z = 0; z < splits; ++z) s += P[z * plane + e];
+    int64_t z = 0;
+    for (; z + 8 <= count; z += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = P[(z + u) * stride + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; z < count; ++z) s += P[z * stride + e];
     W[e] = s;
+  }
+}
+
+// First level of a two-level fixed-order split sum (many splits, small plane): P[q G][e] =
+// sum of P[z][e] for z in [q G, q G + G), in z order - every element is read and written by one
+// thread, so the group's first slot is overwritten in place.
+__global__ __launch_bounds__(256) void vtc64_group_sum(double* __restrict__ P, int64_t splits, int64_t plane, int G) {
+  const int64_t ngroups = (splits + G - 1) / G;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < ngroups * plane;
+       idx += (int64_t)gridDim.x * 256) {
+    const int64_t q = idx / plane, e = idx % plane;
+    const int64_t z0 = q * G, z1 = z0 + G < splits ? z0 + G : splits;
+    double s = 0.0;
+    int64_t z = z0;
+    for (; z + 8 <= z1; z += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = P[(z + u) * plane + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; z < z1; ++z) s += P[z * plane + e];
+    P[z0 * plane + e] = s;
   }
 }
 
@@ -356,6 +572,14 @@ HA_EXPORT int ha_gemm64(const double* A, const double* B, double* C, int64_t M, 
 // with >= 32 stages per split; the caller sizes the partial buffer as splits * nc * N doubles.
 HA_EXPORT int64_t ha_vtc64_splits(int64_t m, int64_t nc, int64_t N) {
   if (m <= 0 || nc <= 0 || N <= 0) return 1;
+  if (nc <= 32) {  // vtc32: 32 x 256 tiles, >= ~512 workgroups, >= 64 rows per split
+    const int64_t tiles = (N + 255) / 256;
+    int64_t s = (512 + tiles - 1) / tiles;
+    const int64_t maxs = (m + 63) / 64;
+    if (s > maxs) s = maxs;
+    if (s > 65535) s = 65535;
+    return s < 1 ? 1 : s;
+  }
   const int64_t tiles = ((nc + VT_T - 1) / VT_T) * ((N + VT_T - 1) / VT_T);
   int64_t s = (1024 + tiles - 1) / tiles;
   const int64_t maxs = (m + 32 * VT_BK - 1) / (32 * VT_BK);
@@ -380,10 +604,18 @@ HA_EXPORT int ha_vtc64(const void* V, int64_t ldv, const void* C, int64_t ldc, i
   const int64_t splits = ha_vtc64_splits(m, nc, N);
   const int64_t chunk = ((m + splits - 1) / splits + VT_BK - 1) / VT_BK * VT_BK;
   const dim3 grid((unsigned)((N + VT_T - 1) / VT_T), (unsigned)((nc + VT_T - 1) / VT_T), (unsigned)splits);
-  if (dtype == 0) {
+  if (dtype == 0 && nc <= 32) {
+    const int64_t chunk32 = ((m + splits - 1) / splits + 31) / 32 * 32;
+    hipLaunchKernelGGL(vtc32, dim3((unsigned)((N + 255) / 256), 1, (unsigned)splits), dim3(256), 0, s,
+                       (const float*)V, ldv, (const float*)C, ldc, m, nc, N, chunk32, P);
+  } else if (dtype == 0) {
     const bool v4 = nc % 4 == 0 && N % 4 == 0 && ldv % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)V & 15) == 0 &&
                     ((uintptr_t)C & 15) == 0;
-    if (v4)
+    static const bool v1 = getenv("HEAT_VTC64_V1") && atoi(getenv("HEAT_VTC64_V1"));  // A/B: register staging
+    if (v4 && !v1)
+      hipLaunchKernelGGL(vtc64d, grid, dim3(256), 0, s, (const float*)V, ldv, (const float*)C, ldc, m, nc, N, chunk,
+                         P);
+    else if (v4)
       hipLaunchKernelGGL((vtc64<float, 4>), grid, dim3(256), 0, s, (const float*)V, ldv, (const float*)C, ldc, m, nc,
                          N, chunk, P);
     else
@@ -401,8 +633,17 @@ HA_EXPORT int ha_vtc64(const void* V, int64_t ldv, const void* C, int64_t ldc, i
   }
   const int64_t plane = nc * N;
   const int64_t g = (plane + 255) / 256;
-  hipLaunchKernelGGL(vtc64_sum, dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0, s, P, splits, plane, W,
-                     accumulate);
+  if (splits > 64 && g < 256) {
+    // few output elements, many splits: sum groups of 32 splits in parallel first
+    constexpr int G = 32;
+    const int64_t ng = (splits + G - 1) / G;
+    const int64_t g1 = (ng * plane + 255) / 256;
+    hipLaunchKernelGGL(vtc64_group_sum, dim3((unsigned)(g1 < 8192 ? g1 : 8192)), dim3(256), 0, s, P, splits, plane, G);
+    hipLaunchKernelGGL(vtc64_sum, dim3((unsigned)g), dim3(256), 0, s, P, ng, G * plane, plane, W, accumulate);
+  } else {
+    hipLaunchKernelGGL(vtc64_sum, dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0, s, P, splits, plane, plane, W,
+                       accumulate);
+  }
   return ha_launch_status();
 }
 

@@ -1378,7 +1378,9 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
     block; the outer block is then applied to the trailing matrix as ONE block reflector
     Q_b = I - V T V^T with T = (striu(V^T V) + diag(1/tau))^-1 (``tri_inv_upper``), W = V^T C
     from the fp64 matrix-core kernel (``csrc/linalg64.hip: vtc64``, exact products, split-K in
-    fixed order) and C -= V (T^T W) on the exact-fp32 MFMA GEMM (``gemm_f32``). No library GEMM."""
+    fixed order) and C -= V (T^T W) as one fp32 GEMM (hipBLASLt: a plain small-K update, see
+    ``_HH_UPDATE``). Each 32-column panel is factored in a compact m x 32 copy and its V^T V comes
+    from the column sums of the steps (no separate pass)."""
     m_r, n = local.shape
     m_total = m_r if m_total is None else m_total
     native = local.is_cuda and use_native(local)
@@ -1406,8 +1408,12 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
             nc = min(nb, K0 + ncol - k0)
             S = torch.zeros((nc + 1, slen), dtype=torch.float64, device=dev)
             tau = torch.empty(nc, dtype=dt, device=dev)
+            Y = torch.zeros((nc, nc), dtype=torch.float64, device=dev)  # V^T V, written by the steps
             if native:
-                check(L.ha_hh_colsums(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, k0, _ptr(S[0]), _ptr(hpart),
+                # the panel in a compact m x nc copy: the nc + 1 passes stream contiguous rows
+                # instead of one 128-byte segment per (16 KB) matrix row
+                Pb = A[:, k0: k0 + nc].contiguous()
+                check(L.ha_hh_colsums(_ptr(Pb), code, m_r, nc, g0, 0, nc, k0, _ptr(S[0]), _ptr(hpart),
                                       _ptr(hcnt), st), "ha_hh_colsums")
             else:
                 _hh_colsums_host(A, rows, k0, nc, S[0])
@@ -1415,30 +1421,31 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
             for j in range(nc):
                 last = j + 1 == nc
                 if native:
-                    check(L.ha_hh_step(_ptr(A), code, m_r, A.stride(0), g0, k0, nc, j, _ptr(S[j]),
-                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), _ptr(hpart), _ptr(hcnt),
-                                       st), "ha_hh_step")
+                    check(L.ha_hh_step(_ptr(Pb), code, m_r, nc, g0, k0, 0, nc, j, _ptr(S[j]),
+                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), _ptr(Y), _ptr(hpart),
+                                       _ptr(hcnt), st), "ha_hh_step")
                 else:
-                    _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau)
+                    _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau, Y)
                 if not last:
                     red(S[j + 1])
             taus.append(tau)
-            V = _hh_v(A, rows, k0, nc)
-            Y = _vtc(V, V, native, st)   # V^T V, fp64 accumulation (a tall-skinny fp64 BLAS GEMM is slow)
-            red(Y)
+            if native:
+                A[:, k0: k0 + nc] = Pb
+                V = _hh_v_fix(Pb, rows, k0, g0)
+            else:
+                V = _hh_v(A, rows, k0, nc, g0)
             Tm = torch.empty((nc, nc), dtype=dt, device=dev)
             if native:
-                check(L.ha_hh_larft(_ptr(Y.contiguous()), _ptr(tau), nc, code, _ptr(Tm), st), "ha_hh_larft")
+                check(L.ha_hh_larft(_ptr(Y), _ptr(tau), nc, code, _ptr(Tm), st), "ha_hh_larft")
             else:
                 Tm.copy_(_hh_larft_host(Y, tau))
             inner.append(Tm)
             if k0 + nc < K0 + ncol:        # the rest of this outer block
                 _hh_block_update(A[:, k0 + nc: K0 + ncol], V, Tm, True, native, st, red)
+        V = _hh_v(A, rows, K0, ncol, g0)
         if len(inner) == 1:
             Tb = inner[0].double()
-            V = _hh_v(A, rows, K0, ncol)
         else:
-            V = _hh_v(A, rows, K0, ncol)
             Y = _vtc(V, V, native, st)
             red(Y)
             tinv = torch.triu(Y, diagonal=1)
@@ -1467,7 +1474,7 @@ def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, tra
     red = allreduce or (lambda t: t)
     rows = torch.arange(g0, g0 + A.shape[0], device=A.device).unsqueeze(1)
     for k0, nc, Tm in (panels if transpose else list(reversed(panels))):
-        V = _hh_v(A, rows, k0, nc)
+        V = _hh_v(A, rows, k0, nc, g0)
         # C = [I; 0] accumulation: columns before k0 are still unit vectors that V (zero above
         # global row k0) does not touch
         Cc = C[:, k0:] if identity_start else C
@@ -1475,14 +1482,37 @@ def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, tra
     return C
 
 
-_HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "f32")   # f32 (exact MFMA) | h3 (fp16x3 MFMA) | blas
+# the rank-nc update C -= V X of the Householder QR: blas (hipBLASLt fp32) | f32 (gemm_f32t) | h3
+# (fp16x3 MFMA). The update is a plain fp32 GEMM with a small K (256 outer / 32 inner) and a tall
+# C that is read and written once; measured at 1.25e6 rows (tools/microbench/hh_parts.py,
+# profiles/householder_r04.md): K = 256, N = 3840: hipBLASLt 19.8 ms vs gemm_f32t 32.2 ms;
+# K = 32, N = 224 (strided C): 0.60 vs 1.25 ms - gemm_f32t's 256 x 256 tile pays its prologue and
+# C epilogue per 16 k-stages there. The blas form runs at float32 matmul precision "highest" whatever
+# the caller set: under "high" hipBLASLt drops to a reduced-precision fp32 path (measured ||Q^T Q - I||
+# 1.5e-5 instead of 1.2e-7, tools/microbench/hh_prec.py), and the Householder path is the backward-
+# stable one.
+_HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "blas")
+
+
+def _exact_addmm_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: float) -> None:
+    """C += alpha A B through the library GEMM with exact fp32 products (precision "highest" for the
+    duration of the call)."""
+    prev = torch.get_float32_matmul_precision()
+    if prev == "highest":
+        C.addmm_(A, B, alpha=alpha)
+        return
+    torch.set_float32_matmul_precision("highest")
+    try:
+        C.addmm_(A, B, alpha=alpha)
+    finally:
+        torch.set_float32_matmul_precision(prev)
 
 
 def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpose: bool, native: bool, st,
                      red) -> None:
     """C -= V op(T) (V^T C) in place: W = V^T C with fp64 accumulation (summed over the ranks by
-    ``red``), X = op(T) W in fp64 (``gemm64``), then the rank-nc update on the hand-written MFMA
-    GEMMs (fp32: ``gemm_f32`` exact / ``gemm_h3``; fp64: ``gemm64``)."""
+    ``red``), X = op(T) W in fp64 (``gemm64``), then the rank-nc update (fp32: hipBLASLt, see
+    ``_HH_UPDATE``; fp64: ``gemm64``)."""
     if C.shape[1] == 0 or V.shape[1] == 0:
         return
     W = _vtc(V, C, native, st)
@@ -1490,7 +1520,7 @@ def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpo
     T64 = Tm.double()
     Tt = T64.T if transpose else T64
     if not native:
-        C.addmm_(V, (Tt @ W).to(C.dtype), alpha=-1.0)
+        _exact_addmm_(C, V, (Tt @ W).to(C.dtype), -1.0)
         return
     X = gemm64(Tt, W)
     if C.dtype == torch.float64:
@@ -1498,7 +1528,7 @@ def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpo
         return
     X = X.to(C.dtype)
     if C.stride(1) != 1 or _HH_UPDATE == "blas":
-        C.addmm_(V, X, alpha=-1.0)
+        _exact_addmm_(C, V, X, -1.0)
     elif _HH_UPDATE == "h3" and gemm_h3(V, X, out=C, alpha=-1.0, accumulate=True) is not None:
         pass
     else:
@@ -1538,16 +1568,16 @@ def vtc64(V: torch.Tensor, C: torch.Tensor, out: Optional[torch.Tensor] = None,
 
 
 def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:
-    """V^T C in fp64 accumulation: panels up to the 32-column panel width on the VALU kernel
-    (``hh_vtc``, memory-bound there), wider block reflectors on the fp64 matrix cores
-    (:func:`vtc64`); host: an fp64 GEMM."""
+    """V^T C in fp64 accumulation on the fp64 matrix cores (:func:`vtc64`: ``vtc32`` for fp32
+    panels up to 32 columns, the 128-tile kernels for wider block reflectors); fp64 panels on the
+    VALU kernel ``hh_vtc``; host: an fp64 GEMM."""
     if not native:
         return V.double().T @ C.double()
     nc, N = V.shape[1], C.shape[1]
     if C.stride(1) != 1:
         C = C.contiguous()
     L = lib()
-    if nc > L.ha_hh_nb():
+    if nc > L.ha_hh_nb() or V.dtype == torch.float32:  # fp32 panels: the narrow MFMA kernel vtc32
         return vtc64(V, C)
     W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)
     P = torch.empty(max(1, L.ha_hh_vtc_splits(V.shape[0], N) * nc * N), dtype=torch.float64, device=V.device)
@@ -1556,12 +1586,23 @@ def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:
     return W
 
 
-def _hh_v(A: torch.Tensor, rows: torch.Tensor, k0: int, nc: int) -> torch.Tensor:
+def _hh_v(A: torch.Tensor, rows: torch.Tensor, k0: int, nc: int, g0: int) -> torch.Tensor:
     """Explicit reflectors of a factorised panel: V[g, c] = A[g, k0 + c] below the diagonal row
-    k0 + c, 1 on it, 0 above."""
-    dcol = torch.arange(k0, k0 + nc, device=A.device).unsqueeze(0)
-    P = A[:, k0: k0 + nc]
-    return torch.where(rows > dcol, P, (rows == dcol).to(A.dtype))
+    k0 + c, 1 on it, 0 above (a contiguous copy of the columns; only the local rows above global
+    row k0 + nc need the mask)."""
+    return _hh_v_fix(A[:, k0: k0 + nc].clone(memory_format=torch.contiguous_format), rows, k0, g0)
+
+
+def _hh_v_fix(P: torch.Tensor, rows: torch.Tensor, k0: int, g0: int) -> torch.Tensor:
+    """In place: the rows of a contiguous panel copy P (global rows g0 ...) above global row
+    k0 + P.shape[1] become the unit-lower reflector rows (1 on the diagonal, 0 above)."""
+    nc = P.shape[1]
+    top = min(max(k0 + nc - g0, 0), P.shape[0])
+    if top:
+        dcol = torch.arange(k0, k0 + nc, device=P.device).unsqueeze(0)
+        r = rows[:top]
+        P[:top] = torch.where(r > dcol, P[:top], (r == dcol).to(P.dtype))
+    return P
 
 
 # host (CPU) reference of the panel kernels: same math, same buffer conventions (the oracle of the
@@ -1575,7 +1616,7 @@ def _hh_colsums_host(A, rows, k0, nc, S):
         S[32: 32 + nc] += A[own, k0: k0 + nc].double().reshape(-1)
 
 
-def _hh_step_host(A, rows, k0, nc, j, Sin, Sout, tau):
+def _hh_step_host(A, rows, k0, nc, j, Sin, Sout, tau, Y=None):
     d = k0 + j
     alpha = float(Sin[32 + j])
     nrm2 = float(Sin[j])
@@ -1589,6 +1630,9 @@ def _hh_step_host(A, rows, k0, nc, j, Sin, Sout, tau):
     tau[j] = tv
     rd = Sin[32: 32 + nc]
     w = rd + scale * (Sin[:nc] - alpha * rd)
+    if Y is not None:  # column j of V^T V from the same sums (see csrc/householder.hip: hh_step)
+        Y[:j, j] = w[:j]
+        Y[j, j] = 1.0 + scale * scale * sig
     w[: j + 1] = 0.0
     g = rows[:, 0]
     own = g == d

@@ -151,11 +151,12 @@ def test_cholqr_native_path(m, n, precision):
 
 # ------------------------------------------------- two-level Householder / fp64 V^T C / split-K Gram
 @pytest.mark.parametrize("m,nc,N", [(100_000, 256, 1000), (5000, 256, 256), (777, 130, 333), (64, 3, 5),
-                                    (300_001, 128, 128)])
+                                    (300_001, 128, 128), (400_003, 32, 224), (70_000, 17, 300), (1000, 32, 31)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_vtc64(m, nc, N, dtype):
     """V^T C on the fp64 matrix cores: exact products, fp64 accumulation, against an fp64 GEMM
-    (vector and scalar load variants, row/column edges, split-K chunk tails)."""
+    (vector and scalar load variants, the narrow nc <= 32 kernel with its two-level split sum,
+    row/column edges, split-K chunk tails)."""
     from heat_amd import ops
 
     dev = _dev()
@@ -198,12 +199,25 @@ def test_gram64_split_k(m, n, group_bytes, exact, monkeypatch):
     assert rel < 10 * 2.0 ** -24 * kc / m ** 0.5, rel
 
 
-def test_householder_two_level_orthogonality_fp32():
-    """fp32 Householder with 256-column block reflectors (vtc64 + exact fp32 MFMA update): Q is
-    orthogonal to < 1e-6 for an ill-conditioned input, R matches the host algorithm."""
+@pytest.mark.parametrize("precision", ["highest", "high"])
+def test_householder_two_level_orthogonality_fp32(precision):
+    """fp32 Householder with 256-column block reflectors (vtc64 + exact fp32 library update): Q is
+    orthogonal to < 1e-6 for an ill-conditioned input, R matches the host algorithm - also when
+    the caller set float32 matmul precision "high" (the update must not take the reduced-precision
+    library path then)."""
     from heat_amd import ops
 
     dev = _dev()
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(precision)
+    try:
+        _householder_two_level_check(dev, ops)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    assert torch.get_float32_matmul_precision() == prev
+
+
+def _householder_two_level_check(dev, ops):
     a = _ill(60_000, 640, 1e8, 9, torch.float32)
     q, r = ops.householder_qr(a.to(dev), 0, a.shape[0], True)
     Q = q.double()

@@ -39,7 +39,7 @@ def test_outer_block_T_is_the_larft_product(monkeypatch):
     assert [(k0, nc) for k0, nc, _ in panels] == [(0, 64), (64, 36)]
     rows = torch.arange(200).unsqueeze(1)
     for k0, nc, T in panels:
-        V = K._hh_v(A, rows, k0, nc)
+        V = K._hh_v(A, rows, k0, nc, 0)
         Qb = torch.eye(200, dtype=torch.float64) - V @ T @ V.T
         prod = torch.eye(200, dtype=torch.float64)
         for c in range(nc):

@@ -38,8 +38,8 @@ int ha_gemm_h3t(const void* Ahi, const void* Alo, const void* Bhi, const void* B
                 int upper, int64_t slices, int64_t cslice, void* stream);
 int ha_hh_colsums(const void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols, int64_t d,
                   double* S, double* part, unsigned* cnt, void* stream);
-int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int ncols, int j, const double* Sin,
-               double* Sout, void* tau, double* part, unsigned* cnt, void* stream);
+int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int64_t coff, int ncols, int j,
+               const double* Sin, double* Sout, void* tau, double* Y, double* part, unsigned* cnt, void* stream);
 int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counter_lo, uint64_t counter_hi, uint64_t seed,
                      int bits, int dist, double low, double span, void* stream);
 }
@@ -105,7 +105,10 @@ int main() {
                     nullptr) == BAD);  // Mp < M
   CHECK(ha_hh_colsums(dummy, 0, 10, 4, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr) == BAD);
   CHECK(ha_hh_colsums(dummy, 0, 10, 4, 0, 0, 99, 0, nullptr, nullptr, nullptr, nullptr) == BAD);
-  CHECK(ha_hh_step(dummy, 0, 10, 4, 0, 0, 4, 4, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) == BAD);
+  CHECK(ha_hh_step(dummy, 0, 10, 4, 0, 0, 0, 4, 4, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) ==
+        BAD);  // j >= ncols
+  CHECK(ha_hh_step(dummy, 0, 10, 4, 0, 0, -1, 4, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) ==
+        BAD);  // coff < 0
   CHECK(ha_threefry_fill(dummy, 0, 0, 0, 0, 1, 32, 0, 0.0, 1.0, nullptr) == OK);
   CHECK(ha_threefry_fill(dummy, 0, 4, 0, 0, 1, 16, 0, 0.0, 1.0, nullptr) == BAD);
   if (fails) {

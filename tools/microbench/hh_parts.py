@@ -2,6 +2,7 @@
   * one 32-column panel (hh_colsums + 32 hh_step launches) on a column slice of the full matrix
     (row pitch 4096) vs the same panel in a compact m x 32 buffer (row pitch 32);
   * the trailing update C -= V X (K = 256, N = 3840) on gemm_f32t vs hipBLASLt (torch addmm_);
+    the inner panel update (K = 32, N = 224, C a column slice of the matrix) the same way;
   * W = V^T C (nc = 256, N = 3840) on vtc64 (fp64 matrix cores).
 One JSON line per measurement."""
 import ctypes
@@ -71,6 +72,15 @@ def main():
     Cc.copy_(C)
     t_f32c = timed(lambda: K.gemm_f32(V, X, out=Cc, accumulate=True, alpha=-1.0))
     t_vtcc = timed(lambda: K.vtc64(V, Cc))
+    Vi = V[:, :32].contiguous()
+    Xi = X[:32, :224].contiguous()
+    Ci = A[:, 32:256]
+    fi = 2.0 * m * 32 * 224
+    ti_f32 = timed(lambda: K.gemm_f32(Vi, Xi, out=Ci, accumulate=True, alpha=-1.0))
+    ti_blas = timed(lambda: Ci.addmm_(Vi, Xi, alpha=-1.0))
+    ti_vtc = timed(lambda: K._vtc(Vi, Ci, True, st))
+    print(json.dumps({"piece": "inner_k32_n224", "gemm_f32t_ms": ti_f32, "hipblaslt_ms": ti_blas,
+                      "hh_vtc_ms": ti_vtc, "gemm_f32t_tf": fi / ti_f32 / 1e9}), flush=True)
     print(json.dumps({"piece": "update_k256_contig", "gemm_f32t_ms": t_f32c, "gemm_f32t_tf": flops / t_f32c / 1e9,
                       "vtc64_ms": t_vtcc, "vtc64_tf": flops / t_vtcc / 1e9}), flush=True)
 
