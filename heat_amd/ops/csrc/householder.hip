@@ -140,6 +140,50 @@ __global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64
   hh_block_sum(acc, S, red, part, cnt);
 }
 
+// rows per thread and sweep in hh_step, loads issued before the first use. 4 measured SLOWER:
+// 4.34 vs 2.74 ms per 32-column panel at 1.25e6 rows (tools/microbench/hh_parts.py, r4t)
+constexpr int HH_ROWS = 1;
+
+// hh_step's work on one row g >= d (a: the row's 4 panel values of this lane, already loaded)
+template <typename T>
+__device__ __forceinline__ void hh_step_row(Vec4<T>& a, T* row, int64_t g, int64_t d, int j, int jl, int jq, int j1l,
+                                            int j1q, int q, int ncols, int nh, bool wr, double beta, double tauv,
+                                            double scale, const double (&w)[4], double* __restrict__ Sout,
+                                            double (&acc)[4]) {
+  if (g == d) {
+    // the owner writes the R row: beta on the diagonal, rowd[c] - tau w_c right of it
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = 4 * q + c;
+      if (col == j) a.v[c] = (T)beta;
+      else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * w[c]);
+    }
+    if (wr) hh_store4(row, a, nh);
+    return;
+  }
+  // g > d: v_g = x_g / (alpha - beta), A[g][c] -= tau v_g w_c
+  const T xj = __shfl(a.v[jl], (threadIdx.x & ~7) + jq, 64);
+  const double v = (double)xj * scale;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int col = 4 * q + c;
+    if (col == j) a.v[c] = (T)v;
+    else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * v * w[c]);
+  }
+  if (wr) hh_store4(row, a, nh);
+  if (Sout) {
+    // next column's sums over rows g >= d + 1 (all rows handled here), row d + 1's values
+    const double x1 = (double)__shfl(a.v[j1l], (threadIdx.x & ~7) + j1q, 64);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] += x1 * (double)a.v[c];
+    if (g == d + 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < nh) Sout[HH_NB + 4 * q + c] = (double)a.v[c];  // row d + 1: one writer
+    }
+  }
+}
+
 // One panel column: apply reflector j (from Sin) to this rank's rows, store v / R, accumulate the
 // next column's S / rowd into Sout (nullptr for the panel's last column).
 template <typename T>
@@ -185,42 +229,22 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
   const bool wr = 4 * q + 3 >= j;  // columns < j are read (sums), never changed: no store
   const int j1 = j + 1, j1l = j1 & 3, j1q = j1 >> 2;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t i = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3); i < m; i += (int64_t)gridDim.x * 32) {
-    const int64_t g = g0 + i;
-    if (g < d) continue;  // rows above the diagonal: untouched (the group is uniform in g)
-    T* row = A + i * lda + coff + 4 * q;
-    Vec4<T> a = hh_load4(row, nh);
-    if (g == d) {
-      // the owner writes the R row: beta on the diagonal, rowd[c] - tau w_c right of it
+  const int64_t stride = (int64_t)gridDim.x * 32;
+  for (int64_t i0 = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3); i0 < m; i0 += HH_ROWS * stride) {
+    Vec4<T> a[HH_ROWS];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int col = 4 * q + c;
-        if (col == j) a.v[c] = (T)beta;
-        else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * w[c]);
-      }
-      if (wr) hh_store4(row, a, nh);
-      continue;
+    for (int u = 0; u < HH_ROWS; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < m && g0 + i >= d) a[u] = hh_load4(A + i * lda + coff + 4 * q, nh);
     }
-    // g > d: v_g = x_g / (alpha - beta), A[g][c] -= tau v_g w_c
-    const T xj = __shfl(a.v[jl], (threadIdx.x & ~7) + jq, 64);
-    const double v = (double)xj * scale;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int col = 4 * q + c;
-      if (col == j) a.v[c] = (T)v;
-      else if (col > j && col < ncols) a.v[c] = (T)((double)a.v[c] - tauv * v * w[c]);
-    }
-    if (wr) hh_store4(row, a, nh);
-    if (Sout) {
-      // next column's sums over rows g >= d + 1 (all rows handled here), row d + 1's values
-      const double x1 = (double)__shfl(a.v[j1l], (threadIdx.x & ~7) + j1q, 64);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] += x1 * (double)a.v[c];
-      if (g == d + 1) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c < nh) Sout[HH_NB + 4 * q + c] = (double)a.v[c];  // row d + 1: one writer
-      }
+    for (int u = 0; u < HH_ROWS; ++u) {
+      const int64_t i = i0 + u * stride;
+      const int64_t g = g0 + i;
+      // rows above the diagonal: untouched (the group is uniform in g)
+      if (i >= m || g < d) continue;
+      T* row = A + i * lda + coff + 4 * q;
+      hh_step_row(a[u], row, g, d, j, jl, jq, j1l, j1q, q, ncols, nh, wr, beta, tauv, scale, w, Sout, acc);
     }
   }
   if (Sout) hh_block_sum(acc, Sout, red, part, cnt);

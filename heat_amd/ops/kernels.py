@@ -1567,16 +1567,62 @@ def vtc64(V: torch.Tensor, C: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
+# 1024-row slices: on the cond-1e8 test matrix ||QR - A|| is 4.5e-6 (4.2e-6 with exact fp64 V^T C)
+# vs 1.3e-5 with 4096-row slices, for 2 % of the QR time (tools/microbench/hh_variants.py, r4t)
+_VTC_KCHUNK = max(256, int(os.environ.get("HEAT_VTC_KCHUNK", "1024")) // 256 * 256)
+_VTC_WIDE = os.environ.get("HEAT_HH_VTC", "f32s")   # f32s (sliced fp32 MFMA) | f64 (vtc64)
+
+
+def vtc_f32s(V: torch.Tensor, C: torch.Tensor) -> Optional[torch.Tensor]:
+    """``V^T C`` ([nc, N] fp64) of fp32 device blocks on the f32-input matrix cores: the exact-fp32
+    256-tile GEMM (``csrc/gemm_tiled.hip: gemm_f32t``) split over K slices of ``HEAT_VTC_KCHUNK``
+    = 1024 rows (fp32 accumulation inside a slice, a 256 x 256 tile per workgroup), the slices
+    summed in fp64 in fixed order (``ha_sum_slices64``) - the Gram's accumulation scheme
+    (:func:`gram64`). Error ~ u sqrt(chunk) / sqrt(m / chunk) |v||c| < 1 u |v||c| at m = 1.25e6,
+    below the fp32 rounding of the Householder update that consumes W; ~2.5x the fp64-MFMA rate
+    of :func:`vtc64`. Returns None when the operands do not fit the tiled kernel (alignment)."""
+    m, nc = V.shape
+    N = C.shape[1]
+    W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)
+    if m == 0 or nc == 0 or N == 0:
+        return W
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(V.device))
+    kc = _VTC_KCHUNK
+    group = max(1, min(-(-m // kc), _GRAM_PARTIAL_BYTES // (4 * nc * N)))
+    P = torch.empty(group * nc * N, dtype=torch.float32, device=V.device)
+    for k0 in range(0, m, group * kc):
+        k1 = min(m, k0 + group * kc)
+        slices = -(-(k1 - k0) // kc)
+        Vs, Cs = V[k0:k1], C[k0:k1]
+        # A = V^T: k-major (rows of V contiguous along nc); B = C: k-major (rows contiguous along N)
+        rc = L.ha_gemm_f32t(_ptr(Vs), _ptr(Cs), _ptr(P), nc, N, k1 - k0, Vs.stride(0), Cs.stride(0), N, 1, 1,
+                            1.0, 0, 0, slices, nc * N, st)
+        if rc == _HA_UNSUPPORTED:
+            return None
+        check(rc, "ha_gemm_f32t")
+        used = L.ha_gemm_tiled_slices(k1 - k0, slices)
+        check(L.ha_sum_slices64(_ptr(P), used, nc, N, nc * N, _ptr(W), N, 0, 1, st), "ha_sum_slices64")
+    return W
+
+
 def _vtc(V: torch.Tensor, C: torch.Tensor, native: bool, st) -> torch.Tensor:
-    """V^T C in fp64 accumulation on the fp64 matrix cores (:func:`vtc64`: ``vtc32`` for fp32
-    panels up to 32 columns, the 128-tile kernels for wider block reflectors); fp64 panels on the
-    VALU kernel ``hh_vtc``; host: an fp64 GEMM."""
+    """V^T C with fp64 accumulation across the rows: fp32 block reflectors wider than a panel on
+    the sliced fp32 matrix-core GEMM (:func:`vtc_f32s`), fp32 panels up to 32 columns on the
+    narrow fp64-MFMA kernel ``vtc32`` (:func:`vtc64`; ``HEAT_HH_VTC=f64`` sends the wide ones
+    there too); fp64 panels on the VALU kernel ``hh_vtc``; host: an fp64 GEMM."""
     if not native:
         return V.double().T @ C.double()
     nc, N = V.shape[1], C.shape[1]
     if C.stride(1) != 1:
         C = C.contiguous()
     L = lib()
+    if V.dtype == torch.float32 and nc > L.ha_hh_nb() and _VTC_WIDE == "f32s":
+        if V.stride(1) != 1 or V.stride(0) < nc:
+            V = V.contiguous()
+        W = vtc_f32s(V, C)
+        if W is not None:
+            return W
     if nc > L.ha_hh_nb() or V.dtype == torch.float32:  # fp32 panels: the narrow MFMA kernel vtc32
         return vtc64(V, C)
     W = torch.zeros((nc, N), dtype=torch.float64, device=V.device)

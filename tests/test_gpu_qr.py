@@ -174,6 +174,32 @@ def test_vtc64(m, nc, N, dtype):
     assert torch.equal(ops.vtc64(V, C), W)
 
 
+@pytest.mark.parametrize("m,nc,N,group_bytes", [(300_001, 256, 1000, 1 << 30), (100_000, 256, 3840, 1 << 24),
+                                               (5000, 64, 256, 1 << 30), (70_000, 36, 300, 1 << 30)])
+def test_vtc_f32s(m, nc, N, group_bytes, monkeypatch):
+    """The sliced fp32-MFMA V^T C of the Householder update: fp32 sums inside 1024-row slices,
+    fp64 across them (partial-buffer groups, slice tails), against an fp64 GEMM; deterministic;
+    the wide-reflector path of _vtc uses it."""
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    monkeypatch.setattr(K, "_GRAM_PARTIAL_BYTES", group_bytes)
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + nc + N)
+    V = torch.randn(m, nc, generator=g).to(dev)
+    C = torch.randn(m, N, generator=g).to(dev)
+    W = K.vtc_f32s(V, C)
+    assert W is not None and W.dtype == torch.float64
+    ref = V.double().T @ C.double()
+    bound = V.double().abs().T @ C.double().abs()
+    rel = ((W - ref).abs() / bound).max().item()
+    # one slice: fp32 accumulation of 1024 products (~u sqrt(1024) / 3 typical); the slices'
+    # errors are independent, so the whole sum stays near that
+    assert rel < 16 * 2.0 ** -24, rel
+    assert torch.equal(K.vtc_f32s(V, C), W)
+    assert torch.equal(K._vtc(V, C, True, None), W)
+
+
 @pytest.mark.parametrize("exact", [True, False])
 @pytest.mark.parametrize("m,n,group_bytes", [(200_000, 512, 1 << 30), (100_000, 300, 1 << 20), (9000, 256, 1 << 30),
                                               (50_000, 64, 1 << 16)])
