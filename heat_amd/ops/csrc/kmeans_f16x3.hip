@@ -969,7 +969,10 @@ __device__ __forceinline__ void topk_insert_ev(float (&tv)[KP], int (&ti)[KP], f
 // its threshold makes the whole wave run the insertion. Parking such tiles in LDS and draining
 // them for all lanes together (2 parked tiles per lane) was 5x SLOWER: a drain runs the union of
 // the lanes' insertion positions, so batching sparse, uncorrelated insertions does not pay.
-template <int FPAD, int KH, int KN, int NPB_>
+// KO: output candidates per point (16: the two half lists merged into 16, what the merge lets go
+// raises rej; 32: both half lists kept whole, rej = the halves' own - a wider certification margin,
+// so fewer queries fall back to the 3-term kernel, for twice the rescoring input).
+template <int FPAD, int KH, int KN, int NPB_, int KO_ = 16>
 __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
@@ -1012,7 +1015,7 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     const u32x4 bw = {h ? 0u : (sb | (sb << 16)), h ? 0u : sb, 0u, 0u};
     bsx[pb] = __builtin_bit_cast(bf16x8, bw);
   }
-  constexpr int KO = 16;  // output candidates per point
+  constexpr int KO = KO_;  // output candidates per point
   float tv[NPB][KH], rej[NPB];
   int ti[NPB][KH];
 #pragma unroll
@@ -1506,11 +1509,11 @@ HA_EXPORT int ha_h3_assign_certified(const void* planes, const float* sx, int64_
 
 // Certified one-term k nearest rows of C (see h1_topk): dist / idx [n, kp] approximate squared
 // distances ascending + int32 row indices (the caller rescores them exactly), cert [n] uint8 (1 =
-// the true kn nearest are among the kp). kn <= 8 with kp = 16. workspace: ha_h3_workspace_bytes.
+// the true kn nearest are among the kp). kn <= 8 with kp = 16 or 32. workspace: ha_h3_workspace_bytes.
 HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, const float* C, int m, int64_t ldc,
                          void* workspace, int kn, int kp, float* dist, int* idx, unsigned char* cert, void* stream) {
   const int fpad = h3_fpad(f);
-  if (fpad < 0 || m <= 0 || kn < 1 || kn > 8 || kp != 16) return HA_UNSUPPORTED;
+  if (fpad < 0 || m <= 0 || kn < 1 || kn > 8 || (kp != 16 && kp != 32)) return HA_UNSUPPORTED;
   if (n <= 0) return HA_OK;
   hipStream_t s = (hipStream_t)stream;
   const int cb = fpad >= 128 ? 64 : 128;
@@ -1521,11 +1524,17 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   const _Float16* p = (const _Float16*)planes;
   // the error bound needs max |c| and max u (atomicMax into zeroed words)
   if (hipMemsetAsync(meta, 0, 16, s) != hipSuccess) return HA_LAUNCH;
-#define HA_H1TK_KN(FP, KN)                                                                                     \
-  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KN, NPBT>),                                 \
+#define HA_H1TK_KO(FP, KN, KO)                                                                                 \
+  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KN, NPBT, KO>),                             \
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                    \
-  hipLaunchKernelGGL((h1_topk<FP, 16, KN, NPBT>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,      \
+  hipLaunchKernelGGL((h1_topk<FP, 16, KN, NPBT, KO>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,  \
                      kpad / KC::CB, dist, idx, cert)
+#define HA_H1TK_KN(FP, KN)                                                                                     \
+  if (kp == 32) {                                                                                              \
+    HA_H1TK_KO(FP, KN, 32);                                                                                    \
+  } else {                                                                                                     \
+    HA_H1TK_KO(FP, KN, 16);                                                                                    \
+  }
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
     constexpr int NPBT = FP >= 128 ? 1 : 2;                                                                      \
@@ -1551,6 +1560,7 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   }
 #undef HA_H1TK
 #undef HA_H1TK_KN
+#undef HA_H1TK_KO
   return ha_launch_status();
 }
 

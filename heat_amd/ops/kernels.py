@@ -229,14 +229,31 @@ def _topk_lex(d: torch.Tensor, idx: Optional[torch.Tensor], k: int) -> Tuple[tor
 
 
 _KNN_CERTIFIED = os.environ.get("HEAT_KNN_CERTIFIED", "1") != "0"
-_KNN_KP = 16  # candidates per query of the certified one-term pass
+# candidates per query of the certified one-term pass: 32 keeps both lane halves' lists whole (a
+# wider certification margin: fewer queries re-run through the 3-term kernel) at the price of
+# rescoring twice the rows, which the fused rescoring kernel makes cheap; 16 merges them
+_KNN_KP = 32 if os.environ.get("HEAT_KNN_KP", "32") == "32" else 16
 
 
 def _knn_exact_select(Q: torch.Tensor, T: torch.Tensor, idx: torch.Tensor, k: int):
     """Exact (difference-form) squared distances of the candidate rows ``idx`` [nq, c] (-1 =
-    none), the k smallest per query, equal distances ordered by index."""
+    none), the k smallest per query, equal distances ordered by index. Device fp32 with c <= 32:
+    one fused kernel (``csrc/knn_rescore.hip``: a 32-lane group per query, a bitonic sort of the
+    (distance, index) keys); otherwise torch over [rows, c, f] blocks."""
     nq, c = idx.shape
     f = Q.shape[1]
+    if (Q.is_cuda and use_native(Q) and Q.dtype == torch.float32 and T.dtype == torch.float32 and 0 < k <= c <= 32
+            and nq > 0 and T.shape[0] < 2 ** 32 - 1):
+        Qc = Q if Q.stride(-1) == 1 else Q.contiguous()
+        Tc = T if T.stride(-1) == 1 else T.contiguous()
+        ic = idx.contiguous()
+        dist = torch.empty((nq, k), dtype=torch.float32, device=Q.device)
+        out_i = torch.empty((nq, k), dtype=torch.int64, device=Q.device)
+        check(lib().ha_knn_rescore(_ptr(Qc), Qc.stride(0) if nq > 1 else f, _ptr(Tc),
+                                   Tc.stride(0) if T.shape[0] > 1 else f, T.shape[0], nq, f, _ptr(ic),
+                                   int(ic.dtype == torch.int64), c, k, _ptr(dist), _ptr(out_i),
+                                   ctypes.c_void_p(stream_ptr(Q.device))), "ha_knn_rescore")
+        return dist, out_i
     dist = torch.empty((nq, k), dtype=torch.float32, device=Q.device)
     out_i = torch.empty((nq, k), dtype=torch.int64, device=Q.device)
     step = max(1, (1 << 26) // (c * f))
@@ -253,9 +270,9 @@ def _knn_exact_select(Q: torch.Tensor, T: torch.Tensor, idx: torch.Tensor, k: in
 
 def _knn_certified(Q, T, Tc, k, packed, ws, exact_distances: bool = True):
     """k <= 8 nearest rows of T through the certified one-term kernel (``h1_topk``: 1 fp16 MFMA
-    per k-step instead of 3, a rigorous error bound per query): 16 candidates per query, the
-    queries whose candidates are not certified to contain the true k nearest re-run through the
-    3-term kernel, then every candidate list is rescored exactly."""
+    per k-step instead of 3, a rigorous error bound per query): ``_KNN_KP`` candidates per query,
+    the queries whose candidates are not certified to contain the true k nearest re-run through
+    the 3-term kernel (16 candidates), then every candidate list is rescored exactly."""
     L = lib()
     nq, f = Q.shape
     nt = T.shape[0]
@@ -276,17 +293,19 @@ def _knn_certified(Q, T, Tc, k, packed, ws, exact_distances: bool = True):
         nu = int(unc.numel())
         qblocks = (nu + 127) // 128
         splits = max(1, min(L.ha_h3_topk_chunks(nt, f) // 4, (4 * num_cus(dev) + qblocks - 1) // qblocks))
-        d3 = torch.empty((splits, nu, kp), dtype=torch.float32, device=dev)
-        i3 = torch.empty((splits, nu, kp), dtype=torch.int32, device=dev)
-        check(L.ha_h3_topk(_ptr(pl), _ptr(sxu), nu, f, _ptr(Tc), nt, Tc.stride(0), _ptr(ws), kp, splits, _ptr(d3),
+        k3 = min(kp, 16)   # the 3-term kernel's list length
+        d3 = torch.empty((splits, nu, k3), dtype=torch.float32, device=dev)
+        i3 = torch.empty((splits, nu, k3), dtype=torch.int32, device=dev)
+        check(L.ha_h3_topk(_ptr(pl), _ptr(sxu), nu, f, _ptr(Tc), nt, Tc.stride(0), _ptr(ws), k3, splits, _ptr(d3),
                            _ptr(i3), st), "ha_h3_topk")
         if splits == 1:
             i3 = i3[0].long()
         else:
-            _, i3 = _topk_lex(d3.permute(1, 0, 2).reshape(nu, splits * kp), i3.permute(1, 0, 2).reshape(nu, splits * kp),
-                              kp)
+            _, i3 = _topk_lex(d3.permute(1, 0, 2).reshape(nu, splits * k3), i3.permute(1, 0, 2).reshape(nu, splits * k3),
+                              k3)
         idx = idx.long()
-        idx[unc] = i3
+        idx[unc] = -1
+        idx[unc, :k3] = i3
     else:
         idx = idx.long()
     # the k nearest are certified to be AMONG the candidates, not ranked: always rescore exactly

@@ -320,13 +320,25 @@ def cdist_topk(X: DNDarray, Y: Optional[DNDarray] = None, k: int = 1):
             ids.append(di)
         return torch.cat(ds), torch.cat(ids)
 
+    merged = [0]
+
     def merge(block: torch.Tensor, off: int):
         nonlocal best_d, best_i
         if block.shape[0] == 0 or nq == 0:
             return
         dv, di = block_topk(block)
-        cd = torch.cat([best_d, dv.to(x.device)], dim=1)
-        ci = torch.cat([best_i, di.to(x.device) + off], dim=1)
+        dv, di = dv.to(x.device), di.to(x.device) + off
+        merged[0] += 1
+        if merged[0] == 1 and dv.shape[1] == k and tt == torch.float32 and ops.use_native(x):
+            # the first block's fused-kernel lists are already in (distance, index) order
+            best_d, best_i = dv, di
+            return
+        cd = torch.cat([best_d, dv], dim=1)
+        ci = torch.cat([best_i, di], dim=1)
+        if tt == torch.float32:
+            # one top-k over packed (distance bits, index) keys (distances are >= 0)
+            best_d, best_i = ops.kernels._topk_lex(cd, ci, k)
+            return
         # (distance, index) order: stable sort by index, then stable sort by distance
         o = torch.sort(ci, dim=1, stable=True).indices
         cd, ci = torch.gather(cd, 1, o), torch.gather(ci, 1, o)

@@ -879,6 +879,52 @@ def test_kmeans_assign_small_k(n, f, k):
     assert (lab2.long() == d2.argmin(1)).float().mean() > 0.9999
 
 
+@pytest.mark.parametrize("c,k", [(1, 1), (5, 3), (16, 8), (32, 8), (32, 32), (20, 16)])
+@pytest.mark.parametrize("f", [1, 3, 18, 128])
+@pytest.mark.parametrize("idx64", [False, True])
+def test_knn_rescore_kernel(c, k, f, idx64):
+    """Fused exact rescoring of candidate lists (csrc/knn_rescore.hip) == the torch formulation:
+    difference-form fp32 distances, k smallest in (distance, index) order, -1 candidates ignored,
+    duplicate rows (equal distances) ordered by index; strided / unaligned query rows."""
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(c * 100 + k + f)
+    nq, nt = 3001, 500
+    T = torch.randn(nt, f, generator=g).to(dev)
+    T[100:120] = T[:20]                                     # equal distances at different indices
+    Qw = torch.randn(nq, f + 1, generator=g).to(dev)
+    cand = torch.randint(0, nt, (nq, c), generator=g)
+    cand[::7, -1] = -1                                      # missing candidates
+    if c >= 2:
+        cand[::5, 0] = cand[::5, 0] % 20                    # rows i and i + 100 hold the same values
+        cand[::5, 1] = cand[::5, 0] + 100
+    cand = cand.to(dev).to(torch.int64 if idx64 else torch.int32)
+    for Q in (Qw[:, :f], Qw[:, :f].contiguous()):
+        d, i = K._knn_exact_select(Q, T, cand, k)
+        assert d.shape == (nq, k) and i.dtype == torch.int64
+        # torch reference of the same semantics
+        ci = cand.long()
+        nb = T[ci.clamp(min=0)]
+        rd = ((Q.unsqueeze(1) - nb) ** 2).sum(-1)
+        rd = torch.where(ci >= 0, rd, torch.full_like(rd, float("inf")))
+        key_d = torch.sort(rd, dim=1).values
+        assert torch.allclose(d.double(), key_d[:, :k].double(), rtol=1e-5, atol=1e-6)
+        valid = i >= 0
+        # every reported index is one of the query's candidates at the reported distance
+        hit = (ci.unsqueeze(2) == i.unsqueeze(1)) & valid.unsqueeze(1)
+        assert torch.all(hit.any(1) | ~valid)
+        dd = ((Q.unsqueeze(1) - T[i.clamp(min=0)]) ** 2).sum(-1)
+        assert torch.allclose(torch.where(valid, dd, d), d, rtol=1e-5, atol=1e-6)
+        # ordering: ascending distance, ascending index among equal distances, -1 only after the rest
+        nxt_d, prv_d = d[:, 1:], d[:, :-1]
+        assert torch.all(nxt_d >= prv_d)
+        eq = (nxt_d == prv_d) & valid[:, 1:] & valid[:, :-1]
+        assert torch.all(i[:, 1:][eq] >= i[:, :-1][eq])   # (randint may repeat a candidate)
+        nvalid = (ci >= 0).sum(1).clamp(max=k)
+        assert torch.equal(valid.sum(1), nvalid)
+
+
 @pytest.mark.parametrize("f", [128, 64, 18])
 def test_knn_certified_one_term(f):
     """The certified one-term pass (h1_topk: 16 candidates per query from hi.hi scores + a rigorous
@@ -895,11 +941,12 @@ def test_knn_certified_one_term(f):
     T = torch.randn(nt, f, generator=g).to(dev)
     T[:600] = T[600:1200]                                   # exact duplicates -> ties
     Q[:3000] = T[:3000] + 1e-3 * torch.randn(3000, f, generator=g).to(dev)
-    # 20 training rows of exactly equal norm (sign flips of one vector) nearest to 100 zero queries:
-    # more exact ties than candidates, so those queries cannot be certified and take the 3-term path
+    # 40 training rows of exactly equal norm (sign flips of one vector) nearest to 100 zero queries:
+    # more exact ties than candidates (16 or 32), so those queries cannot be certified and take the
+    # 3-term path
     base = 0.05 * torch.randn(f, generator=g)
-    flips = torch.where(torch.rand(20, f, generator=g) < 0.5, -1.0, 1.0)
-    T[1200:1220] = (flips * base).to(dev)
+    flips = torch.where(torch.rand(40, f, generator=g) < 0.5, -1.0, 1.0)
+    T[1200:1240] = (flips * base).to(dev)
     Q[3000:3100] = 0.0
     before = dict(K._KNN_STATS)
     dist, idx = ops.knn_topk(Q, T, k)

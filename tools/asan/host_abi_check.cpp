@@ -42,6 +42,8 @@ int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k
                const double* Sin, double* Sout, void* tau, double* Y, double* part, unsigned* cnt, void* stream);
 int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counter_lo, uint64_t counter_hi, uint64_t seed,
                      int bits, int dist, double low, double span, void* stream);
+int ha_knn_rescore(const float* Q, int64_t ldq, const float* T, int64_t ldt, int64_t nt, int64_t nq, int f,
+                   const void* cand, int idx64, int c, int k, float* dist, int64_t* out_idx, void* stream);
 }
 
 static int fails = 0;
@@ -111,6 +113,10 @@ int main() {
         BAD);  // coff < 0
   CHECK(ha_threefry_fill(dummy, 0, 0, 0, 0, 1, 32, 0, 0.0, 1.0, nullptr) == OK);
   CHECK(ha_threefry_fill(dummy, 0, 4, 0, 0, 1, 16, 0, 0.0, 1.0, nullptr) == BAD);
+  CHECK(ha_knn_rescore(nullptr, 4, nullptr, 4, 10, 5, 4, nullptr, 0, 33, 8, nullptr, nullptr, nullptr) == BAD);  // c > 32
+  CHECK(ha_knn_rescore(nullptr, 4, nullptr, 4, 10, 5, 4, nullptr, 0, 16, 17, nullptr, nullptr, nullptr) == BAD);  // k > c
+  CHECK(ha_knn_rescore(nullptr, 2, nullptr, 4, 10, 5, 4, nullptr, 0, 16, 8, nullptr, nullptr, nullptr) == BAD);  // ldq < f
+  CHECK(ha_knn_rescore(nullptr, 4, nullptr, 4, 10, 0, 4, nullptr, 0, 16, 8, nullptr, nullptr, nullptr) == OK);   // nq = 0
   if (fails) {
     fprintf(stderr, "%d checks failed\n", fails);
     return 1;
