@@ -1431,7 +1431,9 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
             if native:
                 # the panel in a compact m x nc copy: the nc + 1 passes stream contiguous rows
                 # instead of one 128-byte segment per (16 KB) matrix row
-                Pb = A[:, k0: k0 + nc].contiguous()
+                # (always a copy: when the panel spans every column of A, .contiguous() would return A
+                # itself and the reflector masking below would overwrite R)
+                Pb = A[:, k0: k0 + nc].clone(memory_format=torch.contiguous_format)
                 check(L.ha_hh_colsums(_ptr(Pb), code, m_r, nc, g0, 0, nc, k0, _ptr(S[0]), _ptr(hpart),
                                       _ptr(hcnt), st), "ha_hh_colsums")
             else:

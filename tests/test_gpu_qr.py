@@ -23,7 +23,8 @@ def _ill(m, n, cond, seed, dtype):
     return ((G * s) @ V.T).to(dtype)
 
 
-@pytest.mark.parametrize("m,n", [(5000, 100), (20000, 256), (777, 65), (300, 300), (4097, 33), (30000, 700)])
+@pytest.mark.parametrize("m,n", [(5000, 100), (20000, 256), (777, 65), (300, 300), (4097, 33), (30000, 700),
+                                 (40, 6), (1000, 32), (5000, 17)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_householder_qr_device(m, n, dtype):
     from heat_amd import ops
