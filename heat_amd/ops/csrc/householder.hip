@@ -25,6 +25,8 @@
 // fixed-order two-level sum (hh_block_sum) - no float atomics, bit-reproducible.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int HH_NB = 32;     // panel width (8 lanes x 4 columns)
@@ -67,7 +69,8 @@ __device__ __forceinline__ void hh_store4(T* p, const Vec4<T>& r, int ncols_here
 // made the factorization differ run to run in the last bits): the block's column sums go to its
 // own slot of `part` (write-through), the blocks form HH_COPIES groups of consecutive blocks, and
 // the last-arriving block of each group (ticket on cnt[group], reset by it) adds its group's slots
-// in block order into accumulator copy `group` of out; hh_gather_s then adds the copies in order.
+// in a fixed order (8 strided partial sums + a pairwise tree) into accumulator copy `group` of
+// out; hh_gather_s then adds the copies in a fixed order.
 __device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __restrict__ out, double* red,
                                              double* __restrict__ part, unsigned* __restrict__ cnt) {
   __shared__ bool last;
@@ -96,22 +99,38 @@ __device__ __forceinline__ void hh_block_sum(const double (&acc)[4], double* __r
     }
   }
   __syncthreads();
-  if (last && tid < HH_NB) {
+  if (last) {
+    // the group's partials over all 256 threads: thread (sub = tid / 32, column tid % 32) sums
+    // blocks b0 + sub, b0 + sub + 8, ... (independent loads in flight), then a fixed pairwise tree
+    // over the 8 subs. One thread walking the ~64 partials of its column was a chain of dependent
+    // L2 round trips: ~30 us of the ~50 us fixed cost per launch (tools/microbench/hh_step_scan.py)
+    const int col = tid & (HH_NB - 1), sub = tid >> 5;
     double s = 0.0;
-    for (int b = b0; b < b1; ++b) s += part[(int64_t)b * HH_NB + tid];
-    out[group * HH_SLEN + tid] = s;
+#pragma unroll 4
+    for (int b = b0 + sub; b < b1; b += 8) s += part[(int64_t)b * HH_NB + col];
+    red[sub * HH_NB + col] = s;
+    __syncthreads();
+    if (tid < HH_NB)
+      out[group * HH_SLEN + tid] = ((red[tid] + red[HH_NB + tid]) + (red[2 * HH_NB + tid] + red[3 * HH_NB + tid])) +
+                                   ((red[4 * HH_NB + tid] + red[5 * HH_NB + tid]) +
+                                    (red[6 * HH_NB + tid] + red[7 * HH_NB + tid]));
   }
   __syncthreads();
 }
 
-// Sum of the HH_COPIES replicated accumulators of one S buffer into LDS (every block).
-__device__ __forceinline__ void hh_gather_s(const double* __restrict__ S, double* __restrict__ out) {
-  for (int e = threadIdx.x; e < HH_SLEN; e += blockDim.x) {
-    double v = 0.0;
-#pragma unroll 8
-    for (int c = 0; c < HH_COPIES; ++c) v += S[c * HH_SLEN + e];
-    out[e] = v;
-  }
+// Sum of the HH_COPIES replicated accumulators of one S buffer into LDS (every block): thread
+// (quarter q = tid / 64, element e = tid % 64) adds copies q, q + 4, ... (8 independent loads),
+// then a fixed-order sum of the 4 quarters. `scratch`: 256 doubles of LDS.
+__device__ __forceinline__ void hh_gather_s(const double* __restrict__ S, double* __restrict__ out,
+                                            double* __restrict__ scratch) {
+  static_assert(HH_SLEN == 64 && HH_COPIES % 4 == 0, "one element per lane of a quarter");
+  const int e = threadIdx.x & 63, q = threadIdx.x >> 6;
+  double v = 0.0;
+#pragma unroll
+  for (int c = q; c < HH_COPIES; c += 4) v += S[c * HH_SLEN + e];
+  scratch[q * 64 + e] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) out[e] = (scratch[e] + scratch[64 + e]) + (scratch[128 + e] + scratch[192 + e]);
   __syncthreads();
 }
 
@@ -140,9 +159,15 @@ __global__ __launch_bounds__(256) void hh_colsums(const T* __restrict__ A, int64
   hh_block_sum(acc, S, red, part, cnt);
 }
 
-// rows per thread and sweep in hh_step, loads issued before the first use. 4 measured SLOWER:
-// 4.34 vs 2.74 ms per 32-column panel at 1.25e6 rows (tools/microbench/hh_parts.py, r4t)
-constexpr int HH_ROWS = 1;
+// ROWS: rows per thread and sweep in hh_step, loads issued before the first use (with the serial
+// block-sum tail, 4 measured SLOWER: 4.34 vs 2.74 ms per 32-column panel at 1.25e6 rows, r4t).
+// A/B switches (read once): HEAT_HH_ROWS (1 | 2 | 4), HEAT_HH_BLOCKS_PER_CU (grid cap, default 4).
+// Measured per launch at 1.25e6 rows with the parallel tails (r4y, tools/microbench/hh_step_scan.py):
+// rows 1 / 4 blocks per CU 66 us, rows 2 / 4 66 us, rows 1 / 8 68-79 us, rows 4 / 8 102 us.
+static int hh_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
 
 // hh_step's work on one row g >= d (a: the row's 4 panel values of this lane, already loaded)
 template <typename T>
@@ -186,7 +211,7 @@ __device__ __forceinline__ void hh_step_row(Vec4<T>& a, T* row, int64_t g, int64
 
 // One panel column: apply reflector j (from Sin) to this rank's rows, store v / R, accumulate the
 // next column's S / rowd into Sout (nullptr for the panel's last column).
-template <typename T>
+template <typename T, int HH_ROWS>
 __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int64_t lda, int64_t g0, int64_t k0,
                                                int64_t coff, int ncols, int j, const double* __restrict__ Sin,
                                                double* __restrict__ Sout, T* __restrict__ tau,
@@ -194,7 +219,7 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
                                                unsigned* __restrict__ cnt) {
   __shared__ double red[32 * HH_NB];
   __shared__ double sin_[HH_SLEN];
-  hh_gather_s(Sin, sin_);
+  hh_gather_s(Sin, sin_, red);
   const int64_t d = k0 + j;
   const int q = threadIdx.x & 7;
   const int nh = ncols - 4 * q < 4 ? (ncols - 4 * q > 0 ? ncols - 4 * q : 0) : 4;
@@ -355,7 +380,8 @@ int hh_grid(int64_t m) {
       ncu = 256;
   }
   const int64_t need = (m + 31) / 32;
-  const int64_t cap = 8LL * ncu;  // enough waves in flight; atomics spread over HH_COPIES copies
+  static const int per_cu = hh_env("HEAT_HH_BLOCKS_PER_CU", 4);
+  const int64_t cap = (int64_t)per_cu * ncu;  // enough waves in flight; tickets spread over HH_COPIES groups
   return (int)(need < cap ? (need > 0 ? need : 1) : cap);
 }
 
@@ -396,12 +422,18 @@ HA_EXPORT int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0,
   if (ncols <= 0 || ncols > HH_NB || j < 0 || j >= ncols || m < 0 || coff < 0) return HA_BAD_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int grid = hh_grid(m);
-  if (dtype == 0)
-    hipLaunchKernelGGL(hh_step<float>, dim3(grid), dim3(256), 0, s, (float*)A, m, lda, g0, k0, coff, ncols, j, Sin,
-                       Sout, (float*)tau, Y, part, cnt);
-  else
-    hipLaunchKernelGGL(hh_step<double>, dim3(grid), dim3(256), 0, s, (double*)A, m, lda, g0, k0, coff, ncols, j, Sin,
-                       Sout, (double*)tau, Y, part, cnt);
+  static const int rows = hh_env("HEAT_HH_ROWS", 1);
+#define HA_HH_STEP(T, R)                                                                                    \
+  hipLaunchKernelGGL((hh_step<T, R>), dim3(grid), dim3(256), 0, s, (T*)A, m, lda, g0, k0, coff, ncols, j, Sin, Sout, \
+                     (T*)tau, Y, part, cnt)
+  if (dtype == 0) {
+    if (rows >= 4) HA_HH_STEP(float, 4);
+    else if (rows == 2) HA_HH_STEP(float, 2);
+    else HA_HH_STEP(float, 1);
+  } else {
+    HA_HH_STEP(double, 1);
+  }
+#undef HA_HH_STEP
   return ha_launch_status();
 }
 
