@@ -76,11 +76,19 @@ __device__ __forceinline__ float kundu_fast(uint32_t v23) {
   const uint32_t mi = 8388607u - v23;  // 2^23 (1 - u) - 1
   const bool in_tab = mi < (1u << KUNDU_TAB_BITS);
   const float tabv = g_kundu_tab[in_tab ? mi : 0u];
+  // kundu(u) = (ln(-ln(1 - u^0.0775 + tiny) + tiny) - 1.0821) / 0.3807 with the constants folded
+  // (VALU-bound kernel: every instruction counts):
+  //   w = exp2(0.0775 log2 u)                     (u = 0: -inf -> w = 0; NOT fma(0.0775, log2 v23,
+  //       -0.0775 * 23): the rounded constant shifts w by a systematic ~1e-7, which 1 / (1 - w)
+  //       amplifies into a 1.7e-6 bias of the sample mean, measured)
+  //   ln(l1 + tiny) = ln(ln 2) + ln 2 log2(t),   t = -log2(1 - w) + tiny / ln 2
+  //   kundu = KA log2(t) + KB,   KA = ln 2 / 0.3807,   KB = (ln(ln 2) - 1.0821) / 0.3807
+  // (1 - w + tiny == 1 - w outside the table range, where w < 1 - 2^-6)
+  const float KA = 0.69314718056f / 0.3807f, KB = (-0.36651292058f - 1.0821f) / 0.3807f;
   const float u = (float)v23 * (1.0f / 8388608.0f);
-  const float ln2 = 0.693147180559945f, tiny = 1.17549435e-38f;
-  const float w = __builtin_amdgcn_exp2f(0.0775f * __builtin_amdgcn_logf(u));  // u = 0: exp2(-inf) = 0
-  const float l1 = -ln2 * __builtin_amdgcn_logf(1.f - w + tiny);
-  const float r = (ln2 * __builtin_amdgcn_logf(l1 + tiny) - 1.0821f) * (1.0f / 0.3807f);
+  const float w = __builtin_amdgcn_exp2f(0.0775f * __builtin_amdgcn_logf(u));
+  const float t = 1.69587987e-38f - __builtin_amdgcn_logf(1.f - w);
+  const float r = fmaf(KA, __builtin_amdgcn_logf(t), KB);
   return in_tab ? tabv : r;
 }
 
@@ -130,6 +138,35 @@ __global__ __launch_bounds__(256) void tf_fill32(void* __restrict__ out, int64_t
     } else {
       if (i >= 0 && i < n) tf_convert32<DIST>(x0, out, i, low, span);
       if (i + 1 >= 0 && i + 1 < n) tf_convert32<DIST>(x1, out, i + 1, low, span);
+    }
+  }
+}
+
+// Fast path of tf_fill32 for uniform / normal output when e0 is even and out is 16-byte aligned:
+// each thread turns TWO consecutive counter pairs into 4 consecutive elements with one 16-byte
+// store, halving the per-element loop, index and store-issue overhead (the normal transform keeps
+// this kernel VALU-bound).
+template <int DIST>
+__global__ __launch_bounds__(256) void tf_fill32q(float* __restrict__ out, int64_t e0, int64_t n, uint64_t counter_lo,
+                                                  uint32_t key) {
+  const int64_t nq = (n + 3) >> 2;
+  const uint64_t c0 = counter_lo + (uint64_t)(e0 >> 1);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t V0 = c0 + 2 * (uint64_t)q, V1 = V0 + 1;
+    uint32_t a0 = (uint32_t)(V0 >> 32), a1 = (uint32_t)V0, b0 = (uint32_t)(V1 >> 32), b1 = (uint32_t)V1;
+    tf32(a0, a1, key);
+    tf32(b0, b1, key);
+    const uint32_t v[4] = {a0 & 0x7FFFFFu, a1 & 0x7FFFFFu, b0 & 0x7FFFFFu, b1 & 0x7FFFFFu};
+    floatx4 o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = DIST == DIST_NORMAL ? kundu_fast(v[c]) : (float)v[c] * (1.0f / 8388608.0f);
+    const int64_t i = 4 * q;
+    if (i + 3 < n) {
+      *reinterpret_cast<floatx4*>(out + i) = o;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (i + c < n) out[i + c] = o[c];
     }
   }
 }
@@ -195,7 +232,16 @@ HA_EXPORT int ha_threefry_fill(void* out, int64_t e0, int64_t n, uint64_t counte
   }
   if (bits == 32) {
     const uint32_t key = (uint32_t)(seed & 0x7FFFFFFFull);
-    if (dist == DIST_NORMAL)
+    if (dist != DIST_INT && (e0 & 1) == 0 && ((uintptr_t)out & 15) == 0) {
+      int64_t qb = ((n + 3) / 4 + 255) / 256;
+      if (qb > 65536) qb = 65536;
+      if (dist == DIST_NORMAL)
+        hipLaunchKernelGGL(tf_fill32q<DIST_NORMAL>, dim3((unsigned)qb), dim3(256), 0, s, (float*)out, e0, n, counter_lo,
+                           key);
+      else
+        hipLaunchKernelGGL(tf_fill32q<DIST_UNIFORM>, dim3((unsigned)qb), dim3(256), 0, s, (float*)out, e0, n,
+                           counter_lo, key);
+    } else if (dist == DIST_NORMAL)
       hipLaunchKernelGGL(tf_fill32<DIST_NORMAL>, dim3((unsigned)blocks), dim3(256), 0, s, out, e0, n, counter_lo, key,
                          (int64_t)low, (int64_t)span);
     else if (dist == DIST_INT)
