@@ -40,6 +40,20 @@ def test_distributed_on_device(module, name):
         pytest.fail("check {} failed with device buffers:\n{}".format(name, err))
 
 
+CASES3 = [(m, n) for m, n in CASES if m in ("tests.dist_checks", "tests.dist_checks_edge")]
+
+
+@pytest.mark.parametrize("module,name", CASES3)
+def test_distributed_on_device_3_ranks(module, name):
+    """The same checks at 3 ranks: every split of the check data is uneven (e.g. 40 rows -> 14 /
+    13 / 13), so the offset / count / padding logic of the device paths runs off the even case."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ok, err = _batch(module, 3)[name]
+    if not ok:
+        pytest.fail("check {} failed with device buffers at 3 ranks:\n{}".format(name, err))
+
+
 @pytest.mark.parametrize("nprocs", [3, 5])
 @pytest.mark.parametrize("name", VCOLL)
 def test_vcollectives_uneven_on_device(name, nprocs):
