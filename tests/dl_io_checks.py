@@ -30,21 +30,28 @@ class _NetWithUnused(torch.nn.Module):
         return self.b(torch.relu(self.a(x)))
 
 
+def _dev():
+    """cuda when the ranks run with device buffers (tests/test_gpu_dist.py), else cpu."""
+    on = os.environ.get("HEAT_AMD_DEFAULT_DEVICE") == "gpu" and torch.cuda.is_available()
+    return torch.device("cuda", 0) if on else torch.device("cpu")
+
+
 def _dp_run(blocking: bool, bucket_mb: float, steps: int = 3, momentum: float = 0.0):
     comm = ht.MPI_WORLD
+    dev = _dev()
     torch.manual_seed(0)
-    net = _NetWithUnused()
+    net = _NetWithUnused().to(dev)
     opt = ht.optim.DataParallelOptimizer(torch.optim.SGD(net.parameters(), lr=0.1, momentum=momentum),
                                          blocking=blocking)
     dp = ht.nn.DataParallel(net, comm, opt, blocking_parameter_updates=blocking, bucket_cap_mb=bucket_mb)
-    ref = _NetWithUnused()
+    ref = _NetWithUnused().to(dev)
     ref.load_state_dict(net.state_dict())
     ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=momentum)
     g = torch.Generator().manual_seed(7)
     per = 5
     for _ in range(steps):
-        Xg = torch.randn(per * comm.size, 4, generator=g)
-        yg = torch.randn(per * comm.size, 1, generator=g)
+        Xg = torch.randn(per * comm.size, 4, generator=g).to(dev)
+        yg = torch.randn(per * comm.size, 1, generator=g).to(dev)
         sl = slice(comm.rank * per, (comm.rank + 1) * per)     # per-rank data
         opt.zero_grad()
         torch.nn.functional.mse_loss(dp(Xg[sl]), yg[sl]).backward()
@@ -53,7 +60,7 @@ def _dp_run(blocking: bool, bucket_mb: float, steps: int = 3, momentum: float = 
         torch.nn.functional.mse_loss(ref(Xg), yg).backward()
         ref_opt.step()
     dp.eval()  # finalises a deferred (non-blocking) update
-    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu()
     allflat = comm.allgather(flat.numpy())
     for r, other in enumerate(allflat):
         assert np.array_equal(other, allflat[0]), "rank {} diverged from rank 0".format(r)

@@ -7,13 +7,14 @@ the native kernels, with the same NumPy oracles as ``test_distributed.py``."""
 import pytest
 import torch
 
-from . import dist_checks, dist_checks_edge, oracle_checks, random_checks, vcoll_checks
+from . import dist_checks, dist_checks_edge, dl_io_checks, oracle_checks, random_checks, vcoll_checks
 from ._dist import run_distributed, run_distributed_batch
 
 pytestmark = pytest.mark.gpu
 
 MODULES = {"tests.dist_checks": dist_checks, "tests.dist_checks_edge": dist_checks_edge,
-           "tests.random_checks": random_checks, "tests.oracle_checks": oracle_checks}
+           "tests.random_checks": random_checks, "tests.oracle_checks": oracle_checks,
+           "tests.dl_io_checks": dl_io_checks}
 CASES = [(m, n) for m, mod in MODULES.items() for n in dir(mod) if n.startswith("check_")
          and getattr(getattr(mod, n), "__module__", m) == m]
 ENV = {"HEAT_AMD_DEFAULT_DEVICE": "gpu", "HEAT_COMM_TIMEOUT": "60"}
