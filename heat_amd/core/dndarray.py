@@ -573,6 +573,35 @@ class DNDarray:
         return ravel(self)
 
     # ------------------------------------------------------------------ indexing
+    def _index_out_shape(self, key: tuple) -> Tuple[int, ...]:
+        """Global result shape of a normalized key. Integer index tensors stay where they are: they
+        are bounds-checked on their device (ONE host sync for all of them) and the shape comes from
+        the meta device - copying a device index tensor to the host for the zero-stride proxy cost
+        ~0.4 ms per million indices (``tools/microbench/ops_overhead.py``). Keys with boolean tensors
+        (data-dependent length) use the host proxy."""
+        if any(isinstance(k, torch.Tensor) and k.dtype == torch.bool for k in key):
+            proxy = self.__torch_proxy__()
+            return tuple(proxy[tuple(k.cpu() if isinstance(k, torch.Tensor) else k for k in key)].shape)
+        bounds, dim = [], 0
+        for k in key:
+            if k is None:
+                continue
+            if isinstance(k, torch.Tensor) and k.numel():
+                bounds.append((k, dim))
+            dim += 1
+        if bounds:
+            ext = torch.stack([torch.stack([k.min(), k.max()]).to(torch.int64).cpu() if k.is_cuda
+                               else torch.stack([k.min(), k.max()]).to(torch.int64) for k, _ in bounds]).tolist()
+            for (lo, hi), (_, d) in zip(ext, bounds):
+                n = self.gshape[d]
+                bad = lo if lo < -n else hi if hi >= n else None
+                if bad is not None:
+                    raise IndexError("index {} is out of bounds for dimension {} with size {}".format(bad, d, n))
+        # (a 0-d index tensor acts as an integer: torch reads its value, which a meta tensor has not)
+        mkey = tuple((int(k) if k.dim() == 0 else torch.empty(k.shape, dtype=torch.int64, device="meta"))
+                     if isinstance(k, torch.Tensor) else k for k in key)
+        return tuple(torch.empty(self.gshape, dtype=torch.int8, device="meta")[mkey].shape)
+
     def _normalize_key(self, key) -> Tuple[tuple, bool]:
         """Return (key tuple without Ellipsis/DNDarrays, has_advanced)."""
         if isinstance(key, DNDarray) and key.dtype is types.bool:
@@ -666,9 +695,7 @@ class DNDarray:
                 n = sum(self.comm.allgather_sizes(res.shape[0]))
                 return DNDarray(res, (n,), self.dtype, 0, self.device, self.comm, None)
         key, adv = self._normalize_key(key)
-        proxy = self.__torch_proxy__()
-        pkey = tuple(k.cpu() if isinstance(k, torch.Tensor) else k for k in key)
-        gout = tuple(proxy[pkey].shape)
+        gout = self._index_out_shape(key)
 
         if not self.is_distributed():
             dkey = tuple(k.to(self.__array.device) if isinstance(k, torch.Tensor) else k for k in key)
@@ -975,6 +1002,8 @@ class DNDarray:
 
         key, adv = self._normalize_key(key)
         if not self.is_distributed():
+            if any(isinstance(k, torch.Tensor) and k.dtype != torch.bool for k in key):
+                self._index_out_shape(key)  # bounds check: an out-of-range device index_put asserts on the GPU
             dkey = tuple(k.to(dev) if isinstance(k, torch.Tensor) else k for k in key)
             self.__array[dkey] = gathered_value() if value_d is not None else vt
             return
@@ -984,9 +1013,7 @@ class DNDarray:
         counts, displs = self.counts_displs()
         rank = self.comm.rank
         c0, c1 = displs[rank], displs[rank] + counts[rank]
-        proxy = self.__torch_proxy__()
-        pkey = tuple(k.cpu() if isinstance(k, torch.Tensor) else k for k in key)
-        gsel = tuple(proxy[pkey].shape)
+        gsel = self._index_out_shape(key)
         shaped_value = value_d is not None and tuple(value_d.gshape) == gsel
 
         if isinstance(ks, int):

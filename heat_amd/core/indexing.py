@@ -60,16 +60,41 @@ def where(cond: DNDarray, x=None, y=None) -> DNDarray:
     dtype = types.result_type(x, y)
     tt = dtype.torch_type()
 
+    # identically distributed operands (the common case, e.g. a mask computed from x): ONE
+    # torch.where on the local blocks - the generic path below makes three passes
+    arrs = [v for v in (cond, x, y) if isinstance(v, DNDarray)]
+    dev = cond.larray.device
+    if all(v.gshape == cond.gshape and v.split == cond.split and v.larray.device == dev for v in arrs) and \
+            (not cond.is_distributed() or all(v.balanced for v in arrs)):
+        xa = x.larray.to(tt) if isinstance(x, DNDarray) else torch.tensor(x, dtype=tt, device=dev)
+        ya = y.larray.to(tt) if isinstance(y, DNDarray) else torch.tensor(y, dtype=tt, device=dev)
+        res = torch.where(cond.larray.bool(), xa, ya)
+        if res.shape != cond.larray.shape:   # 0-d operands only: broadcast to the block
+            res = res.expand(cond.larray.shape).contiguous()
+        return DNDarray(res, cond.gshape, dtype, cond.split, cond.device, cond.comm, cond.balanced)
+
     def take_x(c, a):
         return torch.where(c.bool(), a.to(tt), torch.zeros((), dtype=tt, device=a.device))
 
     def take_y(c, b):
         return torch.where(c.bool(), torch.zeros((), dtype=tt, device=b.device), b.to(tt))
 
-    # the two halves are disjoint, so their sum is the selection (exact: one term is always 0)
+    # the two halves are disjoint (one is all-zero bits at every position), so their bitwise OR is
+    # the selection - exact for every value, -0.0 and NaN payloads included (a sum turned -0.0 into
+    # +0.0)
+    ibits = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64, 16: torch.int64}
+
+    def merge(a, b):
+        if a.dtype == torch.bool:
+            return a | b
+        av, bv = (torch.view_as_real(a), torch.view_as_real(b)) if a.is_complex() else (a, b)
+        it = ibits[av.element_size()]
+        out = (av.contiguous().view(it) | bv.contiguous().view(it)).view(av.dtype)
+        return torch.view_as_complex(out) if a.is_complex() else out
+
     px = _operations.binary_op(take_x, cond, x)
     py = _operations.binary_op(take_y, cond, y)
-    res = _operations.binary_op(torch.add, px, py)
+    res = _operations.binary_op(merge, px, py)
     return DNDarray(res.larray.to(tt), res.gshape, dtype, res.split, res.device, res.comm, res.balanced)
 
 
