@@ -815,7 +815,32 @@ __global__ __launch_bounds__(256) void tg_sum_slices(const float* __restrict__ P
   }
 }
 
+// fp32 out[i, j] = alpha * (sum over s of P[s cslice + i N + j], in slice order, fp64) (+ out): the
+// split-K epilogue of a GEMM whose few output tiles cannot fill the GPU
+__global__ __launch_bounds__(256) void tg_sum_slices32(const float* __restrict__ P, int64_t S, int64_t M, int64_t N,
+                                                       int64_t cslice, float* __restrict__ out, int64_t ldo,
+                                                       float alpha, int accumulate) {
+  const int64_t total = M * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / N, j = e - i * N;
+    double acc = 0.0;
+    for (int64_t z = 0; z < S; ++z) acc += (double)P[z * cslice + e];
+    const float r = (float)(alpha * acc);
+    out[i * ldo + j] = accumulate ? out[i * ldo + j] + r : r;
+  }
+}
+
 }  // namespace
+
+HA_EXPORT int ha_sum_slices32(const float* P, int64_t S, int64_t M, int64_t N, int64_t cslice, float* out, int64_t ldo,
+                              float alpha, int accumulate, void* stream) {
+  if (S < 1 || M < 0 || N < 0 || ldo < N) return HA_BAD_ARG;
+  if (M == 0 || N == 0) return HA_OK;
+  const int64_t g = (M * N + 255) / 256;
+  hipLaunchKernelGGL(tg_sum_slices32, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, (hipStream_t)stream, P,
+                     S, M, N, cslice, out, ldo, alpha, accumulate);
+  return ha_launch_status();
+}
 
 // C[M, N] (row-major, ldc) = alpha A B (+ C if beta), exact fp32. a_kmajor: A element (m, k) at
 // A[k lda + m] (else A[m lda + k]); b_kmajor: B element (k, n) at B[k ldb + n] (else B[n ldb + k]).

@@ -1038,6 +1038,22 @@ def _gemm_operand(t: torch.Tensor, contig_dim: int):
 
 
 _GEMM_BK = int(os.environ.get("HEAT_GEMM_VARIANT", "4"))  # 128-tile exact GEMM block: 2 = 128x128, 4 = 128x256
+_SPLITK = os.environ.get("HEAT_GEMM_SPLITK", "1") != "0"
+_SPLITK_MIN_K = 1024          # K per slice: the pipeline's prologue / C epilogue amortised over >= 64 k-stages
+_SPLITK_MAX_BYTES = 1 << 29   # partial buffer cap
+
+
+def _splitk_slices(M: int, N: int, K: int, device) -> int:
+    """Number of K slices for a 256 x 256-tile GEMM whose output tiles cover less than half the CUs
+    (1 = no split): enough slices for one workgroup per CU, each >= _SPLITK_MIN_K deep."""
+    if not _SPLITK:
+        return 1
+    tiles = -(-M // 256) * -(-N // 256)
+    ncu = num_cus(device)
+    if 2 * tiles > ncu or K < 2 * _SPLITK_MIN_K:
+        return 1
+    s = min(-(-ncu // tiles), K // _SPLITK_MIN_K, max(1, _SPLITK_MAX_BYTES // (4 * M * N)))
+    return max(1, s)
 _HA_UNSUPPORTED = 2
 
 
@@ -1074,6 +1090,17 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     L = lib()
     st = ctypes.c_void_p(stream_ptr(a.device))
     ldc = out.stride(0) if M > 1 else N
+    slices = _splitk_slices(M, N, K, a.device)
+    if slices > 1:
+        # few 256 x 256 output tiles: split K so the grid fills the CUs, fp32 partial per slice,
+        # slices summed in fixed order (fp64) with alpha / accumulate in the same pass
+        P = torch.empty(slices * M * N, dtype=torch.float32, device=a.device)
+        rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(P), M, N, K, lda, ldb, N, int(a_km), int(not b_nm), 1.0, 0, 0,
+                            slices, M * N, st)
+        if rc == 0:
+            check(L.ha_sum_slices32(_ptr(P), L.ha_gemm_tiled_slices(K, slices), M, N, M * N, _ptr(out), ldc,
+                                    float(alpha), int(accumulate), st), "ha_sum_slices32")
+            return out
     rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(not b_nm),
                         float(alpha), int(accumulate), 0, 1, 0, st)
     if rc == _HA_UNSUPPORTED:
@@ -1134,9 +1161,19 @@ def gemm_h3_planes(pa: H3Planes, pb: H3Planes, out: torch.Tensor, alpha: float =
     if pa.Kp != pb.Kp:
         raise ValueError("gemm_h3_planes: contraction lengths differ")
     M, N = pa.rows, pb.rows
-    check(lib().ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(out),
-                            M, N, pa.Kp, pa.Rp, pb.Rp, out.stride(0) if M > 1 else N, float(alpha), int(accumulate),
-                            0, 1, 0, ctypes.c_void_p(stream_ptr(out.device))), "ha_gemm_h3t")
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(out.device))
+    slices = _splitk_slices(M, N, pa.Kp, out.device)
+    if slices > 1:   # few output tiles: split K (see gemm_f32)
+        P = torch.empty(slices * M * N, dtype=torch.float32, device=out.device)
+        check(L.ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(P), M,
+                            N, pa.Kp, pa.Rp, pb.Rp, N, 1.0, 0, 0, slices, M * N, st), "ha_gemm_h3t")
+        check(L.ha_sum_slices32(_ptr(P), L.ha_gemm_tiled_slices(pa.Kp, slices), M, N, M * N, _ptr(out),
+                                out.stride(0) if M > 1 else N, float(alpha), int(accumulate), st), "ha_sum_slices32")
+        return out
+    check(L.ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(out),
+                        M, N, pa.Kp, pa.Rp, pb.Rp, out.stride(0) if M > 1 else N, float(alpha), int(accumulate),
+                        0, 1, 0, st), "ha_gemm_h3t")
     return out
 
 

@@ -167,3 +167,53 @@ def test_gemm_h3t_gram_alpha_accumulate_and_nonfinite():
     y = x.clone()
     y[3, 4] = float("inf")
     assert ops.gemm_h3(y, gram) is None
+
+
+@pytest.mark.parametrize("m,k,n", [(2048, 8192, 2048), (300, 5000, 520), (256, 2048, 256), (1000, 65536, 40),
+                                   (4, 4096, 4)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt"])
+def test_gemm_f32_split_k(m, k, n, layout, monkeypatch):
+    """Few output tiles: K split over slices (one fp32 partial per slice, fixed-order fp64 slice
+    sum with alpha / accumulate); same error class as the unsplit GEMM, deterministic, and equal
+    to the unsplit kernel within that bound."""
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + k + n)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    assert K._splitk_slices(m, n, k, dev) > 1 or m * n > 64 * 65536 or k < 2048
+    c = ops.gemm_f32(A, B)
+    ref = a.double() @ b.double()
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
+    assert torch.equal(ops.gemm_f32(A, B), c)
+    c0 = torch.randn(m, n, generator=g).to(dev)
+    c2 = c0.clone()
+    ops.gemm_f32(A, B, out=c2, accumulate=True, alpha=-0.5)
+    assert torch.all((c2.double() - (c0.double() - 0.5 * ref)).abs() <= 0.5 * _bound(a, b) + 1e-6)
+    monkeypatch.setattr(K, "_SPLITK", False)
+    cu = ops.gemm_f32(A, B)
+    assert torch.all((cu.double() - c.double()).abs() <= 2 * _bound(a, b))
+
+
+@pytest.mark.parametrize("m,k,n", [(2048, 8192, 2048), (300, 5000, 520)])
+def test_gemm_h3_split_k(m, k, n):
+    """The fused fp16x3 GEMM with few output tiles takes the split-K path: fp32-GEMM accuracy."""
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    assert K._splitk_slices(m, n, k, dev) > 1
+    g = torch.Generator().manual_seed(m + 2 * k + n)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    c = ops.gemm_h3(a, b)
+    ref = a.double() @ b.double()
+    assert torch.all((c.double() - ref).abs() <= 4 * _bound(a, b)), (c.double() - ref).abs().max()
+    c0 = torch.randn(m, n, generator=g).to(dev)
+    c2 = c0.clone()
+    ops.gemm_h3(a, b, out=c2, alpha=2.0, accumulate=True)
+    assert torch.all((c2.double() - (c0.double() + 2 * ref)).abs() <= 8 * _bound(a, b) + 1e-5)
