@@ -123,12 +123,40 @@ def _native_fp32(a: torch.Tensor, b: torch.Tensor) -> bool:
     return ops.use_native(a)
 
 
+def _library_better(M: int, N: int, K: int, exact: bool) -> bool:
+    """Plain fp32 GEMMs whose 256 x 256 output tiles fill the 256 CUs poorly go to the library
+    (hipBLASLt, exact fp32 products). Measured (``tools/microbench/gemm_small.py``, profiles/README):
+    hipBLASLt 0.029 / 0.133 / 0.46 / 3.06 ms vs gemm_f32t 0.27 / 0.30 / 0.74 / 4.44 ms at 1024^3 /
+    2048^3 / 3072^3 / 6144^3 (tail waves), and vs the fp16x3 kernel 0.20 / 0.26 ms at 1024^3 /
+    2048^3; the hand-written kernels win or tie from ~4 full waves of tiles (8192^3: 7.7 vs 7.2 ms
+    exact, 3.3 ms fp16x3; 1.25e6 x 4096^2: 296 vs 283 ms exact without the library's 4 GB
+    blocking) and on tiny-output, huge-K products through split-K (512^2 x 1e6: 3.8 vs 5.5 ms)."""
+    tiles = -(-M // 256) * -(-N // 256)
+    if tiles <= 16 and K >= (1 << 18):
+        return False            # split-K on the hand-written kernel
+    return tiles < (1024 if exact else 256)
+
+
 def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
           accumulate: bool = False) -> torch.Tensor:
     """``alpha * a @ b`` (``+ out`` when ``accumulate``) for 2-D operands: device fp32 on the
     hand-written MFMA kernels - the fused fp16x3 kernel when the float32 matmul precision allows it,
     else the exact f32-MFMA kernel (both 256 x 256 tiles, any operand layout, 64-bit offsets, so no
-    blocking); other dtypes / host tensors on torch (blocked below the library's operand limit)."""
+    blocking) - except products with too few output tiles to fill the GPU, which run on the library
+    with exact fp32 products (:func:`_library_better`); other dtypes / host tensors on torch
+    (blocked below the library's operand limit)."""
+    if _native_fp32(a, b) and _library_better(a.shape[0], b.shape[1], a.shape[1], not _split_gemm_ok(a, b)):
+        prev = torch.get_float32_matmul_precision()
+        torch.set_float32_matmul_precision("highest")   # exact fp32 products under any setting
+        try:
+            r = _mm_blocked(a, b)
+        finally:
+            torch.set_float32_matmul_precision(prev)
+        if alpha != 1.0:
+            r = r * alpha
+        if out is None:
+            return r
+        return out.add_(r) if accumulate else out.copy_(r)
     if _native_fp32(a, b):
         from ... import ops
 

@@ -29,25 +29,27 @@ def _stale(target, deps):
 
 def _build_asan():
     hipcc = _build.hipcc()
-    os.makedirs(ASAN_DIR, exist_ok=True)
+    obj_dir = os.path.join(ASAN_DIR, "obj")   # per-source objects: only changed sources recompile
+    os.makedirs(obj_dir, exist_ok=True)
     deps = _build.sources() + _build.headers() + [__file__]
     if _stale(ASAN_LIB, deps):
         flags = ["--offload-arch=" + _build.ARCH, "-O1", "-g", "-std=c++17", "-fPIC", "-Wno-unused-value",
                  "-Wno-unused-result", "-I" + _build.CSRC] + HOST_ASAN
-        objs = [os.path.join(ASAN_DIR, os.path.basename(s) + ".o") for s in _build.sources()]
+        objs = [os.path.join(obj_dir, os.path.basename(s) + ".o") for s in _build.sources()]
+        common = _build.headers() + [__file__]
+        todo = [(src, obj) for src, obj in zip(_build.sources(), objs) if _stale(obj, [src] + common)]
 
         def cc(so):
             src, obj = so
-            subprocess.run([hipcc] + flags + _build.file_flags(src) + ["-c", src, "-o", obj], check=True,
+            subprocess.run([hipcc] + flags + _build.file_flags(src) + ["-c", src, "-o", obj + ".part"], check=True,
                            capture_output=True)
+            os.replace(obj + ".part", obj)
 
-        jobs = max(1, min(len(objs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+        jobs = max(1, min(max(len(todo), 1), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
         with ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(cc, zip(_build.sources(), objs)))
+            list(ex.map(cc, todo))
         subprocess.run([hipcc, "--offload-arch=" + _build.ARCH, "-shared", "-fPIC"] + HOST_ASAN + objs +
                        ["-ldl", "-o", ASAN_LIB], check=True, capture_output=True)
-        for o in objs:
-            os.unlink(o)
     if _stale(DRIVER, [ASAN_LIB, DRIVER_SRC]):
         # the driver is plain host C++ (ROCm's clang, the same ASan runtime as the library's host code)
         clang = os.path.join(os.path.dirname(os.path.realpath(hipcc)), "..", "lib", "llvm", "bin", "clang++")
