@@ -719,13 +719,15 @@ def test_gemm_f16x3_nonfinite_falls_back(gpu):
 
 def test_matmul_split_precision(gpu):
     """ht.matmul / ht.linalg.qr honour torch's float32 matmul precision ("high" -> the fused
-    fp16x3 kernel gemm_h3t, "highest" -> the exact f32 MFMA kernel), both hand-written."""
+    fp16x3 kernel gemm_h3t, "highest" -> the exact f32 MFMA kernel), both hand-written for products
+    with enough output tiles to fill the GPU (smaller ones go to the library with exact fp32
+    products, see test_matmul_small_products_use_library)."""
     import heat_amd as ht
     from heat_amd import ops
 
     ht.random.seed(2)
-    a = ht.random.randn(4096, 1024, split=0)
-    b = ht.random.randn(1024, 512)
+    a = ht.random.randn(16384, 1024, split=0)
+    b = ht.random.randn(1024, 4096)          # 64 x 16 = 1024 output tiles of 256 x 256
     ref = a.larray.double() @ b.larray.double()
     old = torch.get_float32_matmul_precision()
     calls = []
@@ -758,6 +760,34 @@ def test_matmul_split_precision(gpu):
     assert torch.allclose(qr, a.larray.double(), atol=1e-4)
     qd = q.larray.double()
     assert torch.allclose(qd.T @ qd, torch.eye(qd.shape[1], dtype=torch.float64, device="cuda"), atol=1e-4)
+
+
+def test_matmul_small_products_use_library(gpu):
+    """A product whose 256-tiles cannot fill the CUs runs on the library with EXACT fp32 products
+    under either precision setting (no hand-written kernel is called) and matches fp64."""
+    import heat_amd as ht
+    from heat_amd import ops
+
+    ht.random.seed(5)
+    a = ht.random.randn(2048, 1024, split=0)
+    b = ht.random.randn(1024, 2048)
+    ref = a.larray.double() @ b.larray.double()
+    calls = []
+    orig_h3, orig_f32 = ops.gemm_h3, ops.gemm_f32
+    ops.gemm_h3 = lambda *x, **k: calls.append("h3") or orig_h3(*x, **k)
+    ops.gemm_f32 = lambda *x, **k: calls.append("f32") or orig_f32(*x, **k)
+    old = torch.get_float32_matmul_precision()
+    try:
+        for prec in ("high", "highest"):
+            torch.set_float32_matmul_precision(prec)
+            c = ht.matmul(a, b).larray
+            assert torch.get_float32_matmul_precision() == prec
+            err = ((c.double() - ref).abs() / (a.larray.abs().double() @ b.larray.abs().double())).max().item()
+            assert err < 1024 * 2.0 ** -24, (prec, err)   # exact-fp32 class, not a reduced-precision path
+    finally:
+        torch.set_float32_matmul_precision(old)
+        ops.gemm_h3, ops.gemm_f32 = orig_h3, orig_f32
+    assert calls == [], calls
 
 
 @pytest.mark.parametrize("m,n", [(5000, 300), (131, 64), (20000, 1024)])
