@@ -590,8 +590,7 @@ class DNDarray:
                 bounds.append((k, dim))
             dim += 1
         if bounds:
-            ext = torch.stack([torch.stack([k.min(), k.max()]).to(torch.int64).cpu() if k.is_cuda
-                               else torch.stack([k.min(), k.max()]).to(torch.int64) for k, _ in bounds]).tolist()
+            ext = [torch.stack(torch.aminmax(k)).to(torch.int64).tolist() for k, _ in bounds]
             for (lo, hi), (_, d) in zip(ext, bounds):
                 n = self.gshape[d]
                 bad = lo if lo < -n else hi if hi >= n else None
