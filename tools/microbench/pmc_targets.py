@@ -53,6 +53,10 @@ def main():
         for _ in range(3):
             ht.random.randn(1_000_000, 800, split=0)
             ht.random.rand(1_000_000, 800, split=0)
+    elif which == "hh":
+        # round 4: two-level Householder QR pieces (panel steps, sliced V^T C, library update)
+        a = torch.randn(400_000, 1024, device="cuda")
+        ops.householder_qr(a, 0, a.shape[0], True)
     torch.cuda.synchronize()
     print("done", which)
 

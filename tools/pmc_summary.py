@@ -33,11 +33,12 @@ def short(name):
 
 
 def main(root, out):
-    lines = ["# rocprofv3 PMC counters of the hot kernels (one MI355X, round 3)", "",
+    rnd = os.environ.get("PMC_ROUND", "3")
+    lines = ["# rocprofv3 PMC counters of the hot kernels (one MI355X, round {})".format(rnd), "",
              "Produced by `tools/gpu_pmc_r03.sh` (three passes per workload: SQ issue / MFMA counters, "
              "FETCH_SIZE, WRITE_SIZE; `--kernel-trace` only besides the counters) and `tools/pmc_summary.py`. "
              "Workloads: `tools/microbench/pmc_targets.py`. Kernels under 20 us are omitted.", ""]
-    for w in ("kmeans", "moments", "gemm", "cdist", "topk"):
+    for w in os.environ.get("PMC_TARGETS", "kmeans moments gemm cdist topk").split():
         fa = glob.glob(os.path.join(root, w + "_A", "*counter_collection.csv"))
         fb = glob.glob(os.path.join(root, w + "_B", "*counter_collection.csv"))
         fc = glob.glob(os.path.join(root, w + "_C", "*counter_collection.csv"))
