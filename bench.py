@@ -8,7 +8,12 @@ Data are synthetic (Threefry normal samples generated on the device, random-init
 ``value`` is the whole-job GFLOP/s of the distance computation (2*n*k*f per iteration, the
 quantity the reference's benchmark scales with); ``ms_per_step`` the wall time of one iteration.
 
-Run: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Run: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (starts N rank processes itself) or
+``torchrun --nproc-per-node N bench.py --gpus N`` (WORLD_SIZE must equal ``--gpus``).
+``--comm {pg,native,ipc}`` picks the device collective path of the timed loop, ``--ring
+{ring,direct}`` the Y-block circulation; at world > 1 the k-means all-reduce payload is also timed
+on every path (``extra.comm_ab``) and ``extra.comm.collective_paths`` counts the path each
+collective of the run took.
 Secondary workloads: ``--workload cdist`` (distance_matrix, streamed), ``--workload knn`` (the
 distance_matrix config reduced to each row's ``--topk`` nearest rows by the fused kernel, no
 matrix) and ``--workload moments`` (statistical_moments mean/var of 1e9 float32).
@@ -43,11 +48,102 @@ def parse():
                    help="kmeans fast: also time this many steps of the exact fp32-MFMA path (0 = skip)")
     p.add_argument("--with-reference", action="store_true",
                    help="also time a reference-style (heat 1.1 algorithm) iteration on torch-ROCm")
+    p.add_argument("--comm", default="pg", choices=["pg", "native", "ipc"],
+                   help="device collectives of the timed loop: torch ProcessGroupNCCL (RCCL), the native "
+                        "stream-ordered RCCL communicator (comm.hip) or the xGMI IPC kernels (ipc_allreduce.hip)")
+    p.add_argument("--ring", default="ring", choices=["ring", "direct"],
+                   help="Y-block circulation of the cdist/knn workloads: neighbour ring or all-peer direct posts")
+    p.add_argument("--comm-ab", type=int, default=1,
+                   help="world > 1: also time the k-means all-reduce payload on every comm path after the timed "
+                        "loop (0 = skip); bounded by a watchdog so a stuck path cannot hold the result back")
     return p.parse_args()
+
+
+def launch_or_check(args) -> int:
+    """Rank bookkeeping BEFORE anything touches the GPU (no torch.cuda call other than
+    device_count here, never exec): -1 = this process is a rank, go on; else an exit code.
+
+    * under a launcher (WORLD_SIZE set) the launcher's world must equal ``--gpus``;
+    * without one, ``--gpus N > 1`` starts N rank processes itself (subprocesses with
+      RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* = 127.0.0.1), relays rank 0's stdout, and fails if any
+      rank fails (the first failure terminates the others)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print("bench.py: --gpus {} but the launcher started WORLD_SIZE={} ranks".format(args.gpus, ws),
+                  file=sys.stderr, flush=True)
+            return 2
+        return -1
+    if args.gpus <= 1:
+        return -1
+    ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+    if 0 < ndev < args.gpus:
+        print("bench.py: --gpus {} but only {} GPUs are visible".format(args.gpus, ndev), file=sys.stderr, flush=True)
+        return 2
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE, start_new_session=True))
+
+    def relay(r, pr):
+        for line in iter(pr.stdout.readline, b""):
+            if r == 0:
+                sys.stdout.write(line.decode(errors="replace"))
+                sys.stdout.flush()
+            else:
+                sys.stderr.write("[rank {}] {}".format(r, line.decode(errors="replace")))
+
+    pumps = [threading.Thread(target=relay, args=(r, pr), daemon=True) for r, pr in enumerate(procs)]
+    for t in pumps:
+        t.start()
+    rc, alive = 0, set(range(args.gpus))
+    while alive:
+        for r in sorted(alive):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            alive.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print("bench.py: rank {} exited with {}; stopping the others".format(r, code), file=sys.stderr,
+                      flush=True)
+                for q in alive:
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        if alive:
+            time.sleep(0.05)
+    for t in pumps:
+        t.join(timeout=5)
+    return rc
+
+
+def apply_comm_env(args) -> None:
+    """Select the collective paths of this rank before ``heat_amd`` is imported."""
+    os.environ["HEAT_COMM_NATIVE"] = "1" if args.comm == "native" else os.environ.get("HEAT_COMM_NATIVE", "0")
+    os.environ["HEAT_IPC_ALLREDUCE"] = "1" if args.comm == "ipc" else os.environ.get("HEAT_IPC_ALLREDUCE", "0")
+    os.environ["HEAT_RING_MODE"] = args.ring
 
 
 def main():
     args = parse()
+    rc = launch_or_check(args)
+    if rc >= 0:
+        sys.exit(rc)
+    apply_comm_env(args)
     import heat_amd as ht
     from heat_amd.core.communication import MPI_WORLD
 
@@ -67,7 +163,9 @@ def main():
     extra = {"world_size_seen_by_rccl": rccl_world_size(comm)}
     scaling = "weak"
     if args.workload == "kmeans":
-        args.n_per_gpu = args.n_per_gpu or 12_500_000
+        # 1.25e7 points per GPU (8 GPUs = the BASELINE's 1e8); a CPU-only host (the gloo contract
+        # tests, no GPU) defaults to 2^16 so that a plain ``--gpus N`` finishes in seconds
+        args.n_per_gpu = args.n_per_gpu or (12_500_000 if torch.cuda.is_available() else 1 << 16)
         n, k, f = args.n_per_gpu * n_gpus, args.k, args.f or 64
         ht.random.seed(1234)
         x = ht.random.randn(n, f, split=0, device=dev)
@@ -198,12 +296,107 @@ def main():
                "parallelism": "dp{}".format(n_gpus)}
     if args.workload == "kmeans" and args.precision == "fast":
         unit = "GFLOP/s (fp32-equivalent)"
+    from heat_amd.core.communication import PATH_COUNTS
+    from heat_amd.parallel.ring import PASSES
+
+    extra["comm"] = {"requested": args.comm, "ring_mode": args.ring, "collective_paths": dict(PATH_COUNTS),
+                     "ring_passes": dict(PASSES)}
+    cfg["comm"] = args.comm
+    out = {"metric": metric, "value": value, "unit": unit, "n_gpus": n_gpus, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": scaling,
+           "vs_baseline": None, "dtype": "fp32", "data": "synthetic (device Threefry normal samples)",
+           "config": cfg, "extra": extra}
+    if comm.size > 1 and args.comm_ab:
+        # after the timed loop and its result: the all-reduce of the k-means payload on every
+        # path, under a watchdog (a path that hangs on this node must not cost the measurement)
+        payload = (args.k * (args.f or 64) + args.k) * 8
+        dog = Watchdog(float(os.environ.get("HEAT_BENCH_AB_TIMEOUT", "120")), comm.rank, out)
+        extra["comm_ab"] = comm_ab(comm, dev, [8, payload])
+        dog.cancel()
     if comm.rank == 0:
-        out = {"metric": metric, "value": value, "unit": unit, "n_gpus": n_gpus, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": scaling,
-               "vs_baseline": None, "dtype": "fp32", "data": "synthetic (device Threefry normal samples)",
-               "config": cfg, "extra": extra}
         print(json.dumps(out), flush=True)
+
+
+class Watchdog:
+    """Prints ``out`` (rank 0, marked) and ends the process if the guarded section has not
+    finished within ``seconds``."""
+
+    def __init__(self, seconds: float, rank: int, out: dict):
+        import threading
+
+        self.rank, self.out = rank, out
+        self.timer = threading.Timer(seconds, self.fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def fire(self):
+        if self.rank == 0:
+            self.out["extra"]["comm_ab"] = {"error": "timed out"}
+            print(json.dumps(self.out), flush=True)
+        os._exit(0)
+
+    def cancel(self):
+        self.timer.cancel()
+
+
+def comm_ab(comm, dev, sizes) -> dict:
+    """Microseconds per all-reduce (SUM, fp64, max over ranks, 20 back-to-back calls after 3
+    warm-up calls) of each payload in ``sizes`` bytes on each device path: torch ProcessGroup
+    (RCCL via ProcessGroupNCCL, or gloo on a CPU job), the native RCCL communicator (``comm.hip``)
+    and the xGMI IPC one-/two-shot kernels (``ipc_allreduce.hip``); every result is checked
+    (sum of ones == world size). A path whose construction fails on any rank is skipped on all."""
+    import torch.distributed as dist
+
+    import heat_amd as ht
+
+    res = {}
+    reps = 20
+    paths = [("pg", lambda b: dist.all_reduce(b))]
+    if torch.cuda.is_available():
+        from heat_amd.parallel import ipc as _ipc
+        from heat_amd.parallel import native_comm as _nc
+
+        def agree(make):
+            obj, err = None, None
+            try:
+                obj = make()
+            except Exception as e:  # noqa: BLE001 - reported, and the path skipped on every rank
+                err = "{}: {}".format(type(e).__name__, e)[:300]
+            ok = comm.allreduce(int(err is None), ht.MPI.MIN)
+            return (obj if ok else None), err
+
+        nc, err = agree(lambda: comm._native() or _nc.NativeComm(comm))
+        if nc is not None:
+            paths.append(("native", lambda b: nc.allreduce_(b, "sum")))
+        else:
+            res["native_error"] = err or "failed on another rank"
+        ar, err = agree(lambda: getattr(comm, "_ipc", None) or _ipc.IpcAllreduce(comm, capacity_bytes=max(sizes)))
+        if ar is not None:
+            paths.append(("ipc", lambda b: ar.allreduce_(b)))
+        else:
+            res["ipc_error"] = err or "failed on another rank"
+    device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    for name, fn in paths:
+        for nbytes in sizes:
+            buf = torch.ones(max(1, nbytes // 8), dtype=torch.float64, device=device)
+            fn(buf)
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            ok = bool((buf == comm.size).all())
+            for _ in range(2):
+                fn(buf)
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            comm.Barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn(buf)
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            us = (time.perf_counter() - t0) / reps * 1e6
+            res["{}_{}B_us".format(name, nbytes)] = comm.allreduce(us, ht.MPI.MAX)
+            res["{}_{}B_ok".format(name, nbytes)] = bool(comm.allreduce(int(ok), ht.MPI.MIN))
+    return res
 
 
 def validate_kmeans(km, x, comm, k: int) -> dict:

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import os
 import pickle
+from collections import Counter
 from typing import Any, Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -39,6 +40,11 @@ from ..parallel import staging as _SD
 
 # device buffers are handed straight to RCCL unless the world group is gloo-only (host staging)
 CUDA_AWARE_MPI = os.environ.get("HEAT_COMM_BACKEND", "").lower() != "gloo"
+
+#: collective -> data path counters ("allreduce:ipc", "allreduce:native", "allreduce:pg",
+#: "allgatherv:...", "reduce_scatter:..."); ``bench.py`` reports them so a run records which
+#: path (torch ProcessGroup / native RCCL communicator / xGMI IPC kernels) each collective took
+PATH_COUNTS = Counter()
 
 
 # ----------------------------------------------------------------------------------------------
@@ -428,12 +434,14 @@ class MPICommunication(Communication):
     def _reduce_tensor_async(self, t: torch.Tensor, op: Op):
         """All-reduce ``t`` in place (returns (work, finalize))."""
         if op is MPI.SUM and self._ipc_allreduce(t) is not None:
+            PATH_COUNTS["allreduce:ipc"] += 1
             return None, None  # stream-ordered on the current stream: nothing to wait for
         opname = {MPI.SUM: "sum", MPI.PROD: "prod", MPI.MAX: "max", MPI.MIN: "min"}.get(op)
         if t.is_cuda and opname is not None and self._native() is not None and self._native().supports(t, opname):
             nc = self._native()
             contig = t if t.is_contiguous() else t.contiguous()
             nc.allreduce_(contig, opname)  # ordered on the current stream: nothing to wait for
+            PATH_COUNTS["allreduce:native"] += 1
             if contig is not t:
                 t.copy_(contig)
             return None, None
@@ -441,6 +449,7 @@ class MPICommunication(Communication):
         if native:
             contig = _wire_dtype(t) if t.is_contiguous() else _wire_dtype(t).contiguous()
             work = _SD.all_reduce(contig, op=op.torch_op, group=self.group, async_op=True)
+            PATH_COUNTS["allreduce:pg"] += 1
 
             def fin():
                 if contig is not t:
@@ -557,11 +566,14 @@ class MPICommunication(Communication):
             counts = self.allgather_sizes(moved.shape[0])
         rest = tuple(moved.shape[1:])
         got = self._ipc_allgather(moved, counts) if len(counts) else None
+        path = "ipc"
         if got is None and moved.is_cuda and len(counts) and self._native() is not None \
                 and moved.dtype in (torch.int8, torch.uint8, torch.bool, torch.int32, torch.int64, torch.float16,
                                     torch.float32, torch.float64, torch.bfloat16):
             got = self._native().allgatherv(moved, counts)  # grouped RCCL p2p on the current stream
+            path = "native"
         if got is not None:
+            PATH_COUNTS["allgatherv:" + path] += 1
             return _SD.StagedWork(None), (lambda: got.movedim(0, axis) if axis != 0 else got)
         mx = max(counts) if len(counts) else 0
         if all(c == mx for c in counts):
@@ -571,6 +583,7 @@ class MPICommunication(Communication):
             padded[: moved.shape[0]] = moved
         out = torch.empty((self.size * mx,) + rest, dtype=moved.dtype, device=moved.device)
         work = _SD.all_gather_into_tensor(out, padded, group=self.group, async_op=True)
+        PATH_COUNTS["allgatherv:pg"] += 1
 
         def fin():
             if all(c == mx for c in counts):
@@ -593,7 +606,9 @@ class MPICommunication(Communication):
         nc = self._native() if inp.is_cuda else None
         if nc is not None and opname is not None and nc.supports(inp, opname) and inp.is_contiguous() \
                 and out.is_contiguous():
+            PATH_COUNTS["reduce_scatter:native"] += 1
             return nc.reduce_scatter(inp, out, opname)
+        PATH_COUNTS["reduce_scatter:pg"] += 1
         _SD.reduce_scatter_tensor(out, inp, op=op.torch_op, group=self.group)
         return out
 

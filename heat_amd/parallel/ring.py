@@ -9,12 +9,17 @@ isend/irecv to the ring neighbours), so communication overlaps the compute of ``
 from __future__ import annotations
 
 import os
+from collections import Counter
 from typing import Callable, List
 
 import torch
 import torch.distributed as dist
 
 from . import staging as _SD
+
+
+#: passes taken per mode ("ring" / "direct"), reported by ``bench.py``
+PASSES = Counter()
 
 
 def ring_mode() -> str:
@@ -38,7 +43,9 @@ def ring_pass(block: torch.Tensor, fn: Callable[[torch.Tensor, int], None], comm
     if sizes is None:
         sizes = comm.allgather_sizes(block.shape[0])
     if (mode or ring_mode()) == "direct":
+        PASSES["direct"] += 1
         return _direct_pass(block, fn, comm, sizes)
+    PASSES["ring"] += 1
     rest = tuple(block.shape[1:])
     cur = block.contiguous()
     src = me

@@ -72,3 +72,47 @@ def test_bench_secondary_workloads_validate(workload):
     else:
         assert lines[0]["scaling"] == "strong" and lines[0]["config"]["global_batch"] == 6000
         assert ex["self_first"] is True and ex["index_agreement"] == 1.0 and ex["max_rel_dist_err"] < 1e-5
+
+
+def _clean_env(**kw):
+    env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", **kw)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        if k not in kw:
+            env.pop(k, None)
+    return env
+
+
+def test_bench_self_launches_gpus_ranks():
+    """``bench.py --gpus 4`` with no launcher starts 4 rank processes itself and relays ONE JSON
+    line from rank 0 that saw a 4-rank device world."""
+    cmd = [sys.executable, "bench.py", "--gpus", "4", "--steps", "2", "--warmup", "1", "--n-per-gpu", "3000",
+           "--exact-steps", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    assert rec["n_gpus"] == 4 and rec["extra"]["world_size_seen_by_rccl"] == 4
+    assert rec["config"]["parallelism"] == "dp4" and rec["config"]["global_batch"] == 4 * 3000
+    # every path the run took is recorded, and the A/B all-reduce timing ran and was checked
+    assert rec["extra"]["comm"]["collective_paths"].get("allreduce:pg", 0) > 0
+    ab = rec["extra"]["comm_ab"]
+    assert ab["pg_8B_ok"] is True and ab["pg_532480B_ok"] is True and ab["pg_8B_us"] > 0
+
+
+def test_bench_world_size_mismatch_fails():
+    cmd = [sys.executable, "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_clean_env(WORLD_SIZE="2", RANK="0"), capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr
+    assert not _json_lines(r.stdout)
+
+
+def test_bench_failing_rank_fails_the_job():
+    """A rank that dies (here: an invalid workload size on every rank) makes the self-launched job
+    exit non-zero without a JSON line."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--n-per-gpu", "-5"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True, timeout=180)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)
