@@ -42,18 +42,39 @@ constexpr int KS_FMAX = 64;
 constexpr int KS_LDMAX = KS_FMAX + 4;  // padded LDS row stride (words) at f = 64
 enum { KS_ROW4 = 0, KS_FLAT = 1, KS_SCALAR = 2 };
 
-// ceil(f / 4) * 4 + 4: 16-byte aligned rows, conflict-free row-per-lane b128 reads
-__host__ __device__ inline int ks_ld(int f) { return ((f + 3) / 4) * 4 + 4; }
-__host__ __device__ inline int ks_fp(int f) { return ((f + 7) / 8) * 8; }
+// features covered by the assignment: a multiple of 16 (a loop iteration takes 16 / CPI...16
+// features, see ks_step); the LDS rows are fp + 4 words: 16-byte aligned, zero beyond f, and the
+// row-per-lane ds_read_b128 of a 16-lane pass conflict-free (fp + 4 = 4 mod 16 words: the 16 start
+// banks are 4 apart modulo 64)
+__host__ __device__ inline int ks_fp(int f) { return ((f + 15) / 16) * 16; }
+__host__ __device__ inline int ks_ld(int f) { return ks_fp(f) + 4; }
 
-// padded centroid copy: Cp[c][j] (c < KP, j < FP); rows >= k at +inf, features >= f zero
+// chunked centroid copy for the scalar (SGPR-operand) reads of the assignment:
+// Cq[q][c][4] = C[c][4q .. 4q+3] for the fp / 4 chunks q (+ one zero chunk past the end);
+// rows c >= k at +inf (they never win), features >= f zero
 __global__ __launch_bounds__(256) void ks_pad_centroids(const float* __restrict__ C, int k, int f, int64_t ldc,
-                                                        int kp, float* __restrict__ Cp) {
+                                                        int kp, float* __restrict__ Cq) {
   const int fp = ks_fp(f);
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= kp * fp) return;
-  const int c = e / fp, j = e - c * fp;
-  Cp[e] = c < k ? (j < f ? C[(int64_t)c * ldc + j] : 0.f) : (j == 0 ? __builtin_huge_valf() : 0.f);
+  if (e >= kp * (fp + 4)) return;
+  const int q = e / (4 * kp), c = (e / 4) % kp, j = 4 * q + (e & 3);
+  Cq[e] = c < k ? (j < f ? C[(int64_t)c * ldc + j] : 0.f) : (j == 0 ? __builtin_huge_valf() : 0.f);
+}
+
+// acc[c] += (x - c)^2 over one 4-feature chunk for the KP centroids: the centroid pair is an SGPR
+// operand of v_pk_add_f32 (x - c in one packed op; the compiler does not select SGPR pairs for
+// packed fp32 by itself and fell back to scalar subtracts plus SGPR spills to VGPR lanes)
+template <int KP>
+__device__ __forceinline__ void ks_chunk(const floatx4 (&cc)[KP], floatx4 x, floatx2 (&acc)[KP]) {
+  const floatx2 x0 = {x[0], x[1]}, x1 = {x[2], x[3]};
+#pragma unroll
+  for (int c = 0; c < KP; ++c) {
+    floatx2 d0, d1;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d0) : "v"(x0), "s"((floatx2){cc[c][0], cc[c][1]}));
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d1) : "v"(x1), "s"((floatx2){cc[c][2], cc[c][3]}));
+    acc[c] = __builtin_elementwise_fma(d0, d0, acc[c]);
+    acc[c] = __builtin_elementwise_fma(d1, d1, acc[c]);
+  }
 }
 
 // NFB: 16-feature blocks covered by the update (4 for f <= 64, 2 for f <= 32)
@@ -161,31 +182,24 @@ __global__ __launch_bounds__(KS_ROWS, 4) void ks_step(const float* __restrict__ 
     store(rows);
     __syncthreads();
     if (t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight during this tile's compute
-    // ---- assign: thread = row, centroids as SGPR operands (wave-uniform scalar loads)
+    // ---- assign: thread = row, centroids as SGPR operands (wave-uniform scalar loads of CPI
+    // chunks per loop iteration, one lgkm wait per iteration)
     {
       const float* xr = tile + (tid < rows ? tid : 0) * ld;
+      const floatx4* Cq = reinterpret_cast<const floatx4*>(Cp);
+      constexpr int CPI = KP <= 4 ? 2 : 1;  // 4-feature chunks per iteration
       floatx2 acc[KP];
 #pragma unroll
       for (int c = 0; c < KP; ++c) acc[c] = (floatx2)(0.f);
-#pragma unroll 2
-      for (int j = 0; j < fp; j += 8) {
-        const floatx4 xa = *reinterpret_cast<const floatx4*>(xr + j);
-        // xb lies in the row's zero padding when f <= j + 4 (ld >= 4 ceil(f/4) + 4 >= j + 8 then)
-        const floatx4 xb = *reinterpret_cast<const floatx4*>(xr + j + 4);
-        const floatx2 x0 = {xa[0], xa[1]}, x1 = {xa[2], xa[3]}, x2 = {xb[0], xb[1]}, x3 = {xb[2], xb[3]};
+      for (int q = 0; q < (fp >> 2); q += CPI) {
+        floatx4 cc[CPI][KP];
 #pragma unroll
-        for (int c = 0; c < KP; ++c) {
-          const floatx4 ca = *reinterpret_cast<const floatx4*>(Cp + c * fp + j);
-          const floatx4 cb = *reinterpret_cast<const floatx4*>(Cp + c * fp + j + 4);
-          const floatx2 d0 = x0 - (floatx2){ca[0], ca[1]};
-          const floatx2 d1 = x1 - (floatx2){ca[2], ca[3]};
-          const floatx2 d2 = x2 - (floatx2){cb[0], cb[1]};
-          const floatx2 d3 = x3 - (floatx2){cb[2], cb[3]};
-          acc[c] = __builtin_elementwise_fma(d0, d0, acc[c]);
-          acc[c] = __builtin_elementwise_fma(d1, d1, acc[c]);
-          acc[c] = __builtin_elementwise_fma(d2, d2, acc[c]);
-          acc[c] = __builtin_elementwise_fma(d3, d3, acc[c]);
-        }
+        for (int u = 0; u < CPI; ++u)
+#pragma unroll
+          for (int c = 0; c < KP; ++c) cc[u][c] = Cq[(q + u) * KP + c];
+#pragma unroll
+        for (int u = 0; u < CPI; ++u)
+          ks_chunk<KP>(cc[u], *reinterpret_cast<const floatx4*>(xr + 4 * (q + u)), acc);
       }
       float best = acc[0][0] + acc[0][1];
       int bi = 0;
@@ -253,6 +267,123 @@ __global__ __launch_bounds__(KS_ROWS, 4) void ks_step(const float* __restrict__ 
   }
 }
 
+// The common case as its own kernel: f = 64, 16-byte aligned rows, whole 128-row tiles (the
+// generic kernel above takes the tail). Fixed index math keeps the register file to the prefetch
+// buffer, the accumulators and ONE live load address: in the generic kernel the compiler hoists
+// the per-piece row/column/LDS offsets of the guarded load/store loops out of the tile loop (~60
+// VGPRs + spills to AGPRs at 256 registers), and the SGPR-resident centroids spilled into VGPR
+// lanes. Thread t's pieces are rows (t >> 4) + 8 i, features 4 (t & 15) .. +3: each load
+// instruction covers 4 whole 256-byte rows, and the LDS stores use immediate offsets.
+template <int KP, bool UPDATE>
+__global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
+                                                        const float* __restrict__ Cp, int* __restrict__ labels,
+                                                        float* __restrict__ mind, float* __restrict__ sums_part,
+                                                        float* __restrict__ counts_part) {
+  constexpr int LD = KS_LDMAX;
+  __shared__ __attribute__((aligned(16))) float tile[KS_ROWS * LD];
+  __shared__ int lab[KS_ROWS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c4 = tid & 15, rb = tid >> 4;
+  if (tid < KS_ROWS) *reinterpret_cast<floatx4*>(tile + tid * LD + KS_FMAX) = (floatx4)(0.f);  // row padding
+  floatx4 uacc[2][4];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) uacc[b][g] = (floatx4)(0.f);
+  float ucnt = 0.f;
+  floatx4 buf[16];
+  const int64_t pstride = 8 * ldx;
+  typedef const floatx4 __attribute__((address_space(1)))* gptr;  // global, not flat (flat loads count in lgkmcnt)
+  auto load = [&](int64_t t) {
+    gptr p = (gptr)(X + (t * KS_ROWS + rb) * ldx + 4 * c4);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      buf[i] = __builtin_nontemporal_load(p);
+      p += pstride / 4;
+      asm volatile("" : "+v"(p));  // one live address, not 16 hoisted ones
+    }
+  };
+  float* const st = tile + rb * LD + 4 * c4;
+  const floatx4* Cq = reinterpret_cast<const floatx4*>(Cp);
+  constexpr int CPI = KP <= 8 ? 2 : 1;
+  int64_t t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) *reinterpret_cast<floatx4*>(st + i * 8 * LD) = buf[i];
+    __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight during this tile's compute
+    const int64_t row0 = t * KS_ROWS;
+    {
+      const float* xr = tile + tid * LD;
+      floatx2 acc[KP];
+#pragma unroll
+      for (int c = 0; c < KP; ++c) acc[c] = (floatx2)(0.f);
+      for (int q = 0; q < KS_FMAX / 4; q += CPI) {
+        floatx4 cc[CPI][KP];
+#pragma unroll
+        for (int u = 0; u < CPI; ++u)
+#pragma unroll
+          for (int c = 0; c < KP; ++c) cc[u][c] = Cq[(q + u) * KP + c];
+#pragma unroll
+        for (int u = 0; u < CPI; ++u)
+          ks_chunk<KP>(cc[u], *reinterpret_cast<const floatx4*>(xr + 4 * (q + u)), acc);
+      }
+      float best = acc[0][0] + acc[0][1];
+      int bi = 0;
+#pragma unroll
+      for (int c = 1; c < KP; ++c) {
+        const float d = acc[c][0] + acc[c][1];
+        const bool better = d < best;
+        best = better ? d : best;
+        bi = better ? c : bi;
+      }
+      if (labels) labels[row0 + tid] = bi;
+      if (mind) mind[row0 + tid] = best;
+      lab[tid] = bi;
+    }
+    if (UPDATE) {
+      __syncthreads();
+      // onehot(labels)^T X on v_mfma_f32_16x16x4_f32, wave w owns feature blocks w and w + 2
+      const int kq = lane >> 4, c16 = lane & 15;
+#pragma unroll 2
+      for (int r0 = 0; r0 < KS_ROWS; r0 += 16) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r = r0 + 4 * g + kq;
+          const float a = lab[r] == c16 ? 1.f : 0.f;
+          const float* xrow = tile + r * LD + c16;
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            uacc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xrow[(wave + 2 * b) * 16], uacc[b][g], 0, 0, 0);
+        }
+      }
+      if (wave == 0) {
+#pragma unroll
+        for (int c = 0; c < KP; ++c) {
+          const int cnt = __popcll(__ballot(lab[lane] == c)) + __popcll(__ballot(lab[64 + lane] == c));
+          ucnt += lane == c ? (float)cnt : 0.f;
+        }
+      }
+    }
+    __syncthreads();  // the tile is overwritten next
+  }
+  if (UPDATE) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int cb = wave + 2 * b;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 4 * (lane >> 4) + i;
+        if (c < KP)
+          sums_part[((int64_t)blockIdx.x * KP + c) * KS_FMAX + cb * 16 + (lane & 15)] =
+              (uacc[b][0][i] + uacc[b][1][i]) + (uacc[b][2][i] + uacc[b][3][i]);
+      }
+    }
+    if (wave == 0 && lane < KP) counts_part[(int64_t)blockIdx.x * KP + lane] = ucnt;
+  }
+}
+
 // sums[c][j] = sum over the workgroups' partials (fp64), counts[c] likewise: one workgroup per
 // output, its threads stride over the partials (a thread-per-output loop over ~1000 partials was
 // latency-bound at ~0.5 ms)
@@ -281,6 +412,56 @@ __global__ __launch_bounds__(256) void ks_reduce(const float* __restrict__ sums_
 
 int ks_kp(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : 16; }
 
+template <int KP, int MODE, bool U>
+void ks_launch_generic(int nblk, hipStream_t s, const float* X, int64_t n, int f, int64_t ldx, const float* cpad,
+                       int* labels, float* mind, float* sp, float* cp) {
+  if (U && f <= 32)
+    hipLaunchKernelGGL((ks_step<KP, MODE, U, 2>), dim3(nblk), dim3(KS_ROWS), 0, s, X, n, f, ldx, cpad, labels, mind,
+                       sp, cp);
+  else
+    hipLaunchKernelGGL((ks_step<KP, MODE, U, 4>), dim3(nblk), dim3(KS_ROWS), 0, s, X, n, f, ldx, cpad, labels, mind,
+                       sp, cp);
+}
+
+// one pass: ks_step64 over the whole tiles when it applies (f = 64, aligned rows) plus the
+// generic kernel on the remaining rows as ONE extra partial slot, else the generic kernel alone;
+// then the fp64 reduction of the partials
+template <int KP, bool U>
+void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, int f, int64_t ldx, const float* cpad,
+               int* labels, float* mind, float* sp, float* cp, int k, float* sums, float* counts) {
+  int nblk = 0;
+  int64_t done = 0;
+  if (mode == KS_ROW4 && f == KS_FMAX) {
+    const int64_t full = n / KS_ROWS;
+    if (full > 0) {
+      nblk = (int)(full < 4 * num_cus ? full : 4 * num_cus);
+      hipLaunchKernelGGL((ks_step64<KP, U>), dim3(nblk), dim3(KS_ROWS), 0, s, X, full, ldx, cpad, labels, mind, sp, cp);
+      done = full * KS_ROWS;
+    }
+  }
+  const int64_t rest = n - done;
+  if (rest > 0) {
+    const int64_t ntiles = (rest + KS_ROWS - 1) / KS_ROWS;
+    const int g = done > 0 ? 1 : (int)(ntiles < 4 * num_cus ? ntiles : 4 * num_cus);
+    const float* Xr = X + done * ldx;
+    int* lr = labels ? labels + done : nullptr;
+    float* mr = mind ? mind + done : nullptr;
+    float* spr = sp + (int64_t)nblk * KP * KS_FMAX;
+    float* cpr = cp + (int64_t)nblk * KP;
+    if (mode == KS_ROW4)
+      ks_launch_generic<KP, KS_ROW4, U>(g, s, Xr, rest, f, ldx, cpad, lr, mr, spr, cpr);
+    else if (mode == KS_FLAT)
+      ks_launch_generic<KP, KS_FLAT, U>(g, s, Xr, rest, f, ldx, cpad, lr, mr, spr, cpr);
+    else
+      ks_launch_generic<KP, KS_SCALAR, U>(g, s, Xr, rest, f, ldx, cpad, lr, mr, spr, cpr);
+    nblk += g;
+  }
+  if (U) hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, sums, counts);
+}
+
+// partial slots: 4 per CU + one for the tail rows of the f = 64 kernel
+int ks_slots(int num_cus) { return 4 * num_cus + 1; }
+
 }  // namespace
 
 HA_EXPORT int ha_ks_max_k() { return 16; }
@@ -289,7 +470,7 @@ HA_EXPORT int ha_ks_max_f() { return KS_FMAX; }
 // Workspace floats: per-workgroup partials (nblk = 4 workgroups per CU) + the padded centroids.
 HA_EXPORT int64_t ha_ks_workspace_floats(int k, int num_cus) {
   if (k <= 0 || k > 16 || num_cus <= 0) return -1;
-  return (int64_t)4 * num_cus * ks_kp(k) * (KS_FMAX + 1) + (int64_t)ks_kp(k) * KS_FMAX;
+  return (int64_t)ks_slots(num_cus) * ks_kp(k) * (KS_FMAX + 1) + (int64_t)ks_kp(k) * (KS_FMAX + 4);
 }
 
 // One pass over X [n, f] (f <= 64, k <= 16): labels (int32, optional), mind (optional) and, when
@@ -300,55 +481,33 @@ HA_EXPORT int ha_ks_step(const float* X, int64_t n, int f, int64_t ldx, const fl
   if (k <= 0 || k > 16 || f <= 0 || f > KS_FMAX || ldx < f || ldc < f || num_cus <= 0) return HA_BAD_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int kp = ks_kp(k);
-  const int64_t ntiles = (n + KS_ROWS - 1) / KS_ROWS;
-  int nblk = 4 * num_cus;
-  if (ntiles < nblk) nblk = (int)(ntiles > 0 ? ntiles : 1);
   const bool al = ((uintptr_t)X & 15) == 0;
   const int mode = (f % 4 == 0 && ldx % 4 == 0 && al) ? KS_ROW4 : (ldx == f && f >= 4 && al) ? KS_FLAT : KS_SCALAR;
   const bool upd = sums != nullptr;
+  const int64_t slots = ks_slots(num_cus);
   float* sp = workspace;
-  float* cp = workspace + (int64_t)4 * num_cus * kp * KS_FMAX;
-  float* cpad = workspace + (int64_t)4 * num_cus * kp * (KS_FMAX + 1);
+  float* cp = workspace + slots * kp * KS_FMAX;
+  float* cpad = workspace + slots * kp * (KS_FMAX + 1);
   if (upd && n <= 0) {
-    hipMemsetAsync(sums, 0, (size_t)k * f * sizeof(float), s);
-    hipMemsetAsync(counts, 0, (size_t)k * sizeof(float), s);
+    (void)hipMemsetAsync(sums, 0, (size_t)k * f * sizeof(float), s);
+    (void)hipMemsetAsync(counts, 0, (size_t)k * sizeof(float), s);
     return ha_launch_status();
   }
   if (n <= 0) return HA_OK;
-  hipLaunchKernelGGL(ks_pad_centroids, dim3((unsigned)((kp * ks_fp(f) + 255) / 256)), dim3(256), 0, s, C, k, f, ldc,
-                     kp, cpad);
-#define HA_KS_L(KP, V, U)                                                                                   \
-  if (U && f <= 32)                                                                                         \
-    hipLaunchKernelGGL((ks_step<KP, V, U, 2>), dim3(nblk), dim3(KS_ROWS), 0, s, X, n, f, ldx, cpad, labels, mind, sp, \
-                       cp);                                                                                 \
-  else                                                                                                      \
-    hipLaunchKernelGGL((ks_step<KP, V, U, 4>), dim3(nblk), dim3(KS_ROWS), 0, s, X, n, f, ldx, cpad, labels, mind, sp, \
-                       cp)
-#define HA_KS_M(KP, M)                                                                                      \
-  if (upd)                                                                                                  \
-    HA_KS_L(KP, M, true);                                                                                   \
-  else                                                                                                      \
-    HA_KS_L(KP, M, false);
-#define HA_KS_KP(KP)                                                                                        \
-  if (mode == KS_ROW4) {                                                                                    \
-    HA_KS_M(KP, KS_ROW4)                                                                                    \
-  } else if (mode == KS_FLAT) {                                                                             \
-    HA_KS_M(KP, KS_FLAT)                                                                                    \
-  } else {                                                                                                  \
-    HA_KS_M(KP, KS_SCALAR)                                                                                  \
-  }                                                                                                         \
-  if (upd)                                                                                                  \
-    hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk,          \
-                       k, f, sums, counts);
+  hipLaunchKernelGGL(ks_pad_centroids, dim3((unsigned)((kp * (ks_fp(f) + 4) + 255) / 256)), dim3(256), 0, s, C, k, f,
+                     ldc, kp, cpad);
+#define HA_KS(KP)                                                                                            \
+  if (upd)                                                                                                   \
+    ks_launch<KP, true>(mode, num_cus, s, X, n, f, ldx, cpad, labels, mind, sp, cp, k, sums, counts);        \
+  else                                                                                                       \
+    ks_launch<KP, false>(mode, num_cus, s, X, n, f, ldx, cpad, labels, mind, sp, cp, k, sums, counts);
   if (kp == 4) {
-    HA_KS_KP(4)
+    HA_KS(4)
   } else if (kp == 8) {
-    HA_KS_KP(8)
+    HA_KS(8)
   } else {
-    HA_KS_KP(16)
+    HA_KS(16)
   }
-#undef HA_KS_KP
-#undef HA_KS_M
-#undef HA_KS_L
+#undef HA_KS
   return ha_launch_status();
 }

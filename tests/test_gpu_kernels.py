@@ -857,7 +857,8 @@ def test_knn_classifier_fused(gpu):
     assert (pred.cpu() == ref.cpu()).float().mean() > 0.99
 
 
-@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (3000, 128), (777, 200), (100, 1), (300000, 60)])
+@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (3000, 128), (777, 200), (100, 1), (300000, 60),
+                                 (384, 64), (100, 64), (129, 64)])
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
 def test_kmeans_step_small(n, f, k):
     """Fused small-k Lloyd pass: labels == fp64 argmin, sums/counts == index_add of the points."""
