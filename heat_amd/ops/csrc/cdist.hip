@@ -11,6 +11,8 @@
 // m x n x f intermediate (the reference's _manhattan_fast materialises one).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int BM = 128, BN = 128, KB = 32;   // output tile, features per LDS chunk
@@ -189,6 +191,113 @@ __global__ __launch_bounds__(256) void cdist_vk(const float* __restrict__ X, int
   }
 }
 
+// Exact kernel, round 5: 128 x 128 outputs per workgroup, 8 x 8 per thread (rows 4 tr + {0..3,
+// 64..67}, columns 4 tc + {0..3, 64..67}: four ds_read_b128 per feature feed 64 difference pairs).
+// The staging issues ALL of a chunk's global loads before the first LDS write (the kernel above
+// waits for each load before issuing the next: its SUSY 40k x 18 run was bound by that serial
+// load latency, 2.25 ms of which 1.80 ms without the stores): a thread loads 4 consecutive rows
+// of one feature column (32 lanes = one 128-byte run of a row) and writes them transposed as one
+// ds_write_b128. Squared differences on packed fp32 (x broadcast by op_sel), |x - y| on scalar
+// v_sub + v_add with the abs modifier (no abs on packed ops).
+constexpr int VB = 128, VK = 32, VS = VB + 4;  // tile, features per chunk, LDS row stride
+
+template <int OP>
+__global__ __launch_bounds__(256, 2) void cdist_vx(const float* __restrict__ X, int64_t m, const float* __restrict__ Y,
+                                                   int64_t n, int f, int64_t ldx, int64_t ldy, float* __restrict__ C,
+                                                   int64_t ldc, float scale, int64_t per_xcd, int vec_out) {
+  __shared__ __attribute__((aligned(16))) float sx[VK * VS];
+  __shared__ __attribute__((aligned(16))) float sy[VK * VS];
+  const int tid = threadIdx.x;
+  const int64_t tiles_n = (n + VB - 1) / VB;
+  const int64_t tiles = ((m + VB - 1) / VB) * tiles_n;
+  const int64_t t = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  if (t >= tiles) return;
+  const int64_t row0 = (t / tiles_n) * VB, col0 = (t % tiles_n) * VB;
+  const int tr = tid >> 4, tc = tid & 15;
+  // staging role: feature column sc, 4-row groups sq + 8 u (u = 0..3) of the 32 groups
+  const int sc = tid & 31, sq = tid >> 5;
+  floatx2 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (floatx2)(0.f);
+  // buffer descriptors over this tile's rows (the range check returns 0 past the last valid row):
+  // one 32-bit per-lane offset, the per-load row offsets are scalars
+  const int xrows = (int)(m - row0 < VB ? m - row0 : VB), yrows = (int)(n - col0 < VB ? n - col0 : VB);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X + row0 * ldx), (short)0, (int)(((int64_t)(xrows - 1) * ldx + f) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Y + col0 * ldy), (short)0, (int)(((int64_t)(yrows - 1) * ldy + f) * 4), 0x00020000);
+  for (int k0 = 0; k0 < f; k0 += VK) {
+    floatx4 vx[4], vy[4];
+    const bool cin = k0 + sc < f;
+    const int ox = (int)((4 * sq * ldx + k0 + sc) * 4), oy = (int)((4 * sq * ldy + k0 + sc) * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 32 * u + j;
+        const float a = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, ox, (int)(r * ldx * 4), 0));
+        const float b = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, oy, (int)(r * ldy * 4), 0));
+        vx[u][j] = cin ? a : 0.f;
+        vy[u][j] = cin ? b : 0.f;
+      }
+    }
+    if (k0 > 0) __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      *reinterpret_cast<floatx4*>(sx + sc * VS + 4 * (sq + 8 * u)) = vx[u];
+      *reinterpret_cast<floatx4*>(sy + sc * VS + 4 * (sq + 8 * u)) = vy[u];
+    }
+    __syncthreads();
+    const int kk = (f - k0) < VK ? (f - k0) : VK;
+    for (int k = 0; k < kk; ++k) {
+      const floatx4 xa = *reinterpret_cast<const floatx4*>(sx + k * VS + 4 * tr);
+      const floatx4 xb = *reinterpret_cast<const floatx4*>(sx + k * VS + 64 + 4 * tr);
+      const floatx4 ya = *reinterpret_cast<const floatx4*>(sy + k * VS + 4 * tc);
+      const floatx4 yb = *reinterpret_cast<const floatx4*>(sy + k * VS + 64 + 4 * tc);
+      const float xv[8] = {xa[0], xa[1], xa[2], xa[3], xb[0], xb[1], xb[2], xb[3]};
+      const floatx2 yv[4] = {{ya[0], ya[1]}, {ya[2], ya[3]}, {yb[0], yb[1]}, {yb[2], yb[3]}};
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (OP == 0) {
+            acc[a][b][0] += __builtin_fabsf(xv[a] - yv[b][0]);
+            acc[a][b][1] += __builtin_fabsf(xv[a] - yv[b][1]);
+          } else {
+            const floatx2 d = (floatx2){xv[a], xv[a]} - yv[b];
+            acc[a][b] = __builtin_elementwise_fma(d, d, acc[a][b]);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    const int64_t row = row0 + 4 * tr + (a & 3) + 64 * (a >> 2);
+    if (row >= m) continue;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t col = col0 + 64 * h + 4 * tc;
+      float o[4] = {acc[a][2 * h][0], acc[a][2 * h][1], acc[a][2 * h + 1][0], acc[a][2 * h + 1][1]};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if (OP == 1) o[v] = __builtin_amdgcn_sqrtf(o[v]);
+        else if (OP == 3) o[v] = __expf(-o[v] * scale);
+      }
+      float* cp = C + row * ldc + col;
+      if (vec_out && col + 3 < n) {
+        __builtin_nontemporal_store((floatx4){o[0], o[1], o[2], o[3]}, reinterpret_cast<floatx4*>(cp));
+      } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (col + v < n) cp[v] = o[v];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // mode: 0 euclidean, 1 squared euclidean, 2 gaussian (exp(-d2*scale)) - MFMA quadratic expansion;
@@ -197,7 +306,25 @@ HA_EXPORT int ha_cdist(const float* X, int64_t m, const float* Y, int64_t n, int
                        int64_t ldc, int mode, float scale, void* stream) {
   if (m <= 0 || n <= 0) return HA_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (mode >= 3) {
+  static const bool vk64 = [] { const char* e = getenv("HEAT_CDIST_VK64"); return e && atoi(e) != 0; }();
+  // cdist_vx addresses a 128-row tile with 32-bit byte offsets
+  const bool fits = (int64_t)VB * (ldx > ldy ? ldx : ldy) * 4 < 0x7fffffffLL;
+  if (mode >= 3 && !vk64 && fits) {
+    const int64_t tiles = ((m + VB - 1) / VB) * ((n + VB - 1) / VB);
+    const int64_t per_xcd = (tiles + 7) / 8;
+    if (per_xcd * 8 > 0x7fffffffLL) return HA_UNSUPPORTED;
+    const int vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+    const dim3 g((unsigned)(per_xcd * 8)), b(256);
+    switch (mode) {
+      case 3: hipLaunchKernelGGL(cdist_vx<0>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 4: hipLaunchKernelGGL(cdist_vx<1>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 5: hipLaunchKernelGGL(cdist_vx<2>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 6: hipLaunchKernelGGL(cdist_vx<3>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      default: return HA_BAD_ARG;
+    }
+    return ha_launch_status();
+  }
+  if (mode >= 3) {  // round-4 64 x 64 kernel (HEAT_CDIST_VK64=1, A/B only)
     const int64_t tiles = ((m + LB - 1) / LB) * ((n + LB - 1) / LB);
     const int64_t per_xcd = (tiles + 7) / 8;
     if (per_xcd * 8 > 0x7fffffffLL) return HA_UNSUPPORTED;

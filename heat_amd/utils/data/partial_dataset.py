@@ -114,6 +114,8 @@ class PartialH5Dataset(torch_data.Dataset):
         self.load_thread = None
         self.io_queue = None
         self._next_first = None
+        self._cancel = threading.Event()
+        self._epoch_done = True
 
     # ------------------------------------------------------------------ windows and reads
     def _windows(self):
@@ -156,20 +158,60 @@ class PartialH5Dataset(torch_data.Dataset):
             items = [t(x) if t is not None else x for t, x in zip(self.transforms, items)]
         return items[0] if len(items) == 1 else tuple(items)
 
-    def thread_replace_converted_batches(self, out: "queue.Queue", windows) -> None:
+    @staticmethod
+    def _put(out: "queue.Queue", item, cancel: threading.Event) -> bool:
+        """Put ``item`` into the bounded ``out``, giving up (False) once ``cancel`` is set: an
+        abandoned iterator (a consumer that broke out of its epoch) never leaves the loader
+        blocked on a queue nobody reads."""
+        while not cancel.is_set():
+            try:
+                out.put(item, timeout=0.05)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def thread_replace_converted_batches(self, out: "queue.Queue", windows, cancel: threading.Event = None) -> None:
         """Background loader: read ``windows`` in order into ``out`` (bounded, so at most two
         windows are held ahead), then the end marker, then pre-read the first window of the next
-        epoch into ``self._next_first``."""
+        epoch into ``self._next_first``. Stops early once ``cancel`` is set."""
+        cancel = cancel if cancel is not None else threading.Event()
         try:
             for lo, hi in windows:
-                out.put((lo, self._read(lo, hi)))
+                if cancel.is_set():
+                    return
+                if not self._put(out, (lo, self._read(lo, hi)), cancel):
+                    return
                 self.loads_remaining -= 1
         except BaseException as e:  # surfaced in the consumer
-            out.put(("error", e))
+            self._put(out, ("error", e), cancel)
             return
-        out.put(_END)
+        if not self._put(out, _END, cancel) or cancel.is_set():
+            return
         lo, hi = self.windows[0]
         self._next_first = (lo, self._read(lo, hi))
+
+    def _stop_loader(self) -> None:
+        """End the previous epoch's loader thread. A finished epoch (its end marker consumed)
+        only waits for the pre-read of window 0; an abandoned one is cancelled, its queue
+        drained so a blocked put returns, and its pre-read discarded."""
+        th = self.load_thread
+        if th is None:
+            return
+        if not getattr(self, "_epoch_done", False):
+            self._cancel.set()
+            q = self.io_queue
+            while th.is_alive():
+                try:
+                    while q is not None:
+                        q.get_nowait()
+                except queue.Empty:
+                    pass
+                th.join(timeout=0.05)
+            self._next_first = None
+        else:
+            th.join()
+        self.load_thread = None
 
 
 class PartialH5DataLoaderIter:
@@ -191,19 +233,20 @@ class PartialH5DataLoaderIter:
         self._order = []
         self._pos = 0
         ds.loads_remaining = ds.loads_needed
+        ds._stop_loader()  # the previous epoch's thread: finished, or cancelled if abandoned
         if ds.windows and ds.resident_start != ds.windows[0][0]:
-            if ds.load_thread is not None:
-                ds.load_thread.join()  # it ends with the pre-read of this window
             first = getattr(ds, "_next_first", None)
             lo, hi = ds.windows[0]
             ds._set_resident(first[1] if first is not None else ds._read(lo, hi), lo)
         ds._next_first = None
         self._queue = None
+        ds._epoch_done = False
         if ds.partial_dataset and len(ds.windows) > 1:
             self._queue = queue.Queue(maxsize=2)
             ds.io_queue = self._queue
+            ds._cancel = threading.Event()
             ds.load_thread = threading.Thread(target=ds.thread_replace_converted_batches,
-                                              args=(self._queue, ds.windows[1:]), daemon=True)
+                                              args=(self._queue, ds.windows[1:], ds._cancel), daemon=True)
             ds.load_thread.start()
         self._start_window()
 
@@ -218,6 +261,7 @@ class PartialH5DataLoaderIter:
         item = self._queue.get()  # blocks: a slow loader delays the batch, it never drops rows
         if item is _END:
             self._queue = None
+            self.dataset._epoch_done = True
             return False
         if item[0] == "error":
             raise item[1]

@@ -123,6 +123,32 @@ def check_partial_h5_slow_loader_sees_every_row():
     assert sorted(seen) == list(range(lo, lo + share))
 
 
+def check_partial_h5_break_then_full_epoch():
+    """A consumer that breaks out of an epoch (after moving past window 0, and within window 0)
+    must not leave the loader blocked on its bounded queue: the next epoch starts, and sees every
+    row of the share exactly once (4+ windows)."""
+    comm = ht.MPI_WORLD
+    n = 97 * comm.size
+    path = _h5_file(comm, n)
+    ds = ht.utils.data.PartialH5Dataset(path, comm=comm, dataset_names=["data", "labels"], use_gpu=False,
+                                        initial_load=10, load_length=8)
+    share = n // comm.size
+    assert len(ds.windows) >= 4
+    lo = comm.rank * share
+    for stop_after in (5, 1, 0, 23):    # batches consumed before the break (5 and 23: past window 0)
+        loader = ht.utils.data.DataLoader(ds, batch_size=2)
+        t0 = time.time()
+        for i, _ in enumerate(loader):
+            if i + 1 >= stop_after:
+                break
+        time.sleep(0.2)                 # the abandoned loader fills its queue and blocks
+        loader = ht.utils.data.DataLoader(ds, batch_size=1)
+        seen = torch.cat([y for _, y in loader]).long().tolist()
+        assert sorted(seen) == list(range(lo, lo + share)), stop_after
+        assert time.time() - t0 < 60
+    assert ds.load_thread is None or not ds.load_thread.is_alive() or ds._epoch_done
+
+
 def check_partial_h5_validate_set():
     comm = ht.MPI_WORLD
     n = 9 * comm.size + 1

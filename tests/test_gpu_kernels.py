@@ -436,6 +436,29 @@ def test_cdist(metric, m, n, f, exact):
         assert torch.all(torch.diagonal(self_d) == 0)
 
 
+@pytest.mark.parametrize("metric", ["euclidean", "manhattan"])
+@pytest.mark.parametrize("m,n,f", [(300, 129, 37), (129, 1000, 18), (1, 5, 3), (200, 257, 65)])
+def test_cdist_exact_strided_views(metric, m, n, f):
+    """Exact (difference) kernel on row-strided views whose LAST row ends at the allocation's end
+    (the tile's buffer range must stop at column f of the last row), into an output with a row
+    stride that is not a multiple of 4 (scalar store path)."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(m + n + f)
+    bx = torch.rand(m * (f + 5), generator=g)[: (m - 1) * (f + 5) + f].to(dev)
+    by = torch.rand(n * (f + 3), generator=g)[: (n - 1) * (f + 3) + f].to(dev)
+    X = torch.as_strided(bx, (m, f), (f + 5, 1))
+    Y = torch.as_strided(by, (n, f), (f + 3, 1))
+    big = torch.full((m, n + 3), -1.0, device=dev)
+    out = big[:, :n]
+    ops.cdist(X, Y, metric, exact=True, out=out)
+    Xd, Yd = X.double(), Y.double()
+    ref = torch.cdist(Xd, Yd, p=1) if metric == "manhattan" else torch.cdist(Xd, Yd)
+    assert torch.allclose(out.double(), ref, rtol=1e-5, atol=1e-5)
+    assert torch.all(big[:, n:] == -1.0)
+
+
 @pytest.mark.parametrize("precision", ["f16x3", "fp32"])
 @pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian"])
 @pytest.mark.parametrize("m,n,f", [(100, 50, 3), (1000, 777, 18), (513, 640, 64), (130, 1100, 96), (257, 300, 128),
