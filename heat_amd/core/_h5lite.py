@@ -88,7 +88,7 @@ class H5Dataset:
                 raw = body + raw[n * es:]
             elif fid == 3:    # fletcher32: trailing 4-byte little-endian checksum, verified
                 body, stored = raw[:-4], struct.unpack("<I", raw[-4:])[0]
-                if _fletcher32(body) != stored:
+                if not _fletcher32_ok(body, stored):
                     raise IOError("HDF5 chunk of {!r} failed its fletcher32 checksum".format(self.path))
                 raw = body
             else:
@@ -755,11 +755,23 @@ def encode_chunk(block: np.ndarray, filters) -> bytes:
     return raw
 
 
-def _fletcher32(data: bytes) -> int:
+def _fletcher32_ok(body: bytes, stored: int) -> bool:
+    """Whether ``stored`` is a valid Fletcher-32 of ``body`` as HDF5 reads it
+    (``H5Z__filter_fletcher32``): the checksum, or its byte-pair-swapped form that libraries
+    before 1.6.3 wrote on little-endian hosts; also the ``% 65535``-folded value this package's
+    writer produced before round 4 (it differs only when a sum is a nonzero multiple of 65535)."""
+    c = _fletcher32(body)
+    if stored == c or stored == ((c & 0x00FF00FF) << 8) | ((c >> 8) & 0x00FF00FF):
+        return True
+    return stored == _fletcher32(body, legacy_mod=True)
+
+
+def _fletcher32(data: bytes, legacy_mod: bool = False) -> int:
     """HDF5's Fletcher-32 (``H5_checksum_fletcher32``): 16-bit big-endian words in blocks of 360,
     both sums folded with end-around carry ``(x & 0xffff) + (x >> 16)`` after every block (NOT
     ``% 65535``: a nonzero multiple of 65535 stays 0xffff), an odd trailing byte as the high byte
     of one more word, then a final fold."""
+    fold = (lambda x: x % 65535) if legacy_mod else (lambda x: (x & 0xFFFF) + (x >> 16))
     nw = len(data) // 2
     w = np.frombuffer(data, dtype=">u2", count=nw).astype(np.uint64)
     s1 = s2 = 0
@@ -767,15 +779,12 @@ def _fletcher32(data: bytes) -> int:
         c1 = np.cumsum(w[i: i + 360]) + s1
         s2 += int(c1.sum())
         s1 = int(c1[-1])
-        s1 = (s1 & 0xFFFF) + (s1 >> 16)
-        s2 = (s2 & 0xFFFF) + (s2 >> 16)
+        s1, s2 = fold(s1), fold(s2)
     if len(data) % 2:
         s1 += data[-1] << 8
         s2 += s1
-        s1 = (s1 & 0xFFFF) + (s1 >> 16)
-        s2 = (s2 & 0xFFFF) + (s2 >> 16)
-    s1 = (s1 & 0xFFFF) + (s1 >> 16)
-    s2 = (s2 & 0xFFFF) + (s2 >> 16)
+        s1, s2 = fold(s1), fold(s2)
+    s1, s2 = fold(s1), fold(s2)
     return ((s2 << 16) | s1) & 0xFFFFFFFF
 
 

@@ -40,6 +40,10 @@ _NUMBER_TYPES = {torch.float32, torch.float64, torch.int8, torch.int16, torch.in
 
 
 _INT_DIVS = {torch.div, torch.true_divide, torch.floor_divide, torch.remainder, torch.fmod}
+# floating tensors: only where the number is used as-is. Torch's device division by a scalar
+# multiplies by its reciprocal (x / 3.0 off by an ulp, x / 1e-40 -> inf) and pow by a scalar
+# switches to special cases (sqrt, x*x*x), so those keep the correctly rounded 0-d tensor path
+_FLOAT_NUMBER_OK = {torch.add, torch.sub, torch.mul, torch.eq, torch.ne, torch.lt, torch.le, torch.gt, torch.ge}
 
 
 def _number_operand(operation, fn_kwargs, ptype, v) -> bool:
@@ -49,7 +53,7 @@ def _number_operand(operation, fn_kwargs, ptype, v) -> bool:
     if operation not in _NUMBER_OK or fn_kwargs or ptype not in _NUMBER_TYPES or isinstance(v, bool):
         return False
     if ptype.is_floating_point:
-        return isinstance(v, (int, float))
+        return operation in _FLOAT_NUMBER_OK and isinstance(v, (int, float))
     if not isinstance(v, int) or operation in _INT_DIVS:
         return False
     info = torch.iinfo(ptype)

@@ -160,3 +160,21 @@ print("OK", worst)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_scalar_division_and_pow_exact_on_device(gpu):
+    """Division and pow by a Python number on a device array are correctly rounded (the 0-d
+    tensor path; torch's scalar form multiplies by the reciprocal): bitwise equal to NumPy."""
+    import numpy as np
+    import heat_amd as ht
+
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=4099).astype(np.float32) * 1e3
+    a = ht.array(x, split=0, device="gpu")
+    assert a.larray.is_cuda
+    for v in (3.0, 7.0, 1e-40, 0.1):
+        got = (a / v).numpy()
+        ref = (x / np.float32(v)).astype(np.float32)
+        assert np.array_equal(got, ref), v
+    assert np.all(np.isfinite((a / 1e-40).numpy()[np.abs(x) < 1e-3]))
+    np.testing.assert_allclose((a ** 3.0).numpy(), np.power(x.astype(np.float64), 3.0), rtol=3e-7)

@@ -61,6 +61,20 @@ def test_fletcher32_verified_on_read(tmp_path):
         ht.load_hdf5(p, "d", dtype=ht.int32).numpy()
 
 
+def test_fletcher32_accepts_reversed_and_legacy_forms():
+    """HDF5 reads chunks whose checksum is byte-pair swapped (libraries before 1.6.3); this
+    package's pre-round-4 writer folded with % 65535; a wrong checksum is still refused."""
+    rng = np.random.default_rng(5)
+    body = rng.integers(0, 256, 1000, dtype=np.uint8).tobytes()
+    c = _h5lite._fletcher32(body)
+    rev = ((c & 0x00FF00FF) << 8) | ((c >> 8) & 0x00FF00FF)
+    assert _h5lite._fletcher32_ok(body, c) and _h5lite._fletcher32_ok(body, rev)
+    assert not _h5lite._fletcher32_ok(body, c ^ 0x10)
+    ones = b"\xff" * 4096                      # sums are multiples of 65535: the two folds differ
+    assert _h5lite._fletcher32(ones) == 0xFFFFFFFF and _h5lite._fletcher32(ones, legacy_mod=True) == 0
+    assert _h5lite._fletcher32_ok(ones, 0)
+
+
 def test_netcdf_cdf5_header_roundtrip(tmp_path):
     p = str(tmp_path / "x.nc")
     h = _ncclassic.write_with_variable(p, None, "v", ["a", "b"], (3, 4), _ncclassic.nc_type_for(np.int64), False)

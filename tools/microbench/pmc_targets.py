@@ -6,7 +6,9 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   cdist   - one 32768 x 32768 x 128 distance tile (cdist_f16x3.hip)
   topk    - 8 nearest of 65536 x 128 queries among 1e6 points (spatial.cdist_topk -> h3_topk)
   knn     - the bench.py knn step: 8 nearest of all 1e6 x 128 rows among themselves (certified h1_topk)
-  randn   - 8e8 standard normals and 8e8 uniforms, fp32 (threefry.hip: tf_fill32, 3.2 GB each)"""
+  randn   - 8e8 standard normals and 8e8 uniforms, fp32 (threefry.hip: tf_fill32, 3.2 GB each)
+  smallk  - 10 fused small-k passes, k = 8, 1.25e7 x 64 (kmeans_smallk.hip: ks_step64, the reference protocol)
+  cdist_exact - exact (difference) cdist, SUSY size 40k x 18, 3 calls (cdist.hip: cdist_vx)"""
 import sys
 
 import torch
@@ -53,6 +55,15 @@ def main():
         for _ in range(3):
             ht.random.randn(1_000_000, 800, split=0)
             ht.random.rand(1_000_000, 800, split=0)
+    elif which == "smallk":
+        x = torch.randn(12_500_000, 64, device="cuda")
+        c = torch.randn(8, 64, device="cuda")
+        for _ in range(10):
+            ops.kmeans_step_small(x, c)
+    elif which == "cdist_exact":
+        x = torch.rand(40_000, 18, device="cuda")
+        for _ in range(3):
+            ops.cdist(x, x, exact=True)
     elif which == "hh":
         # round 4: two-level Householder QR pieces (panel steps, sliced V^T C, library update)
         a = torch.randn(400_000, 1024, device="cuda")
