@@ -273,6 +273,26 @@ __global__ __launch_bounds__(256, 2) void cdist_vx(const float* __restrict__ X, 
       }
     }
   }
+  auto fin = [&](float v) {
+    if (OP == 1) return __builtin_amdgcn_sqrtf(v);
+    if (OP == 3) return __expf(-v * scale);
+    return v;
+  };
+  if (vec_out && row0 + VB <= m && col0 + VB <= n) {
+    // whole tile (wave-uniform): 16 unguarded 16-byte stores per thread, no per-element branches
+    // (the guarded form below costs ~400 VALU per thread, a quarter of the kernel's VALU work)
+    float* base = C + (row0 + 4 * tr) * ldc + col0 + 4 * tc;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      float* rp = base + (int64_t)((a & 3) + 64 * (a >> 2)) * ldc;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        __builtin_nontemporal_store((floatx4){fin(acc[a][2 * h][0]), fin(acc[a][2 * h][1]), fin(acc[a][2 * h + 1][0]),
+                                              fin(acc[a][2 * h + 1][1])},
+                                    reinterpret_cast<floatx4*>(rp + 64 * h));
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int64_t row = row0 + 4 * tr + (a & 3) + 64 * (a >> 2);
@@ -282,10 +302,7 @@ __global__ __launch_bounds__(256, 2) void cdist_vx(const float* __restrict__ X, 
       const int64_t col = col0 + 64 * h + 4 * tc;
       float o[4] = {acc[a][2 * h][0], acc[a][2 * h][1], acc[a][2 * h + 1][0], acc[a][2 * h + 1][1]};
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        if (OP == 1) o[v] = __builtin_amdgcn_sqrtf(o[v]);
-        else if (OP == 3) o[v] = __expf(-o[v] * scale);
-      }
+      for (int v = 0; v < 4; ++v) o[v] = fin(o[v]);
       float* cp = C + row * ldc + col;
       if (vec_out && col + 3 < n) {
         __builtin_nontemporal_store((floatx4){o[0], o[1], o[2], o[3]}, reinterpret_cast<floatx4*>(cp));

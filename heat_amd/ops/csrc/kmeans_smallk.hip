@@ -30,6 +30,7 @@
 //    sums/counts stay in registers across tiles, are written once and reduced in fp64.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -274,7 +275,9 @@ __global__ __launch_bounds__(KS_ROWS, 4) void ks_step(const float* __restrict__ 
 // VGPRs + spills to AGPRs at 256 registers), and the SGPR-resident centroids spilled into VGPR
 // lanes. Thread t's pieces are rows (t >> 4) + 8 i, features 4 (t & 15) .. +3: each load
 // instruction covers 4 whole 256-byte rows, and the LDS stores use immediate offsets.
-template <int KP, bool UPDATE>
+// AHEAD = 2: two register buffers, the loads of tile t + 2 G in flight while tile t is computed
+// (151 -> ~215 VGPRs, still two waves per SIMD); AHEAD = 1: one buffer, tile t + G.
+template <int KP, bool UPDATE, int AHEAD>
 __global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
                                                         const float* __restrict__ Cp, int* __restrict__ labels,
                                                         float* __restrict__ mind, float* __restrict__ sums_part,
@@ -291,10 +294,10 @@ __global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict_
 #pragma unroll
     for (int g = 0; g < 4; ++g) uacc[b][g] = (floatx4)(0.f);
   float ucnt = 0.f;
-  floatx4 buf[16];
+  floatx4 buf0[16], buf1[16];
   const int64_t pstride = 8 * ldx;
   typedef const floatx4 __attribute__((address_space(1)))* gptr;  // global, not flat (flat loads count in lgkmcnt)
-  auto load = [&](int64_t t) {
+  auto load = [&](floatx4(&buf)[16], int64_t t) {
     gptr p = (gptr)(X + (t * KS_ROWS + rb) * ldx + 4 * c4);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -306,13 +309,11 @@ __global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict_
   float* const st = tile + rb * LD + 4 * c4;
   const floatx4* Cq = reinterpret_cast<const floatx4*>(Cp);
   constexpr int CPI = KP <= 8 ? 2 : 1;
-  int64_t t = blockIdx.x;
-  if (t < ntiles) load(t);
-  for (; t < ntiles; t += gridDim.x) {
+  auto process = [&](floatx4(&buf)[16], int64_t t, int64_t tnext) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) *reinterpret_cast<floatx4*>(st + i * 8 * LD) = buf[i];
     __syncthreads();
-    if (t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight during this tile's compute
+    if (tnext < ntiles) load(buf, tnext);  // in flight during this tile's (and the next one's) compute
     const int64_t row0 = t * KS_ROWS;
     {
       const float* xr = tile + tid * LD;
@@ -367,6 +368,20 @@ __global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict_
       }
     }
     __syncthreads();  // the tile is overwritten next
+  };
+  const int64_t G = gridDim.x;
+  int64_t t = blockIdx.x;
+  if (AHEAD == 2) {
+    if (t < ntiles) load(buf0, t);
+    if (t + G < ntiles) load(buf1, t + G);
+    for (; t < ntiles; t += 2 * G) {
+      process(buf0, t, t + 2 * G);
+      if (t + G >= ntiles) break;
+      process(buf1, t + G, t + 3 * G);
+    }
+  } else {
+    if (t < ntiles) load(buf0, t);
+    for (; t < ntiles; t += G) process(buf0, t, t + G);
   }
   if (UPDATE) {
 #pragma unroll
@@ -381,6 +396,109 @@ __global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict_
       }
     }
     if (wave == 0 && lane < KP) counts_part[(int64_t)blockIdx.x * KP + lane] = ucnt;
+  }
+}
+
+// One-wave workgroups over 64-row tiles (f = 64): no workgroup barrier at all (a wave's LDS
+// operations execute in order), 17.7 KB of LDS per wave, so 8-9 independent waves per CU each
+// with its next tile in flight, instead of 4 two-wave workgroups stepping through 3 barriers per
+// tile. The wave does the whole update of its tile: 4 feature blocks x 16 row steps of
+// v_mfma_f32_16x16x4_f32; the counts come from ballots of the lane's own label.
+template <int KP, bool UPDATE>
+__global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
+                                                   const float* __restrict__ Cp, int* __restrict__ labels,
+                                                   float* __restrict__ mind, float* __restrict__ sums_part,
+                                                   float* __restrict__ counts_part) {
+  constexpr int LD = KS_LDMAX;
+  __shared__ __attribute__((aligned(16))) float tile[64 * LD];
+  __shared__ int lab[64];
+  const int lane = threadIdx.x;
+  const int c4 = lane & 15, rb = lane >> 4;
+  *reinterpret_cast<floatx4*>(tile + lane * LD + KS_FMAX) = (floatx4)(0.f);  // row padding
+  floatx4 uacc[4][2];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) uacc[b][0] = uacc[b][1] = (floatx4)(0.f);
+  float ucnt = 0.f;
+  floatx4 buf[16];
+  typedef const floatx4 __attribute__((address_space(1)))* gptr;
+  auto load = [&](int64_t t) {
+    gptr p = (gptr)(X + (t * 64 + rb) * ldx + 4 * c4);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      buf[i] = __builtin_nontemporal_load(p);
+      p += ldx;  // 4 rows on (4 ldx floats)
+      asm volatile("" : "+v"(p));
+    }
+  };
+  float* const st = tile + rb * LD + 4 * c4;
+  const floatx4* Cq = reinterpret_cast<const floatx4*>(Cp);
+  constexpr int CPI = KP <= 8 ? 2 : 1;
+  int64_t t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) *reinterpret_cast<floatx4*>(st + i * 4 * LD) = buf[i];
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);
+    const int64_t row0 = t * 64;
+    int bi = 0;
+    {
+      const float* xr = tile + lane * LD;
+      floatx2 acc[KP];
+#pragma unroll
+      for (int c = 0; c < KP; ++c) acc[c] = (floatx2)(0.f);
+      for (int q = 0; q < KS_FMAX / 4; q += CPI) {
+        floatx4 cc[CPI][KP];
+#pragma unroll
+        for (int u = 0; u < CPI; ++u)
+#pragma unroll
+          for (int c = 0; c < KP; ++c) cc[u][c] = Cq[(q + u) * KP + c];
+#pragma unroll
+        for (int u = 0; u < CPI; ++u)
+          ks_chunk<KP>(cc[u], *reinterpret_cast<const floatx4*>(xr + 4 * (q + u)), acc);
+      }
+      float best = acc[0][0] + acc[0][1];
+#pragma unroll
+      for (int c = 1; c < KP; ++c) {
+        const float d = acc[c][0] + acc[c][1];
+        const bool better = d < best;
+        best = better ? d : best;
+        bi = better ? c : bi;
+      }
+      if (labels) labels[row0 + lane] = bi;
+      if (mind) mind[row0 + lane] = best;
+    }
+    if (UPDATE) {
+      lab[lane] = bi;
+      const int kq = lane >> 4, c16 = lane & 15;
+#pragma unroll 4
+      for (int r0 = 0; r0 < 64; r0 += 8) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int r = r0 + 4 * g + kq;
+          const float a = lab[r] == c16 ? 1.f : 0.f;
+          const float* xrow = tile + r * LD + c16;
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            uacc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xrow[16 * b], uacc[b][g], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < KP; ++c) {
+        const int cnt = __popcll(__ballot(bi == c));
+        ucnt += lane == c ? (float)cnt : 0.f;
+      }
+    }
+  }
+  if (UPDATE) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 4 * (lane >> 4) + i;
+        if (c < KP) sums_part[((int64_t)blockIdx.x * KP + c) * KS_FMAX + b * 16 + (lane & 15)] = uacc[b][0][i] + uacc[b][1][i];
+      }
+    }
+    if (lane < KP) counts_part[(int64_t)blockIdx.x * KP + lane] = ucnt;
   }
 }
 
@@ -433,9 +551,30 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
   int64_t done = 0;
   if (mode == KS_ROW4 && f == KS_FMAX) {
     const int64_t full = n / KS_ROWS;
-    if (full > 0) {
+    // HEAT_KS_VARIANT: "wave" (one-wave workgroups, 64-row tiles), "a1" / "a2" (two-wave
+    // workgroups, 128-row tiles, one / two tiles of loads in flight)
+    static const int variant = [] {
+      const char* e = getenv("HEAT_KS_VARIANT");
+      return !e ? 1 : e[0] == 'w' ? 0 : e[1] == '2' ? 2 : 1;
+    }();
+    if (variant == 0 && n / 64 > 0) {
+      const int64_t full64 = n / 64;
+      static const int wpc = [] {  // waves per CU (LDS holds 9 of 17.7 KB)
+        const char* e = getenv("HEAT_KS_WPC");
+        const int v = e ? atoi(e) : 8;
+        return v < 1 ? 1 : v > 9 ? 9 : v;
+      }();
+      nblk = (int)(full64 < (int64_t)wpc * num_cus ? full64 : (int64_t)wpc * num_cus);
+      hipLaunchKernelGGL((ks_wave64<KP, U>), dim3(nblk), dim3(64), 0, s, X, full64, ldx, cpad, labels, mind, sp, cp);
+      done = full64 * 64;
+    } else if (full > 0) {
       nblk = (int)(full < 4 * num_cus ? full : 4 * num_cus);
-      hipLaunchKernelGGL((ks_step64<KP, U>), dim3(nblk), dim3(KS_ROWS), 0, s, X, full, ldx, cpad, labels, mind, sp, cp);
+      if (variant == 2)
+        hipLaunchKernelGGL((ks_step64<KP, U, 2>), dim3(nblk), dim3(KS_ROWS), 0, s, X, full, ldx, cpad, labels, mind, sp,
+                           cp);
+      else
+        hipLaunchKernelGGL((ks_step64<KP, U, 1>), dim3(nblk), dim3(KS_ROWS), 0, s, X, full, ldx, cpad, labels, mind, sp,
+                           cp);
       done = full * KS_ROWS;
     }
   }
@@ -459,8 +598,8 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
   if (U) hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, sums, counts);
 }
 
-// partial slots: 4 per CU + one for the tail rows of the f = 64 kernel
-int ks_slots(int num_cus) { return 4 * num_cus + 1; }
+// partial slots: up to 9 per CU + one for the tail rows of the f = 64 kernels
+int ks_slots(int num_cus) { return 9 * num_cus + 1; }
 
 }  // namespace
 

@@ -218,11 +218,20 @@ def _lex_split(key: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return d, torch.where(i == 0xFFFFFFFF, torch.full_like(i, -1), i)
 
 
-def _topk_lex(d: torch.Tensor, idx: Optional[torch.Tensor], k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def _topk_lex(d: torch.Tensor, idx: Optional[torch.Tensor], k: int,
+              max_index: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """k smallest distances per row with ties ordered by (global) index - the same answer for any
-    blocking of the candidates, hence for any number of ranks."""
+    blocking of the candidates, hence for any number of ranks. ``max_index`` bounds the indices
+    (the caller's row count): the packed keys hold 32-bit indices, so from 2^32 - 1 rows on the
+    selection runs as two stable sorts instead (index, then distance)."""
     if idx is None:
+        max_index = d.shape[1] - 1
         idx = torch.arange(d.shape[1], device=d.device).expand(d.shape[0], -1)
+    if max_index is None or max_index >= 0xFFFFFFFF:
+        o = torch.sort(idx, dim=1, stable=True).indices
+        dd, ii = torch.gather(d, 1, o), torch.gather(idx.to(torch.int64), 1, o)
+        o = torch.sort(dd.float() + 0.0, dim=1, stable=True).indices[:, :k]
+        return torch.gather(dd, 1, o).float(), torch.gather(ii, 1, o)
     key = _lex_key(d, idx)
     key = torch.topk(key, k, dim=1, largest=False).values if k < key.shape[1] else torch.sort(key, dim=1).values
     return _lex_split(key)
@@ -262,7 +271,7 @@ def _knn_exact_select(Q: torch.Tensor, T: torch.Tensor, idx: torch.Tensor, k: in
         nb = T[ib.clamp(min=0)].float()
         d = ((Q[q0: q0 + step].float().unsqueeze(1) - nb) ** 2).sum(-1)
         d = torch.where(ib >= 0, d, torch.full_like(d, float("inf")))
-        dv, di = _topk_lex(d, ib, k)
+        dv, di = _topk_lex(d, ib, k, max_index=T.shape[0] - 1)
         dist[q0: q0 + step] = dv
         out_i[q0: q0 + step] = di
     return dist, out_i
@@ -302,7 +311,7 @@ def _knn_certified(Q, T, Tc, k, packed, ws, exact_distances: bool = True):
             i3 = i3[0].long()
         else:
             _, i3 = _topk_lex(d3.permute(1, 0, 2).reshape(nu, splits * k3), i3.permute(1, 0, 2).reshape(nu, splits * k3),
-                              k3)
+                              k3, max_index=nt - 1)
         idx = idx.long()
         idx[unc] = -1
         idx[unc, :k3] = i3
@@ -354,7 +363,7 @@ def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPo
         else:
             dist = dist.permute(1, 0, 2).reshape(nq, splits * k)
             idx = idx.permute(1, 0, 2).reshape(nq, splits * k)
-            dist, idx = _topk_lex(dist, idx, k)
+            dist, idx = _topk_lex(dist, idx, k, max_index=nt - 1)
     else:
         kk = min(k, nt)
         step = max(1, (1 << 28) // max(nt, 1))

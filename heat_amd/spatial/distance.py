@@ -337,7 +337,7 @@ def cdist_topk(X: DNDarray, Y: Optional[DNDarray] = None, k: int = 1):
         ci = torch.cat([best_i, di], dim=1)
         if tt == torch.float32:
             # one top-k over packed (distance bits, index) keys (distances are >= 0)
-            best_d, best_i = ops.kernels._topk_lex(cd, ci, k)
+            best_d, best_i = ops.kernels._topk_lex(cd, ci, k, max_index=n - 1)
             return
         # (distance, index) order: stable sort by index, then stable sort by distance
         o = torch.sort(ci, dim=1, stable=True).indices

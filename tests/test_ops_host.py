@@ -212,3 +212,19 @@ def test_stale_library_after_failed_rebuild_warns(tmp_path, monkeypatch):
             ops.lib()
     finally:
         ops._lib = saved
+
+
+def test_topk_lex_wide_indices_fall_back_to_stable_sorts():
+    """Global indices from 2^32 - 1 up do not fit the packed 32-bit key: the merge falls back to
+    two stable sorts and still orders equal distances by index."""
+    import torch
+    from heat_amd.ops import kernels
+
+    d = torch.tensor([[3.0, 1.0, 1.0, 0.5, 1.0]])
+    big = 0xFFFFFFFF + 10
+    idx = torch.tensor([[big + 4, big + 3, big + 1, big + 9, big + 2]])
+    dv, di = kernels._topk_lex(d, idx, 3, max_index=big + 9)
+    assert dv.tolist() == [[0.5, 1.0, 1.0]] and di.tolist() == [[big + 9, big + 1, big + 2]]
+    small = idx - big
+    dv2, di2 = kernels._topk_lex(d, small, 3, max_index=9)
+    assert dv2.tolist() == dv.tolist() and (di2 + big).tolist() == di.tolist()
