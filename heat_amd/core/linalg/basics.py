@@ -106,6 +106,10 @@ _CHUNK_ON_HOST = False  # tests: exercise the blocking on CPU tensors too
 _GEMM_BACKEND = os.environ.get("HEAT_GEMM_BACKEND", "native")
 
 
+# Gram products (X^T X, X X^T) from this size on: the upper-triangle tiles only (ops.gram_product)
+_GRAM_MIN_N = int(os.environ.get("HEAT_GRAM_MIN_N", "512"))
+
+
 def _split_gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     """fp32 device GEMMs run as the fused fp16x3 split GEMM (fp32-GEMM accuracy on the FP16 matrix
     cores, ~2.3x faster) when torch's float32 matmul precision is "high" or "medium"
@@ -145,6 +149,16 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
     blocking) - except products with too few output tiles to fill the GPU, which run on the library
     with exact fp32 products (:func:`_library_better`); other dtypes / host tensors on torch
     (blocked below the library's operand limit)."""
+    if _native_fp32(a, b) and a.shape[0] == b.shape[1] >= _GRAM_MIN_N and a.shape[1] >= a.shape[0]:
+        from ... import ops
+
+        g = ops.gram_product(a, b)   # X^T X / X X^T: upper tiles once + mirror (exactly symmetric)
+        if g is not None:
+            if alpha != 1.0:
+                g.mul_(alpha)
+            if out is None:
+                return g
+            return out.add_(g) if accumulate else out.copy_(g)
     if _native_fp32(a, b) and _library_better(a.shape[0], b.shape[1], a.shape[1], not _split_gemm_ok(a, b)):
         prev = torch.get_float32_matmul_precision()
         torch.set_float32_matmul_precision("highest")   # exact fp32 products under any setting

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
+           "split_planes", "gram_product", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "h3_planes", "H3Planes",
            "gemm_h3_planes", "gemm64", "cholesky_upper", "tri_inv_upper", "householder_qr",
            "householder_factor", "householder_apply", "householder_block", "vtc64", "gram64",
@@ -1216,7 +1216,25 @@ _GRAM_KCHUNK = max(16, int(os.environ.get("HEAT_GRAM_KCHUNK", "4096")) // 16 * 1
 _GRAM_PARTIAL_BYTES = 1 << 30
 
 
-def gram64(x: torch.Tensor, exact: Optional[bool] = None) -> torch.Tensor:
+def gram_product(a: torch.Tensor, b: torch.Tensor) -> Optional[torch.Tensor]:
+    """``a @ b`` as a symmetric fp32 matrix when it is the Gram product of ONE device fp32 matrix
+    X - ``X^T X`` (a the transposed view of a row-major b) or ``X X^T`` (b the transposed view of a
+    row-major a) - computed once per upper-triangle tile pair (``gram64``'s upper-tile split-K
+    launches, half the MFMA work of the full product) and mirrored, so the result is exactly
+    symmetric; None when the operands are not of that form."""
+    if not (a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32:
+        return None
+    if _is_gram(a, b):
+        g = gram64(b)
+    elif _is_gram(b, a):
+        g = gram64(a, rows=True)
+    else:
+        return None
+    u = torch.triu(g)
+    return (u + torch.triu(u, 1).t()).float()
+
+
+def gram64(x: torch.Tensor, exact: Optional[bool] = None, rows: bool = False) -> torch.Tensor:
     """Upper triangle (lower triangle zero) of the Gram matrix x^T x of a tall fp32 block as an
     fp64 [n, n] tensor - the CholeskyQR Gram. One 256-tile MFMA launch per group of K slices
     (``csrc/gemm_tiled.hip``: upper-triangle tiles only, split-K over ``HEAT_GRAM_KCHUNK`` = 4096
@@ -1224,10 +1242,15 @@ def gram64(x: torch.Tensor, exact: Optional[bool] = None) -> torch.Tensor:
     (``ha_sum_slices64``): the accumulation error of one fp32 sum over all 1.25e6 rows (~u sqrt(m) / 3
     = 4e-5 relative on the diagonal at m = 1.25e6) drops to ~u chunk / (3 sqrt(m)) = 7e-8. ``exact``: exact fp32
     products (``gemm_f32t``) instead of the fp16x3 split (``gemm_h3t``); default from
-    torch.get_float32_matmul_precision() ("highest" -> exact). Host / fp64: an fp64 GEMM."""
-    m, n = x.shape
+    torch.get_float32_matmul_precision() ("highest" -> exact). Host / fp64: an fp64 GEMM.
+    ``rows``: the Gram of the ROWS, x x^T (x [n, m] row-major, contraction along its columns)."""
+    if rows:
+        n, m = x.shape
+    else:
+        m, n = x.shape
     if not (x.is_cuda and use_native(x)) or x.dtype != torch.float32:
-        return torch.triu(x.double().T @ x.double())
+        xd = x.double()
+        return torch.triu(xd @ xd.T if rows else xd.T @ xd)
     out = torch.zeros((n, n), dtype=torch.float64, device=x.device)
     if m == 0 or n == 0:
         return out
@@ -1240,21 +1263,29 @@ def gram64(x: torch.Tensor, exact: Optional[bool] = None) -> torch.Tensor:
     P = torch.empty(group * n * n, dtype=torch.float32, device=x.device)
     pa = None
     if not exact:
-        pa = h3_planes(x.t(), 1)
+        pa = h3_planes(x, 1) if rows else h3_planes(x.t(), 1)
         if int(pa.flag.item()) != 0:
             pa = None
             exact = True
+    if exact and rows and (x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16):
+        x = x.contiguous()
     for k0 in range(0, m, group * kc):
         k1 = min(m, k0 + group * kc)
         slices = -(-(k1 - k0) // kc)
         if exact:
-            xs = x[k0:k1]
-            if xs.stride(1) != 1 or xs.stride(0) % 4 or xs.data_ptr() % 16 or n % 4:
-                xs = xs.contiguous()
-            rc = L.ha_gemm_f32t(_ptr(xs), _ptr(xs), _ptr(P), n, n, k1 - k0, xs.stride(0), xs.stride(0), n, 1, 1,
-                                1.0, 0, 1, slices, n * n, st)
+            if rows:   # A = x (row-major, k contiguous), B = x^T (n-major): columns k0..k1 of x
+                xs = x[:, k0:k1]
+                ok = xs.data_ptr() % 16 == 0 and (k1 - k0) % 4 == 0
+                rc = L.ha_gemm_f32t(_ptr(xs), _ptr(xs), _ptr(P), n, n, k1 - k0, xs.stride(0), xs.stride(0), n, 0, 0,
+                                    1.0, 0, 1, slices, n * n, st) if ok else _HA_UNSUPPORTED
+            else:
+                xs = x[k0:k1]
+                if xs.stride(1) != 1 or xs.stride(0) % 4 or xs.data_ptr() % 16 or n % 4:
+                    xs = xs.contiguous()
+                rc = L.ha_gemm_f32t(_ptr(xs), _ptr(xs), _ptr(P), n, n, k1 - k0, xs.stride(0), xs.stride(0), n, 1, 1,
+                                    1.0, 0, 1, slices, n * n, st)
             if rc == _HA_UNSUPPORTED:   # tiny / unaligned blocks: the 128-tile kernel, one slice
-                res = gemm_f32(xs.t(), xs)
+                res = gemm_f32(xs, xs.t()) if rows else gemm_f32(xs.t(), xs)
                 out += torch.triu(res.double())
                 continue
             check(rc, "ha_gemm_f32t")

@@ -217,3 +217,61 @@ def test_gemm_h3_split_k(m, k, n):
     c2 = c0.clone()
     ops.gemm_h3(a, b, out=c2, alpha=2.0, accumulate=True)
     assert torch.all((c2.double() - (c0.double() + 2 * ref)).abs() <= 8 * _bound(a, b) + 1e-5)
+
+
+@pytest.mark.parametrize("m,n", [(20000, 1024), (5003, 700), (3000, 513)])
+@pytest.mark.parametrize("form", ["tn", "nt"])
+@pytest.mark.parametrize("prec", ["highest", "high"])
+def test_gram_product_upper_tiles(m, n, form, prec):
+    """X^T X and X X^T of one device matrix: upper-triangle tiles + mirror, exactly symmetric, fp32
+    GEMM accuracy against fp64."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + n)
+    x = torch.randn(m, n, generator=g).to(dev)
+    if form == "nt":
+        x = x.t().contiguous()        # [n, m]: x x^T
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(prec)
+    try:
+        c = ops.gram_product(x.t(), x) if form == "tn" else ops.gram_product(x, x.t())
+    finally:
+        torch.set_float32_matmul_precision(old)
+    assert c is not None and c.dtype == torch.float32 and c.shape == (n, n)
+    xd = x.double()
+    ref = xd.t() @ xd if form == "tn" else xd @ xd.t()
+    a, b = (x.t(), x) if form == "tn" else (x, x.t())
+    assert torch.equal(c, c.t())
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
+
+
+def test_matmul_gram_and_cov_route_to_upper_tiles(gpu):
+    """ht.matmul(A.T, A) (split 0) and ht.cov reach the Gram path and match fp64."""
+    import numpy as np
+    import heat_amd as ht
+    from heat_amd.core.linalg import basics
+
+    rng = np.random.default_rng(1)
+    a = rng.normal(size=(6000, 600)).astype(np.float32)
+    A = ht.array(a, split=0, device="gpu")
+    calls = []
+    orig = basics.fgemm.__globals__.get("_GRAM_MIN_N")
+    import heat_amd.ops as _ops
+    real = _ops.gram_product
+
+    def spy(x, y):
+        r = real(x, y)
+        calls.append(r is not None)
+        return r
+
+    _ops.gram_product = spy
+    try:
+        G = ht.matmul(A.T, A).numpy()
+        C = ht.cov(ht.array(a.T, split=1, device="gpu")).numpy()
+    finally:
+        _ops.gram_product = real
+    assert orig is not None and any(calls)
+    ad = a.astype(np.float64)
+    assert np.allclose(G, ad.T @ ad, rtol=1e-4, atol=1e-2)
+    assert np.allclose(C, np.cov(ad.T), rtol=1e-4, atol=1e-5)
