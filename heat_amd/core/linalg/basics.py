@@ -135,10 +135,13 @@ def _library_better(M: int, N: int, K: int, exact: bool) -> bool:
     2048^3; the hand-written kernels win or tie from ~4 full waves of tiles (8192^3: 7.7 vs 7.2 ms
     exact, 3.3 ms fp16x3; 1.25e6 x 4096^2: 296 vs 283 ms exact without the library's 4 GB
     blocking) and on tiny-output, huge-K products through split-K (512^2 x 1e6: 3.8 vs 5.5 ms)."""
+    from ... import ops
+
+    ncu = ops.num_cus(torch.device("cuda", torch.cuda.current_device())) if torch.cuda.is_available() else 256
     tiles = -(-M // 256) * -(-N // 256)
-    if tiles <= 16 and K >= (1 << 18):
+    if tiles <= ncu // 16 and K >= (1 << 18):
         return False            # split-K on the hand-written kernel
-    return tiles < (1024 if exact else 256)
+    return tiles < (4 * ncu if exact else ncu)
 
 
 def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
@@ -160,12 +163,10 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
                 return g
             return out.add_(g) if accumulate else out.copy_(g)
     if _native_fp32(a, b) and _library_better(a.shape[0], b.shape[1], a.shape[1], not _split_gemm_ok(a, b)):
-        prev = torch.get_float32_matmul_precision()
-        torch.set_float32_matmul_precision("highest")   # exact fp32 products under any setting
-        try:
+        from ...ops import kernels as _kern
+
+        with _kern.exact_fp32_library():   # exact fp32 products under any setting
             r = _mm_blocked(a, b)
-        finally:
-            torch.set_float32_matmul_precision(prev)
         if alpha != 1.0:
             r = r * alpha
         if out is None:

@@ -4,8 +4,10 @@ tensors; also the numerics oracle of the tests).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import threading
 from typing import NamedTuple, Optional, Tuple
 
 import numpy as np
@@ -1592,18 +1594,31 @@ def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, tra
 _HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "blas")
 
 
+_PRECISION_LOCK = threading.RLock()
+
+
+@contextlib.contextmanager
+def exact_fp32_library():
+    """Library GEMMs inside run with exact fp32 products. torch's float32 matmul precision is
+    process-global, so the switch to "highest" and back is serialised under one lock (every
+    framework call site that changes it goes through here), and nothing changes when it already
+    is "highest"."""
+    with _PRECISION_LOCK:
+        prev = torch.get_float32_matmul_precision()
+        if prev == "highest":
+            yield
+            return
+        torch.set_float32_matmul_precision("highest")
+        try:
+            yield
+        finally:
+            torch.set_float32_matmul_precision(prev)
+
+
 def _exact_addmm_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: float) -> None:
-    """C += alpha A B through the library GEMM with exact fp32 products (precision "highest" for the
-    duration of the call)."""
-    prev = torch.get_float32_matmul_precision()
-    if prev == "highest":
+    """C += alpha A B through the library GEMM with exact fp32 products."""
+    with exact_fp32_library():
         C.addmm_(A, B, alpha=alpha)
-        return
-    torch.set_float32_matmul_precision("highest")
-    try:
-        C.addmm_(A, B, alpha=alpha)
-    finally:
-        torch.set_float32_matmul_precision(prev)
 
 
 def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpose: bool, native: bool, st,
