@@ -165,6 +165,11 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
     if _native_fp32(a, b) and _library_better(a.shape[0], b.shape[1], a.shape[1], not _split_gemm_ok(a, b)):
         from ...ops import kernels as _kern
 
+        # the 128 x 128-tile kernel with split-K fills the GPU where the 256-tile one cannot
+        r = _kern.gemm_f32_small(a, b, out=out, alpha=alpha, accumulate=accumulate)
+        if r is not None:
+            return r
+
         with _kern.exact_fp32_library():   # exact fp32 products under any setting
             r = _mm_blocked(a, b)
         if alpha != 1.0:

@@ -1,0 +1,217 @@
+// 128 x 128-tile exact fp32 GEMM with split-K: the products the 256 x 256 kernel
+// of gemm_tiled.hip cannot spread over the 256 CUs - 1024^3 .. 6144^3 (16 .. 576 tiles of 256^2:
+// a fraction of a wave, or 2.25 waves), and the short-K tall updates of the Householder QR
+// (C[1.25e6, 3840] -= V[1.25e6, 256] X[256, 3840]: K = 256 is 16 k-stages, which the 256-tile
+// kernel's 3-stage LDS-DMA prologue and 256 KB C epilogue per tile do not amortise). Before this
+// kernel those shapes went to hipBLASLt (profiles/gemm_small_r04.jsonl: 9x at 1024^3).
+//
+// Design: 4 waves, each a 64 x 64 quadrant (2 x 2 v_mfma_f32_32x32x2_f32 accumulators = 64
+// registers), 32-k stages double-buffered in LDS through registers (the next stage's global loads
+// are in flight during the current stage's 64 MFMAs per wave), two workgroups per CU (70.6 KB of
+// LDS each). The k order inside a stage is permuted - lane half h owns k = 16 h + s at MFMA step
+// s - so a row-major A fragment is four ds_read_b128 of its row. A: row-major [M][K] or k-major
+// [K][M]; B: k-major [K][N] or n-major [N][K]. split-K: grid.y = slices, slice y writes its
+// partial to C + y cslice (summed by ha_sum_slices32/64). XCD-aware tile order (blocks of one XCD
+// walk the column tiles of a row panel, which then stays in that XCD's L2).
+#include "common.h"
+
+namespace {
+
+constexpr int GB = 128, GK = 32;
+constexpr int A_LD = GK + 4;    // As[row][k]: 144-byte rows (conflict-free row-per-lane b128 reads)
+constexpr int B_LD = GB + 4;    // Bs[k][n]
+constexpr int A_SZ = GB * A_LD;
+constexpr int B_SZ = GK * B_LD;
+constexpr int ST_SZ = A_SZ + B_SZ;  // floats per stage
+
+__device__ __forceinline__ int64_t gs_xcd_remap(int64_t orig, int64_t nwg) {
+  const int64_t q = nwg / 8, r = nwg % 8, xcd = orig % 8, loc = orig / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+template <bool AK, bool BN>
+__global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A, const float* __restrict__ B,
+                                                    float* __restrict__ C, int64_t M, int64_t N, int64_t K,
+                                                    int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
+                                                    int64_t kps, int64_t cslice) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * ST_SZ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t tn = (N + GB - 1) / GB, tm = (M + GB - 1) / GB;
+  const int64_t bid = gs_xcd_remap(blockIdx.x, tm * tn);
+  const int64_t m0 = (bid / tn) * GB, n0 = (bid % tn) * GB;
+  const int64_t kb = (int64_t)blockIdx.y * kps;
+  const int64_t ke = K - kb < kps ? K : kb + kps;
+  C += (int64_t)blockIdx.y * cslice;
+
+  floatx4 ra[4], rb[4];
+  // piece p = tid + 256 i of a stage (1024 16-byte pieces per operand)
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + 256 * i;
+      if (!AK) {  // row-major: row p >> 3, k 4 (p & 7)
+        const int64_t gr = m0 + (p >> 3), gk = k0 + 4 * (p & 7);
+        const float* s = A + gr * lda + gk;
+        if (gr < M && gk + 4 <= ke) {
+          ra[i] = *reinterpret_cast<const floatx4*>(s);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ra[i][j] = (gr < M && gk + j < ke) ? s[j] : 0.f;
+        }
+      } else {    // k-major: k p >> 5, rows 4 (p & 31)
+        const int64_t gk = k0 + (p >> 5), gr = m0 + 4 * (p & 31);
+        const float* s = A + gk * lda + gr;
+        if (gk < ke && gr + 4 <= M) {
+          ra[i] = *reinterpret_cast<const floatx4*>(s);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ra[i][j] = (gk < ke && gr + j < M) ? s[j] : 0.f;
+        }
+      }
+      if (!BN) {  // k-major [K][N]: k p >> 5, columns 4 (p & 31)
+        const int64_t gk = k0 + (p >> 5), gc = n0 + 4 * (p & 31);
+        const float* s = B + gk * ldb + gc;
+        if (gk < ke && gc + 4 <= N) {
+          rb[i] = *reinterpret_cast<const floatx4*>(s);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rb[i][j] = (gk < ke && gc + j < N) ? s[j] : 0.f;
+        }
+      } else {    // n-major [N][K]: column p >> 3, k 4 (p & 7)
+        const int64_t gc = n0 + (p >> 3), gk = k0 + 4 * (p & 7);
+        const float* s = B + gc * ldb + gk;
+        if (gc < N && gk + 4 <= ke) {
+          rb[i] = *reinterpret_cast<const floatx4*>(s);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rb[i][j] = (gc < N && gk + j < ke) ? s[j] : 0.f;
+        }
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* As = sm + buf * ST_SZ;
+    float* Bs = As + A_SZ;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + 256 * i;
+      if (!AK) {
+        *reinterpret_cast<floatx4*>(As + (p >> 3) * A_LD + 4 * (p & 7)) = ra[i];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) As[(4 * (p & 31) + j) * A_LD + (p >> 5)] = ra[i][j];
+      }
+      if (!BN) {
+        *reinterpret_cast<floatx4*>(Bs + (p >> 5) * B_LD + 4 * (p & 31)) = rb[i];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Bs[(4 * (p & 7) + j) * B_LD + (p >> 3)] = rb[i][j];
+      }
+    }
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (floatx16)(0.f);
+  auto compute = [&](int buf) {
+    const float* As = sm + buf * ST_SZ;
+    const float* Bs = As + A_SZ;
+    floatx4 fa[2][4];
+    float fb[2][16];
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        fa[bm][q] = *reinterpret_cast<const floatx4*>(As + (wm * 64 + bm * 32 + r) * A_LD + 16 * h + 4 * q);
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) fb[bn][s] = Bs[(16 * h + s) * B_LD + wn * 64 + bn * 32 + r];
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[bm][s >> 2][s & 3], fb[bn][s], acc[bm][bn], 0, 0, 0);
+  };
+
+  const int64_t nk = (ke - kb + GK - 1) / GK;
+  if (nk > 0) {
+    gload(kb);
+    sstore(0);
+    __syncthreads();
+  }
+  for (int64_t t = 0; t < nk; ++t) {
+    if (t + 1 < nk) gload(kb + (t + 1) * GK);  // in flight during this stage's MFMAs
+    compute(t & 1);
+    if (t + 1 < nk) sstore((t + 1) & 1);
+    __syncthreads();
+  }
+  // epilogue: 32 x 32 C/D map - column r, rows (g & 3) + 8 (g >> 2) + 4 h
+  const bool full = m0 + GB <= M && n0 + GB <= N;
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm) {
+    const int64_t rb0 = m0 + wm * 64 + bm * 32 + 4 * h;
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+      const int64_t gc = n0 + wn * 64 + bn * 32 + r;
+      float* cp = C + rb0 * ldc + gc;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int dr = (g & 3) + 8 * (g >> 2);
+        if (full || (rb0 + dr < M && gc < N)) {
+          float v = alpha * acc[bm][bn][g];
+          if (beta) v += cp[dr * ldc];
+          cp[dr * ldc] = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// The k-slice length (a multiple of the 32-k stage) and the number of slices actually launched
+// for a request of `slices`: ceil(K / kps).
+HA_EXPORT int64_t ha_gemm_f32s_kps(int64_t K, int64_t slices) {
+  if (slices < 1) slices = 1;
+  int64_t kps = (K + slices - 1) / slices;
+  kps = (kps + GK - 1) / GK * GK;
+  return kps > 0 ? kps : GK;
+}
+HA_EXPORT int64_t ha_gemm_f32s_slices(int64_t K, int64_t slices) {
+  const int64_t kps = ha_gemm_f32s_kps(K, slices);
+  return K > 0 ? (K + kps - 1) / kps : 1;
+}
+
+// C[M, N] (row-major, ldc) = alpha A B (+ C if beta), exact fp32 products and accumulation.
+// a_kmajor: A element (m, k) at A[k lda + m] (else A[m lda + k]); b_nmajor: B element (k, n) at
+// B[n ldb + k] (else B[k ldb + n]). slices > 1: split-K, slice y -> C + y cslice (beta must be 0).
+// Requirements (else HA_UNSUPPORTED): 16-byte aligned A and B, lda and ldb multiples of 4.
+HA_EXPORT int ha_gemm_f32s(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                           int64_t ldb, int64_t ldc, int a_kmajor, int b_nmajor, float alpha, int beta, int64_t slices,
+                           int64_t cslice, void* stream) {
+  if (M <= 0 || N <= 0) return HA_OK;
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || (lda & 3) || (ldb & 3)) return HA_UNSUPPORTED;
+  if (slices > 1 && beta) return HA_BAD_ARG;
+  const int64_t tiles = ((M + GB - 1) / GB) * ((N + GB - 1) / GB);
+  const int64_t kps = ha_gemm_f32s_kps(K, slices);
+  const int64_t ns = ha_gemm_f32s_slices(K, slices);
+  if (tiles > 0x7fffffffLL || ns > 65535) return HA_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
+  if (!a_kmajor && !b_nmajor)
+    hipLaunchKernelGGL((gemm_f32s<false, false>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  else if (!a_kmajor && b_nmajor)
+    hipLaunchKernelGGL((gemm_f32s<false, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  else if (a_kmajor && !b_nmajor)
+    hipLaunchKernelGGL((gemm_f32s<true, false>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  else
+    hipLaunchKernelGGL((gemm_f32s<true, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  return ha_launch_status();
+}

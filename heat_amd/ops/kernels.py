@@ -17,7 +17,7 @@ import torch.nn.functional as F
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes", "gram_product", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
+           "split_planes", "gram_product", "gemm_f32_small", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "h3_planes", "H3Planes",
            "gemm_h3_planes", "gemm64", "cholesky_upper", "tri_inv_upper", "householder_qr",
            "householder_factor", "householder_apply", "householder_block", "vtc64", "gram64",
@@ -1124,6 +1124,57 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     return out
 
 
+_GEMM_SMALL = os.environ.get("HEAT_GEMM_SMALL", "1") != "0"
+
+
+def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
+                   accumulate: bool = False) -> Optional[torch.Tensor]:
+    """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on the 128 x 128-tile kernel
+    with split-K (``csrc/gemm_small.hip: gemm_f32s``): the products whose 256 x 256 tiles cannot
+    fill the GPU (1024^3 .. 6144^3) and short-K tall updates (the Householder rank-256 update).
+    Any row-/column-major operand views; None where the kernel does not apply (host tensors,
+    unaligned operands: the caller picks another GEMM)."""
+    if not (_GEMM_SMALL and a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32 \
+            or a.dim() != 2 or b.dim() != 2:
+        return None
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K:
+        raise ValueError("gemm_f32_small: inner dimensions differ: {} vs {}".format(K, b.shape[0]))
+    if out is not None and (out.shape != (M, N) or out.dtype != torch.float32 or (N > 1 and out.stride(1) != 1)):
+        raise ValueError("gemm_f32_small: out must be a row-major float32 [M, N] tensor")
+    if out is None:
+        out = torch.zeros((M, N), dtype=torch.float32, device=a.device) if accumulate else \
+            torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if M == 0 or N == 0:
+        return out
+    if K == 0:
+        return out if accumulate else out.zero_()
+    A, lda, a_km = _gemm_operand(a, 1)
+    B, ldb, b_nm = _gemm_operand(b, 1)
+    if A.data_ptr() % 16 or B.data_ptr() % 16 or lda % 4 or ldb % 4:
+        return None
+    L = lib()
+    st = ctypes.c_void_p(stream_ptr(a.device))
+    ldc = out.stride(0) if M > 1 else N
+    tiles = -(-M // 128) * -(-N // 128)
+    ncu = num_cus(a.device)
+    slices = 1
+    if tiles < 2 * ncu and K >= 512:   # two workgroups per CU: split K over the missing ones
+        slices = max(1, min(-(-2 * ncu // tiles), K // 256, _SPLITK_MAX_BYTES // (4 * M * N)))
+    if slices > 1:
+        used = L.ha_gemm_f32s_slices(K, slices)
+        P = torch.empty(used * M * N, dtype=torch.float32, device=a.device)
+        check(L.ha_gemm_f32s(_ptr(A), _ptr(B), _ptr(P), M, N, K, lda, ldb, N, int(a_km), int(b_nm), 1.0, 0, slices,
+                             M * N, st), "ha_gemm_f32s")
+        check(L.ha_sum_slices32(_ptr(P), used, M, N, M * N, _ptr(out), ldc, float(alpha), int(accumulate), st),
+              "ha_sum_slices32")
+        return out
+    check(L.ha_gemm_f32s(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(b_nm), float(alpha),
+                         int(accumulate), 1, 0, st), "ha_gemm_f32s")
+    return out
+
+
 class H3Planes(NamedTuple):
     """fp16 hi/lo planes of one GEMM operand in the K8-panel layout [Kp/8][Rp][8] (rows = the
     operand's non-contracted dimension, padded to 256; K padded to 16; zero padding), int32
@@ -1640,7 +1691,9 @@ def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpo
         gemm64(V, X, out=C, alpha=-1.0, beta=1.0)
         return
     X = X.to(C.dtype)
-    if C.stride(1) != 1 or _HH_UPDATE == "blas":
+    if _HH_UPDATE == "small" and C.stride(1) == 1 and gemm_f32_small(V, X, out=C, alpha=-1.0, accumulate=True) is not None:
+        pass
+    elif C.stride(1) != 1 or _HH_UPDATE == "blas":
         _exact_addmm_(C, V, X, -1.0)
     elif _HH_UPDATE == "h3" and gemm_h3(V, X, out=C, alpha=-1.0, accumulate=True) is not None:
         pass

@@ -275,3 +275,27 @@ def test_matmul_gram_and_cov_route_to_upper_tiles(gpu):
     ad = a.astype(np.float64)
     assert np.allclose(G, ad.T @ ad, rtol=1e-4, atol=1e-2)
     assert np.allclose(C, np.cov(ad.T), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 1024, 1024), (4099, 130, 65), (64, 4096, 64), (1, 7, 1),
+                                   (129, 1, 131), (2000, 33, 3), (5000, 256, 700), (128, 20000, 256)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+def test_gemm_f32_small_layouts(m, k, n, layout):
+    """128-tile split-K kernel: every operand layout, edges, split-K, alpha / accumulate."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m * 5 + k * 3 + n)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    c = ops.gemm_f32_small(A, B)
+    assert c is not None
+    ref = a.double() @ b.double()
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
+    base = torch.randn(m, n, generator=g).to(dev)
+    out = base.clone()
+    ops.gemm_f32_small(A, B, out=out, alpha=-0.5, accumulate=True)
+    ref2 = base.double() - 0.5 * ref
+    assert torch.all((out.double() - ref2).abs() <= _bound(a, b) + 1e-6 * base.abs().double())
