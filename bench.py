@@ -55,7 +55,8 @@ def parse():
                    help="Y-block circulation of the cdist/knn workloads: neighbour ring or all-peer direct posts")
     p.add_argument("--comm-ab", type=int, default=1,
                    help="world > 1: also time the k-means all-reduce payload on every comm path after the timed "
-                        "loop (0 = skip); bounded by a watchdog so a stuck path cannot hold the result back")
+                        "loop (0 = skip), in a separate child job so a failing path cannot cost the result")
+    p.add_argument("--comm-ab-child", default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -144,6 +145,9 @@ def main():
     if rc >= 0:
         sys.exit(rc)
     apply_comm_env(args)
+    if args.comm_ab_child:
+        comm_ab_child(args.comm_ab_child)
+        return
     import heat_amd as ht
     from heat_amd.core.communication import MPI_WORLD
 
@@ -308,35 +312,65 @@ def main():
            "config": cfg, "extra": extra}
     if comm.size > 1 and args.comm_ab:
         # after the timed loop and its result: the all-reduce of the k-means payload on every
-        # path, under a watchdog (a path that hangs on this node must not cost the measurement)
+        # path, in a SEPARATE job (one child per rank, its own rendezvous): a path that crashes or
+        # hangs on this node costs that record, never the measurement above
         payload = (args.k * (args.f or 64) + args.k) * 8
-        dog = Watchdog(float(os.environ.get("HEAT_BENCH_AB_TIMEOUT", "120")), comm.rank, out)
-        extra["comm_ab"] = comm_ab(comm, dev, [8, payload])
-        dog.cancel()
+        extra["comm_ab"] = comm_ab_isolated(comm, [8, payload])
     if comm.rank == 0:
         print(json.dumps(out), flush=True)
 
 
-class Watchdog:
-    """Prints ``out`` (rank 0, marked) and ends the process if the guarded section has not
-    finished within ``seconds``."""
+def comm_ab_isolated(comm, sizes) -> dict:
+    """Run :func:`comm_ab` in a child job of the same ranks (every rank starts one child with the
+    launcher's RANK / WORLD_SIZE / LOCAL_RANK and a fresh MASTER_PORT from rank 0), bounded by
+    ``HEAT_BENCH_AB_TIMEOUT`` seconds; rank 0's child prints the record."""
+    import socket
+    import subprocess
 
-    def __init__(self, seconds: float, rank: int, out: dict):
-        import threading
+    import heat_amd as ht
 
-        self.rank, self.out = rank, out
-        self.timer = threading.Timer(seconds, self.fire)
-        self.timer.daemon = True
-        self.timer.start()
+    port = None
+    if comm.rank == 0:
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+    port = comm.bcast(port, root=0)
+    # a fresh rendezvous: not torchrun's agent store (TORCHELASTIC_USE_AGENT_STORE would make the
+    # child connect to the agent's store on the new port, where nobody listens)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(comm.rank), WORLD_SIZE=str(comm.size))
+    env.setdefault("LOCAL_RANK", str(comm.rank))
+    env.setdefault("LOCAL_WORLD_SIZE", str(comm.size))
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(comm.size), "--comm-ab-child",
+           ",".join(str(x) for x in sizes)]
+    res = {}
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True,
+                           timeout=float(os.environ.get("HEAT_BENCH_AB_TIMEOUT", "180")))
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if lines:
+            res = json.loads(lines[-1])
+        if r.returncode != 0:
+            res["error"] = "child exited with {}: {}".format(r.returncode, r.stderr[-300:])
+    except subprocess.TimeoutExpired:
+        res = {"error": "timed out"}
+    ok = comm.allreduce(int("error" not in res), ht.MPI.MIN)
+    if not ok and "error" not in res:
+        res["error"] = "failed on another rank"
+    return res
 
-    def fire(self):
-        if self.rank == 0:
-            self.out["extra"]["comm_ab"] = {"error": "timed out"}
-            print(json.dumps(self.out), flush=True)
-        os._exit(0)
 
-    def cancel(self):
-        self.timer.cancel()
+def comm_ab_child(sizes) -> None:
+    """Entry point of the isolated comm A/B job (``--comm-ab-child``)."""
+    import heat_amd as ht
+    from heat_amd.core.communication import MPI_WORLD
+
+    if torch.cuda.is_available():
+        ht.use_device("gpu")
+    res = comm_ab(MPI_WORLD, None, [int(x) for x in sizes.split(",")])
+    if MPI_WORLD.rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 def comm_ab(comm, dev, sizes) -> dict:

@@ -277,8 +277,9 @@ def test_matmul_gram_and_cov_route_to_upper_tiles(gpu):
     assert np.allclose(C, np.cov(ad.T), rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 1024, 1024), (4099, 130, 65), (64, 4096, 64), (1, 7, 1),
-                                   (129, 1, 131), (2000, 33, 3), (5000, 256, 700), (128, 20000, 256)])
+@pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 1024, 1024), (4099, 132, 68), (64, 4096, 64), (1, 7, 1),
+                                   (132, 4, 136), (2000, 36, 4), (5000, 256, 700), (128, 20000, 256), (300, 260, 132),
+                                   (4100, 128, 100)])
 @pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
 def test_gemm_f32_small_layouts(m, k, n, layout):
     """128-tile split-K kernel: every operand layout, edges, split-K, alpha / accumulate."""
@@ -291,6 +292,11 @@ def test_gemm_f32_small_layouts(m, k, n, layout):
     A = a if layout[0] == "n" else a.t().contiguous().t()
     B = b if layout[1] == "n" else b.t().contiguous().t()
     c = ops.gemm_f32_small(A, B)
+    lda = A.stride(0) if A.stride(1) == 1 else A.stride(1)
+    ldb = B.stride(0) if B.stride(1) == 1 else B.stride(1)
+    if lda % 4 or ldb % 4:
+        assert c is None      # 16-byte loads need 4-float leading dimensions: the caller picks another GEMM
+        return
     assert c is not None
     ref = a.double() @ b.double()
     assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()

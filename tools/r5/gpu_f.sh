@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 cd "$ROOT"
 export TMPDIR=/tmp
 timeout -k 10 60 ./tools/probes/mfma4x4_probe > "$OUT/probe.txt" 2>&1 && \
-timeout -k 10 400 python -u -m pytest tests/test_gpu_gemm.py -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > "$OUT/tests_gemm.txt" 2>&1 && \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_gemm.py -q --timeout 200 --timeout-method thread -p no:cacheprovider > "$OUT/tests_gemm.txt" 2>&1 && \
 timeout -k 10 400 python -u tools/microbench/gemm_small.py > "$OUT/gemm_small.jsonl" 2>&1 && \
 timeout -k 10 300 python -u -m benchmarks.linalg.run --ops matmul,qr > "$OUT/linalg_blas.txt" 2>&1 && \
 HEAT_HH_UPDATE=small timeout -k 10 300 python -u -m benchmarks.linalg.run --ops qr > "$OUT/linalg_small.txt" 2>&1
