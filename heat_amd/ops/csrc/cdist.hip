@@ -11,6 +11,7 @@
 // m x n x f intermediate (the reference's _manhattan_fast materialises one).
 #include "common.h"
 
+#include <cmath>
 #include <cstdlib>
 
 namespace {
@@ -201,7 +202,10 @@ __global__ __launch_bounds__(256) void cdist_vk(const float* __restrict__ X, int
 // v_sub + v_add with the abs modifier (no abs on packed ops).
 constexpr int VB = 128, VK = 32, VS = VB + 4;  // tile, features per chunk, LDS row stride
 
-template <int OP>
+// SYM (Y = X, m = n): only the tiles on or above the diagonal are launched (row-major order of the
+// upper triangle), and an off-diagonal tile is also stored mirrored at (col, row): every distance
+// pair is computed once (the reference's Y = None path, heat/spatial/distance.py:237, 265-362).
+template <int OP, bool SYM>
 __global__ __launch_bounds__(256, 2) void cdist_vx(const float* __restrict__ X, int64_t m, const float* __restrict__ Y,
                                                    int64_t n, int f, int64_t ldx, int64_t ldy, float* __restrict__ C,
                                                    int64_t ldc, float scale, int64_t per_xcd, int vec_out) {
@@ -209,10 +213,24 @@ __global__ __launch_bounds__(256, 2) void cdist_vx(const float* __restrict__ X, 
   __shared__ __attribute__((aligned(16))) float sy[VK * VS];
   const int tid = threadIdx.x;
   const int64_t tiles_n = (n + VB - 1) / VB;
-  const int64_t tiles = ((m + VB - 1) / VB) * tiles_n;
+  const int64_t tiles = SYM ? tiles_n * (tiles_n + 1) / 2 : ((m + VB - 1) / VB) * tiles_n;
   const int64_t t = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
   if (t >= tiles) return;
-  const int64_t row0 = (t / tiles_n) * VB, col0 = (t % tiles_n) * VB;
+  int64_t row0, col0;
+  if (SYM) {
+    // t -> (i, j >= i): row i holds tiles_n - i tiles; invert the prefix sums with the quadratic
+    // formula, then correct the rounding
+    const double T = (double)tiles_n;
+    int64_t i = (int64_t)((2.0 * T + 1.0 - sqrt((2.0 * T + 1.0) * (2.0 * T + 1.0) - 8.0 * (double)t)) / 2.0);
+    auto first = [&](int64_t r) { return r * tiles_n - r * (r - 1) / 2; };
+    while (i > 0 && first(i) > t) --i;
+    while (first(i + 1) <= t) ++i;
+    row0 = i * VB;
+    col0 = (i + (t - first(i))) * VB;
+  } else {
+    row0 = (t / tiles_n) * VB;
+    col0 = (t % tiles_n) * VB;
+  }
   const int tr = tid >> 4, tc = tid & 15;
   // staging role: feature column sc, 4-row groups sq + 8 u (u = 0..3) of the 32 groups
   const int sc = tid & 31, sq = tid >> 5;
@@ -278,6 +296,33 @@ __global__ __launch_bounds__(256, 2) void cdist_vx(const float* __restrict__ X, 
     if (OP == 3) return __expf(-v * scale);
     return v;
   };
+  if (SYM && row0 != col0) {
+    // the mirrored tile (col block, row block): thread's column 4 tc + j + 64 h becomes a row
+    // holding its 8 values at columns 4 tr + {0..3} and 64 + 4 tr + {0..3}
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t row = col0 + 64 * h + 4 * tc + j;
+        if (row >= n) continue;
+        float o[8];
+#pragma unroll
+        for (int a = 0; a < 8; ++a) o[a] = fin(acc[a][2 * h + (j >> 1)][j & 1]);
+        float* rp = C + row * ldc + row0 + 4 * tr;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int64_t col = row0 + 4 * tr + 64 * half;
+          if (vec_out && col + 3 < m) {
+            __builtin_nontemporal_store((floatx4){o[4 * half], o[4 * half + 1], o[4 * half + 2], o[4 * half + 3]},
+                                        reinterpret_cast<floatx4*>(rp + 64 * half));
+          } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (col + v < m) rp[64 * half + v] = o[4 * half + v];
+          }
+        }
+      }
+  }
   if (vec_out && row0 + VB <= m && col0 + VB <= n) {
     // whole tile (wave-uniform): 16 unguarded 16-byte stores per thread, no per-element branches
     // (the guarded form below costs ~400 VALU per thread, a quarter of the kernel's VALU work)
@@ -324,23 +369,35 @@ HA_EXPORT int ha_cdist(const float* X, int64_t m, const float* Y, int64_t n, int
   if (m <= 0 || n <= 0) return HA_OK;
   hipStream_t s = (hipStream_t)stream;
   static const bool vk64 = [] { const char* e = getenv("HEAT_CDIST_VK64"); return e && atoi(e) != 0; }();
+  // mode bit 8: symmetric (Y is X, m == n): compute-once upper-triangle tiles, exact kernels only
+  const bool sym = (mode & 256) != 0;
+  mode &= 255;
+  if (sym && (mode < 3 || X != Y || m != n || ldx != ldy)) return HA_BAD_ARG;
   // cdist_vx addresses a 128-row tile with 32-bit byte offsets
   const bool fits = (int64_t)VB * (ldx > ldy ? ldx : ldy) * 4 < 0x7fffffffLL;
-  if (mode >= 3 && !vk64 && fits) {
-    const int64_t tiles = ((m + VB - 1) / VB) * ((n + VB - 1) / VB);
+  if (mode >= 3 && (!vk64 || sym) && fits) {
+    const int64_t tn = (n + VB - 1) / VB;
+    const int64_t tiles = sym ? tn * (tn + 1) / 2 : ((m + VB - 1) / VB) * tn;
     const int64_t per_xcd = (tiles + 7) / 8;
     if (per_xcd * 8 > 0x7fffffffLL) return HA_UNSUPPORTED;
     const int vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
     const dim3 g((unsigned)(per_xcd * 8)), b(256);
+#define HA_VX(OPV)                                                                                            \
+  if (sym)                                                                                                   \
+    hipLaunchKernelGGL((cdist_vx<OPV, true>), g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); \
+  else                                                                                                       \
+    hipLaunchKernelGGL((cdist_vx<OPV, false>), g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec);
     switch (mode) {
-      case 3: hipLaunchKernelGGL(cdist_vx<0>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
-      case 4: hipLaunchKernelGGL(cdist_vx<1>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
-      case 5: hipLaunchKernelGGL(cdist_vx<2>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
-      case 6: hipLaunchKernelGGL(cdist_vx<3>, g, b, 0, s, X, m, Y, n, f, ldx, ldy, C, ldc, scale, per_xcd, vec); break;
+      case 3: HA_VX(0) break;
+      case 4: HA_VX(1) break;
+      case 5: HA_VX(2) break;
+      case 6: HA_VX(3) break;
       default: return HA_BAD_ARG;
     }
+#undef HA_VX
     return ha_launch_status();
   }
+  if (sym) return HA_UNSUPPORTED;
   if (mode >= 3) {  // round-4 64 x 64 kernel (HEAT_CDIST_VK64=1, A/B only)
     const int64_t tiles = ((m + LB - 1) / LB) * ((n + LB - 1) / LB);
     const int64_t per_xcd = (tiles + 7) / 8;

@@ -418,6 +418,11 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
   floatx4 uacc[4][2];
 #pragma unroll
   for (int b = 0; b < 4; ++b) uacc[b][0] = uacc[b][1] = (floatx4)(0.f);
+  floatx4 u4[KP <= 8 ? KP / 4 : 1][4];
+#pragma unroll
+  for (int g = 0; g < (KP <= 8 ? KP / 4 : 1); ++g)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) u4[g][s4] = (floatx4)(0.f);
   float ucnt = 0.f;
   floatx4 buf[16];
   typedef const floatx4 __attribute__((address_space(1)))* gptr;
@@ -469,17 +474,40 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
     }
     if (UPDATE) {
       lab[lane] = bi;
-      const int kq = lane >> 4, c16 = lane & 15;
+      if constexpr (KP <= 8) {
+        // onehot^T X on v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4, one row each; layout probed
+        // by tools/probes/mfma4x4_probe.hip: A_b[m] / B_b[n] in lane 4 b + m / 4 b + n, D reg m of
+        // lane 4 b + n): block b = (feature quad fq = b >> 2, row rr = b & 3), so one MFMA covers 4
+        // rows x 16 features x 4 clusters - no padding rows, half (k = 8) or a quarter (k <= 4)
+        // of the 16x16x4 form's matrix-core cycles. The 4 row blocks' partials are summed at the end.
+        const int q = lane & 3, rr = (lane >> 2) & 3, fq = lane >> 4;
+        const float* xb = tile + rr * LD + 4 * fq + q;
 #pragma unroll 4
-      for (int r0 = 0; r0 < 64; r0 += 8) {
+        for (int r0 = 0; r0 < 64; r0 += 4) {
+          const int rl = lab[r0 + rr];
+          float a[KP / 4];
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          const int r = r0 + 4 * g + kq;
-          const float a = lab[r] == c16 ? 1.f : 0.f;
-          const float* xrow = tile + r * LD + c16;
+          for (int g = 0; g < KP / 4; ++g) a[g] = rl == 4 * g + q ? 1.f : 0.f;
 #pragma unroll
-          for (int b = 0; b < 4; ++b)
-            uacc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xrow[16 * b], uacc[b][g], 0, 0, 0);
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const float xv = xb[r0 * LD + 16 * s4];
+#pragma unroll
+            for (int g = 0; g < KP / 4; ++g) u4[g][s4] = __builtin_amdgcn_mfma_f32_4x4x1f32(a[g], xv, u4[g][s4], 0, 0, 0);
+          }
+        }
+      } else {
+        const int kq = lane >> 4, c16 = lane & 15;
+#pragma unroll 4
+        for (int r0 = 0; r0 < 64; r0 += 8) {
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const int r = r0 + 4 * g + kq;
+            const float a = lab[r] == c16 ? 1.f : 0.f;
+            const float* xrow = tile + r * LD + c16;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+              uacc[b][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xrow[16 * b], uacc[b][g], 0, 0, 0);
+          }
         }
       }
 #pragma unroll
@@ -490,12 +518,30 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
     }
   }
   if (UPDATE) {
+    if constexpr (KP <= 8) {
+      // sum the 4 row blocks (lane bits 2-3), then lanes of row block 0 write cluster 4 g + m,
+      // feature 16 s + 4 fq + q
+      const int q = lane & 3, rr = (lane >> 2) & 3, fq = lane >> 4;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+      for (int g = 0; g < KP / 4; ++g)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 4 * (lane >> 4) + i;
-        if (c < KP) sums_part[((int64_t)blockIdx.x * KP + c) * KS_FMAX + b * 16 + (lane & 15)] = uacc[b][0][i] + uacc[b][1][i];
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            float v = u4[g][s4][m];
+            v += __shfl_xor(v, 4, 64);
+            v += __shfl_xor(v, 8, 64);
+            if (rr == 0)
+              sums_part[((int64_t)blockIdx.x * KP + 4 * g + m) * KS_FMAX + 16 * s4 + 4 * fq + q] = v;
+          }
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 4 * (lane >> 4) + i;
+          if (c < KP) sums_part[((int64_t)blockIdx.x * KP + c) * KS_FMAX + b * 16 + (lane & 15)] = uacc[b][0][i] + uacc[b][1][i];
+        }
       }
     }
     if (lane < KP) counts_part[(int64_t)blockIdx.x * KP + lane] = ucnt;
@@ -551,11 +597,13 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
   int64_t done = 0;
   if (mode == KS_ROW4 && f == KS_FMAX) {
     const int64_t full = n / KS_ROWS;
-    // HEAT_KS_VARIANT: "wave" (one-wave workgroups, 64-row tiles), "a1" / "a2" (two-wave
-    // workgroups, 128-row tiles, one / two tiles of loads in flight)
+    // HEAT_KS_VARIANT: "wave" (default: one-wave workgroups, 64-row tiles), "a1" / "a2" (two-wave
+    // workgroups, 128-row tiles, one / two tiles of loads in flight). Measured on one box
+    // (smallk_ab_r05.jsonl), n = 12.5M, f = 64, fused pass: wave 0.734 / 0.978 / 0.611 ms at
+    // k = 8 / 16 / 3 vs a1 0.767 / 1.018 / 0.654 and a2 0.780 / 1.048 / 0.663.
     static const int variant = [] {
       const char* e = getenv("HEAT_KS_VARIANT");
-      return !e ? 1 : e[0] == 'w' ? 0 : e[1] == '2' ? 2 : 1;
+      return !e ? 0 : e[0] == 'w' ? 0 : e[1] == '2' ? 2 : 1;
     }();
     if (variant == 0 && n / 64 > 0) {
       const int64_t full64 = n / 64;

@@ -595,14 +595,17 @@ def _cdist_h3(px: PackedRows, py: PackedRows, mode: int, scale: float, C: torch.
 
 def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: float = 1.0,
           out: Optional[torch.Tensor] = None, exact: bool = False, precision: str = "f16x3",
-          packed_x: Optional[PackedRows] = None, packed_y: Optional[PackedRows] = None) -> torch.Tensor:
+          packed_x: Optional[PackedRows] = None, packed_y: Optional[PackedRows] = None,
+          symmetric: bool = False) -> torch.Tensor:
     """Pairwise distances between the rows of X [m, f] and Y [n, f] as an [m, n] float32 matrix.
 
     Device tensors, L2 family with ``exact=False`` (quadratic expansion, fused norm/clamp/
     sqrt|exp epilogue): ``precision="f16x3"`` -> 3-term fp16 split on the FP16 matrix cores
     (fp32-GEMM accuracy; ``packed_x/packed_y`` from :func:`cdist_pack` skip the packing),
     ``"fp32"`` -> f32-input MFMA kernel. ``exact=True`` (and manhattan) -> VALU tile kernel on the
-    differences (no cancellation for near-identical points). No m x n x f intermediate."""
+    differences (no cancellation for near-identical points). No m x n x f intermediate.
+    ``symmetric`` (Y is X, difference kernels): only the tiles on or above the diagonal are
+    computed, each off-diagonal tile stored twice (the result is exactly symmetric)."""
     m, f = X.shape
     n = Y.shape[0]
     if metric not in _CDIST_MODES:
@@ -621,12 +624,21 @@ def cdist(X: torch.Tensor, Y: torch.Tensor, metric: str = "euclidean", sigma: fl
             Ya = _rows_f32_aligned(Y.to(X.device))
         else:
             Xa = X if X.stride(-1) == 1 else X.contiguous()
-            Ya = Y.to(X.device)
-            Ya = Ya if Ya.stride(-1) == 1 else Ya.contiguous()
+            if Y is X:
+                Ya = Xa
+            else:
+                Ya = Y.to(X.device)
+                Ya = Ya if Ya.stride(-1) == 1 else Ya.contiguous()
         C = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=X.device)
+        sym = symmetric and mode >= 3 and Y is X and Xa is Ya and m == n
         if m and n:
             rc = L.ha_cdist(_ptr(Xa), m, _ptr(Ya), n, Xa.shape[1], Xa.stride(0), Ya.stride(0), _ptr(C), C.stride(0),
-                            mode, ctypes.c_float(1.0 / (2.0 * sigma * sigma)), ctypes.c_void_p(stream_ptr(X.device)))
+                            mode | (256 if sym else 0), ctypes.c_float(1.0 / (2.0 * sigma * sigma)),
+                            ctypes.c_void_p(stream_ptr(X.device)))
+            if sym and rc == _HA_UNSUPPORTED:
+                rc = L.ha_cdist(_ptr(Xa), m, _ptr(Ya), n, Xa.shape[1], Xa.stride(0), Ya.stride(0), _ptr(C),
+                                C.stride(0), mode, ctypes.c_float(1.0 / (2.0 * sigma * sigma)),
+                                ctypes.c_void_p(stream_ptr(X.device)))
             check(rc, "ha_cdist")
         return C
     Xf = X if X.is_floating_point() else X.float()

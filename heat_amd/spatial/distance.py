@@ -83,7 +83,9 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
         return _dist_callable(X, Y, metric)
 
     def _local(metric, x, y, sigma, out=None):
-        return ops.cdist(x, y, metric, sigma=sigma, out=out, exact=exact)
+        # the same block on both sides (Y = None on one rank, or a rank's diagonal block): the
+        # difference kernels compute each distance pair once and mirror it
+        return ops.cdist(x, y, metric, sigma=sigma, out=out, exact=exact, symmetric=x is y)
 
     if not isinstance(X, DNDarray):
         raise TypeError("X must be a DNDarray")
@@ -105,7 +107,7 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
         raise NotImplementedError("Datatype {} currently not supported as input".format(dtype))
     tt = dtype.torch_type()
     x = X.larray.to(tt)
-    y = Y.larray.to(tt)
+    y = x if symmetric else Y.larray.to(tt)
     m, n = X.gshape[0], Y.gshape[0]
     comm = X.comm
     dx, dy = X.is_distributed(), Y.is_distributed()
@@ -119,7 +121,10 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
         return DNDarray(_local(metric, x, y, sigma).to(tt), (m, n), dtype, 1, X.device, comm, Y.balanced)
     counts, displs = Y.counts_displs()
     ybytes = n * Y.gshape[1] * y.element_size()
-    if symmetric and ybytes > _allgather_bytes():
+    if symmetric and (exact or metric == "manhattan" or ybytes > _allgather_bytes()):
+        # compute-once: the VALU difference kernels are compute-bound, so every off-diagonal tile
+        # pair is computed by one rank and mirrored; the MFMA expansion kernels are store-bound and
+        # all-gather below 2 GB
         out = torch.empty((x.shape[0], n), dtype=tt, device=x.device)
         _symmetric_half_ring(x, out, counts, displs, comm, lambda a, b: _local(metric, a, b, sigma).to(tt))
         return DNDarray(out, (m, n), dtype, 0, X.device, comm, X.balanced)
@@ -151,50 +156,69 @@ def _allgather_bytes() -> int:
 
 
 def _symmetric_half_ring(x: torch.Tensor, out: torch.Tensor, counts, displs, comm, tile) -> None:
-    """``cdist(X)`` with X split 0 on p ranks in ceil((p-1)/2) + 1 steps instead of p (reference
-    ``spatial/distance.py:237, 265-362``): d(X_r, X_q) = d(X_q, X_r)^T, so every off-diagonal tile
-    pair is computed ONCE. At step s every rank receives the block of rank r - s, computes the
-    tile (r, r - s), keeps it and sends its transpose back to r - s, which stores it as its tile
-    (r - s, r); for even p the last step (partners r and r + p/2) is computed by the lower half
-    only. Per step: one block exchange and one tile exchange, each a batched send/receive pair."""
+    """``cdist(X)`` with X split 0 on p ranks: every off-diagonal tile pair computed ONCE (reference
+    ``spatial/distance.py:237, 265-362``: d(X_r, X_q) = d(X_q, X_r)^T). Rank r computes its diagonal
+    tile and the tiles (r, r - s) for s = 1 .. floor(p / 2) (for even p the pair r, r + p/2 is
+    computed by the lower half only), and receives the mirrored tiles (r, r + s) from its partners.
+
+    Overlap (round 5): the floor(p/2) block exchanges are posted at once up front (every rank
+    sends its own block to r + 1 .. r + p/2 - all links of the node busy), the diagonal tile is
+    computed while they fly; then each received block's tile is computed and its transpose posted
+    back (paired with the receive of the mirrored tile from r + s) while the next tile computes.
+    Nothing is waited for until the end."""
     import torch.distributed as dist
 
     from ..parallel import staging as _SD
 
     p, r = comm.size, comm.rank
-    out[:, displs[r]: displs[r] + counts[r]] = tile(x, x)
     rest = tuple(x.shape[1:])
     xs = x.contiguous()
+    half = p // 2
+    even = p % 2 == 0
 
-    def exchange(send, dst, recv_shape, src):
-        recv = None if src is None else torch.empty(recv_shape, dtype=xs.dtype, device=xs.device)
-        ops = []
-        if send is not None:
-            ops.append(dist.P2POp(dist.isend, send.contiguous(), comm._g(dst), comm.group))
-        if src is not None:
-            ops.append(dist.P2POp(dist.irecv, recv, comm._g(src), comm.group))
-        for w in _SD.batch_isend_irecv(ops):
-            w.wait()
-        return recv
+    def computes(s_):  # does rank r compute the pair (r, r - s_)?
+        return not (even and s_ == half) or r < half
 
-    for s_ in range(1, p // 2 + 1):
+    # phase 1: every block exchange at once
+    ops, blocks = [], {}
+    for s_ in range(1, half + 1):
         dst, src = (r + s_) % p, (r - s_) % p
-        if p % 2 == 0 and s_ == p // 2:
-            q = dst  # == src: partners r and r + p/2
-            if r < p // 2:   # computes the pair's tile
-                blk = exchange(None, None, (counts[q],) + rest, q)
-                t = tile(xs, blk)
-                out[:, displs[q]: displs[q] + counts[q]] = t
-                exchange(t.t(), q, None, None)
-            else:            # sends its block, receives the mirrored tile
-                exchange(xs, q, None, None)
-                got = exchange(None, None, (counts[r], counts[q]), q)
-                out[:, displs[q]: displs[q] + counts[q]] = got
+        if even and s_ == half:
+            if r < half:
+                blocks[s_] = torch.empty((counts[src],) + rest, dtype=xs.dtype, device=xs.device)
+                ops.append(dist.P2POp(dist.irecv, blocks[s_], comm._g(src), comm.group))
+            else:
+                ops.append(dist.P2POp(dist.isend, xs, comm._g(dst), comm.group))
             continue
-        blk = exchange(xs, dst, (counts[src],) + rest, src)
-        t = tile(xs, blk)
-        out[:, displs[src]: displs[src] + counts[src]] = t
-        got = exchange(t.t(), src, (counts[r], counts[dst]), dst)
+        blocks[s_] = torch.empty((counts[src],) + rest, dtype=xs.dtype, device=xs.device)
+        ops.append(dist.P2POp(dist.isend, xs, comm._g(dst), comm.group))
+        ops.append(dist.P2POp(dist.irecv, blocks[s_], comm._g(src), comm.group))
+    works = _SD.batch_isend_irecv(ops) if ops else []
+    out[:, displs[r]: displs[r] + counts[r]] = tile(xs, xs)    # overlaps the block transfers
+    for w in works:
+        w.wait()
+    # phase 2: tiles in step order, each transpose posted back with the mirrored tile's receive
+    pending, mirrors = [], []
+    for s_ in range(1, half + 1):
+        dst, src = (r + s_) % p, (r - s_) % p
+        tops = []
+        if computes(s_):
+            t = tile(xs, blocks.pop(s_))
+            out[:, displs[src]: displs[src] + counts[src]] = t
+            tt = t.t().contiguous()
+            tops.append(dist.P2POp(dist.isend, tt, comm._g(src), comm.group))
+            pending.append(tt)
+        if not (even and s_ == half and r < half):
+            got = torch.empty((counts[r], counts[dst]), dtype=xs.dtype, device=xs.device)
+            tops.append(dist.P2POp(dist.irecv, got, comm._g(dst), comm.group))
+            mirrors.append((dst, got))
+        works = _SD.batch_isend_irecv(tops)
+        pending.append(works)
+    for item in pending:
+        if isinstance(item, list):
+            for w in item:
+                w.wait()
+    for dst, got in mirrors:
         out[:, displs[dst]: displs[dst] + counts[dst]] = got
 
 

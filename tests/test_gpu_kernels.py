@@ -1019,3 +1019,24 @@ def test_knn_certified_one_term(f):
     clear = (torch.sort(d, dim=1).values[:, k] - rd[:, -1]) > 1e-4 * rd[:, -1].clamp(min=1)
     same = (torch.sort(idx[sel], 1).values == torch.sort(ri, 1).values).all(1)
     assert bool(same[clear].all()), int((~same[clear]).sum())
+
+
+@pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian", "manhattan"])
+@pytest.mark.parametrize("n,f", [(1000, 18), (129, 3), (257, 40), (4000, 64), (1, 5)])
+def test_cdist_symmetric_compute_once(metric, n, f):
+    """Y is X on the difference kernels: upper-triangle tiles + mirrored stores give the same
+    matrix as the full launch, exactly symmetric, with an exact zero diagonal."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + f)
+    X = torch.rand(n, f, generator=g).to(dev)
+    full = ops.cdist(X, X.clone(), metric, sigma=1.5, exact=True)
+    sym = ops.cdist(X, X, metric, sigma=1.5, exact=True, symmetric=True)
+    assert torch.equal(sym, sym.t())
+    assert torch.allclose(sym, full, rtol=1e-6, atol=1e-6)
+    if metric != "gaussian":
+        assert torch.all(torch.diagonal(sym) == 0)
+    big = torch.full((n, n + 5), -1.0, device=dev)
+    ops.cdist(X, X, metric, sigma=1.5, exact=True, symmetric=True, out=big[:, :n])
+    assert torch.equal(big[:, :n], sym) and torch.all(big[:, n:] == -1.0)
