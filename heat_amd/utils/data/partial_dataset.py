@@ -278,6 +278,9 @@ class PartialH5DataLoaderIter:
 
     def __next__(self):
         if self._num_yielded >= self.length:
+            # every batch of the epoch was yielded: the loader only has its end marker and the
+            # pre-read of the next epoch's first window left (both fit), so it is not abandoned
+            self.dataset._epoch_done = True
             raise StopIteration
         items = self._carry
         while len(items) < self.batch_size:
