@@ -1081,7 +1081,7 @@ _HA_UNSUPPORTED = 2
 
 
 def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
-             accumulate: bool = False, alpha: float = 1.0) -> torch.Tensor:
+             accumulate: bool = False, alpha: float = 1.0, slices: Optional[int] = None) -> torch.Tensor:
     """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on the f32-input matrix cores:
     fp32 products and accumulation in k order like any fp32 GEMM, every operand layout
     (row-/column-major views such as ``x.T @ x``) without a copy, 64-bit offsets (no 4 GB operand
@@ -1113,7 +1113,8 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     L = lib()
     st = ctypes.c_void_p(stream_ptr(a.device))
     ldc = out.stride(0) if M > 1 else N
-    slices = _splitk_slices(M, N, K, a.device)
+    if slices is None:
+        slices = _splitk_slices(M, N, K, a.device)
     if slices > 1:
         # few 256 x 256 output tiles: split K so the grid fills the CUs, fp32 partial per slice,
         # slices summed in fixed order (fp64) with alpha / accumulate in the same pass
@@ -1140,7 +1141,7 @@ _GEMM_SMALL = os.environ.get("HEAT_GEMM_SMALL", "1") != "0"
 
 
 def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
-                   accumulate: bool = False) -> Optional[torch.Tensor]:
+                   accumulate: bool = False, slices: Optional[int] = None) -> Optional[torch.Tensor]:
     """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on the 128 x 128-tile kernel
     with split-K (``csrc/gemm_small.hip: gemm_f32s``): the products whose 256 x 256 tiles cannot
     fill the GPU (1024^3 .. 6144^3) and short-K tall updates (the Householder rank-256 update).
@@ -1171,9 +1172,10 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
     ldc = out.stride(0) if M > 1 else N
     tiles = -(-M // 128) * -(-N // 128)
     ncu = num_cus(a.device)
-    slices = 1
-    if tiles < 2 * ncu and K >= 512:   # two workgroups per CU: split K over the missing ones
-        slices = max(1, min(-(-2 * ncu // tiles), K // 256, _SPLITK_MAX_BYTES // (4 * M * N)))
+    if slices is None:
+        slices = 1
+        if tiles < 2 * ncu and K >= 512:   # two workgroups per CU: split K over the missing ones
+            slices = max(1, min(-(-2 * ncu // tiles), K // 256, _SPLITK_MAX_BYTES // (4 * M * N)))
     if slices > 1:
         used = L.ha_gemm_f32s_slices(K, slices)
         P = torch.empty(used * M * N, dtype=torch.float32, device=a.device)

@@ -27,6 +27,7 @@ from ..parallel.ring import ring_pass
 __all__ = ["cdist", "cdist_argmin", "cdist_stream", "cdist_topk", "manhattan", "rbf"]
 
 _ALLGATHER_BYTES = 2 << 30
+_SYM_MIN_F = 64   # compute-once symmetric tiles from this many features on (store-bound below)
 
 
 # local metrics (torch tensors) --------------------------------------------------------------
@@ -84,8 +85,12 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
 
     def _local(metric, x, y, sigma, out=None):
         # the same block on both sides (Y = None on one rank, or a rank's diagonal block): the
-        # difference kernels compute each distance pair once and mirror it
-        return ops.cdist(x, y, metric, sigma=sigma, out=out, exact=exact, symmetric=x is y)
+        # difference kernels compute each distance pair once and mirror it - where that pays: they
+        # write the distances at ~4 TB/s whatever they compute, and 2 f VALU ops per distance only
+        # outweigh the 4-byte store from f ~ 64 (SUSY 40k x 18: 1.65 ms compute-once vs 1.59 ms
+        # full, both store-bound; profiles/README.md round 5)
+        return ops.cdist(x, y, metric, sigma=sigma, out=out, exact=exact,
+                         symmetric=x is y and x.shape[-1] >= _SYM_MIN_F)
 
     if not isinstance(X, DNDarray):
         raise TypeError("X must be a DNDarray")
@@ -121,10 +126,10 @@ def _dist(X: DNDarray, Y: Optional[DNDarray] = None, metric="euclidean", sigma: 
         return DNDarray(_local(metric, x, y, sigma).to(tt), (m, n), dtype, 1, X.device, comm, Y.balanced)
     counts, displs = Y.counts_displs()
     ybytes = n * Y.gshape[1] * y.element_size()
-    if symmetric and (exact or metric == "manhattan" or ybytes > _allgather_bytes()):
-        # compute-once: the VALU difference kernels are compute-bound, so every off-diagonal tile
-        # pair is computed by one rank and mirrored; the MFMA expansion kernels are store-bound and
-        # all-gather below 2 GB
+    if symmetric and ybytes > _allgather_bytes():
+        # the half ring computes every off-diagonal tile pair once but RECEIVES half of the rank's
+        # output over xGMI (~50-100x the time of writing it to HBM); below 2 GB of Y the
+        # all-gather + local kernels win for every metric (see _local)
         out = torch.empty((x.shape[0], n), dtype=tt, device=x.device)
         _symmetric_half_ring(x, out, counts, displs, comm, lambda a, b: _local(metric, a, b, sigma).to(tt))
         return DNDarray(out, (m, n), dtype, 0, X.device, comm, X.balanced)
