@@ -127,6 +127,34 @@ def _native_fp32(a: torch.Tensor, b: torch.Tensor) -> bool:
     return ops.use_native(a)
 
 
+_GEMM_PLAN = os.environ.get("HEAT_GEMM_PLAN", "1") != "0"   # 0: the library for the small products
+
+
+def _native_plan(M: int, N: int, K: int):
+    """(kernel, K slices) for an exact fp32 product that fills the GPU poorly with 256 x 256 tiles,
+    from a cost model fitted to the split-K scan (profiles/gemm_splitk_scan_r05.jsonl): time ~
+    waves x (K per slice + a fixed per-tile overhead) + the slice sum. gemm_f32t: 256-tiles, one
+    workgroup per CU, overhead 256 k; gemm_f32s: 128-tiles, two per CU, overhead 130 k at 0.74x the
+    per-k cost of a 256-tile wave; slice sums (s + 1) M N 4 bytes at ~4 TB/s. Picks 1024^3 ->
+    f32s x8 (1.18x hipBLASLt), 2048^3 -> f32t x4 (1.35x), 3072^3 / 6144^3 -> f32t x3 (1.22x / 1.18x)."""
+    from ... import ops
+
+    ncu = ops.num_cus(torch.device("cuda", torch.cuda.current_device())) if torch.cuda.is_available() else 256
+    t256 = -(-M // 256) * -(-N // 256)
+    t128 = -(-M // 128) * -(-N // 128)
+    best = None
+    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+        ks = -(-K // s)
+        if s > 1 and (ks < 64 or s * M * N * 4 > (1 << 30)):
+            continue
+        sumc = 0.0 if s == 1 else (s + 1) * M * N * 4.37e-6
+        for kern, cost in (("f32t", -(-t256 * s // ncu) * (ks + 256) * 1.0 + sumc),
+                           ("f32s", -(-t128 * s // (2 * ncu)) * (ks + 130) * 0.74 + sumc)):
+            if best is None or cost < best[0]:
+                best = (cost, kern, s)
+    return best[1], best[2]
+
+
 def _library_better(M: int, N: int, K: int, exact: bool) -> bool:
     """Plain fp32 GEMMs whose 256 x 256 output tiles fill the 256 CUs poorly go to the library
     (hipBLASLt, exact fp32 products). Measured (``tools/microbench/gemm_small.py``, profiles/README):
@@ -165,10 +193,15 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
     if _native_fp32(a, b) and _library_better(a.shape[0], b.shape[1], a.shape[1], not _split_gemm_ok(a, b)):
         from ...ops import kernels as _kern
 
-        # the 128 x 128-tile kernel with split-K fills the GPU where the 256-tile one cannot
-        r = _kern.gemm_f32_small(a, b, out=out, alpha=alpha, accumulate=accumulate)
-        if r is not None:
-            return r
+        # products whose 256 x 256 tiles do not fill the GPU: the hand-written kernel and K-slice
+        # count of the measured cost model (_native_plan); the library only if neither applies
+        kern, sl = _native_plan(a.shape[0], b.shape[1], a.shape[1])
+        if _GEMM_PLAN and kern == "f32s":
+            r = _kern.gemm_f32_small(a, b, out=out, alpha=alpha, accumulate=accumulate, slices=sl)
+            if r is not None:
+                return r
+        elif _GEMM_PLAN:
+            return _kern.gemm_f32(a, b, out=out, accumulate=accumulate, alpha=alpha, slices=sl)
 
         with _kern.exact_fp32_library():   # exact fp32 products under any setting
             r = _mm_blocked(a, b)

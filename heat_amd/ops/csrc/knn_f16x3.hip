@@ -444,26 +444,44 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
       }
     need = false;
   };
+  // chunk staging, round 5: THREE LDS buffers and the DMA of chunk ch + 1 issued before chunk ch is
+  // computed (round 4 issued chunk ch's DMA and waited for it at once: ~1-2 us of exposed latency
+  // per 64-row chunk against ~0.4 us of MFMA work, 31 % MFMA-busy). Buffer (ch + 1) % 3 last held
+  // chunk ch - 2, whose deferred last-tile epilogue (pu) ran during chunk ch - 1. Per wave the u
+  // and v pieces are issued first and the image pieces last, so waiting for "all but the newest
+  // IMGW" completes everything of chunk ch (and the small u/v pieces of ch + 1).
+  constexpr int IMGW = PIECES / 4;
+  static_assert(PIECES % 4 == 0 && IMGW >= 1 && IMGW <= 4, "image pieces per wave");
+  auto issue = [&](int ch) {
+    const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
+    unsigned char* dst = smem + (ch % 3) * BUF;
+    if (wave == 0 && lane < CB / 2)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
+                                       (__attribute__((address_space(3))) void*)(dst + CHUNK_H), 16, 0, 0);
+#pragma unroll
+    for (int pc = wave; pc < VPIECES; pc += 4)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(vimg) + (int64_t)ch * CB * 16 + pc * 1024 + lane * 16,
+                                       (__attribute__((address_space(3))) void*)(dst + CHUNK_H + CB * 8 + pc * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int pc = wave; pc < PIECES; pc += 4)
+      __builtin_amdgcn_global_load_lds(src + 2 * pc * 1024,
+                                       (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, 0, 0);
+  };
+  if (nchunks > 0) issue(0);
   for (int ch = 0; ch < nchunks; ++ch) {
-    {
-      const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
-      unsigned char* dst = smem + (ch & 1) * BUF;
-#pragma unroll
-      for (int pc = wave; pc < PIECES; pc += 4)
-        __builtin_amdgcn_global_load_lds(src + 2 * pc * 1024,
-                                         (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, 0, 0);
-      if (wave == 0 && lane < CB / 2)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H), 16, 0, 0);
-#pragma unroll
-      for (int pc = wave; pc < VPIECES; pc += 4)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(vimg) + (int64_t)ch * CB * 16 + pc * 1024 + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(dst + CHUNK_H + CB * 8 + pc * 1024),
-                                         16, 0, 0);
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    if (ch + 1 < nchunks) {
+      issue(ch + 1);
+      if constexpr (IMGW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (IMGW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const unsigned char* buf = smem + (ch & 1) * BUF;
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* buf = smem + (ch % 3) * BUF;
     const _Float16* img = reinterpret_cast<const _Float16*>(buf);
     const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H);
     const unsigned* vb = reinterpret_cast<const unsigned*>(buf + CHUNK_H + CB * 8);
@@ -585,7 +603,7 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
                        meta, (unsigned*)(meta + 4));                                                             \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),       \
                        dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                           \
-    const size_t lds = 2 * ((size_t)KC::CHUNK_H + KC::CB * 8 + KC::CB * 16);                                    \
+    const size_t lds = 3 * ((size_t)KC::CHUNK_H + KC::CB * 8 + KC::CB * 16);  /* 3 chunk buffers */            \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                              \
     if (kn <= 1) { HA_H1TK_KN(FP, 1); }                                                                          \
     else if (kn <= 4) { HA_H1TK_KN(FP, 4); }                                                                     \
