@@ -479,7 +479,8 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    // a raw barrier: __syncthreads() would add s_waitcnt vmcnt(0), i.e. wait for the prefetch too
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const unsigned char* buf = smem + (ch % 3) * BUF;
     const _Float16* img = reinterpret_cast<const _Float16*>(buf);
@@ -515,7 +516,10 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
       ptile = ch * (CB / 32) + cb;
       pu = ub + cb * 32;
     }
-    __syncthreads();
+    // every wave's reads of this chunk (and of the previous one's deferred epilogue) are done
+    // before the buffer is refilled; no vmcnt wait: the next chunk's DMA stays in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (ptile >= 0) {
     epilogue(acc[((CB / 32) - 1) & 1], pu);

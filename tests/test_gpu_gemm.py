@@ -305,3 +305,25 @@ def test_gemm_f32_small_layouts(m, k, n, layout):
     ops.gemm_f32_small(A, B, out=out, alpha=-0.5, accumulate=True)
     ref2 = base.double() - 0.5 * ref
     assert torch.all((out.double() - ref2).abs() <= _bound(a, b) + 1e-6 * base.abs().double())
+
+
+@pytest.mark.parametrize("m,k,n", [(1000, 1000, 1000), (2048, 2048, 2048), (700, 100000, 300), (3000, 3000, 3000),
+                                   (129, 70, 4100)])
+def test_fgemm_native_plan_products(m, k, n):
+    """The products below one wave of 256-tiles run on the kernel / K-slice count of the cost
+    model (no library) and keep fp32-GEMM accuracy, with alpha and accumulate."""
+    from heat_amd.core.linalg import basics
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + n + k)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    assert basics._library_better(m, n, k, True)
+    kern, sl = basics._native_plan(m, n, k)
+    assert kern in ("f32t", "f32s") and sl >= 1
+    c = basics.fgemm(a, b)
+    ref = a.double() @ b.double()
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (kern, sl, (c.double() - ref).abs().max())
+    out = torch.ones(m, n, device=dev)
+    basics.fgemm(a, b, out=out, alpha=2.0, accumulate=True)
+    assert torch.all((out.double() - (1 + 2 * ref)).abs() <= 2 * _bound(a, b) + 1e-6)

@@ -8,7 +8,9 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   knn     - the bench.py knn step: 8 nearest of all 1e6 x 128 rows among themselves (certified h1_topk)
   randn   - 8e8 standard normals and 8e8 uniforms, fp32 (threefry.hip: tf_fill32, 3.2 GB each)
   smallk  - 10 fused small-k passes, k = 8, 1.25e7 x 64 (kmeans_smallk.hip: ks_step64, the reference protocol)
-  cdist_exact - exact (difference) cdist, SUSY size 40k x 18, 3 calls (cdist.hip: cdist_vx)"""
+  cdist_exact - exact (difference) cdist, SUSY size 40k x 18, 3 calls (cdist.hip: cdist_vx)
+  gemm_small - 1024^3 and 2048^3 exact fp32 through fgemm's plan (gemm_small.hip / gemm_tiled.hip split-K)
+  gram    - ht.matmul(A.T, A) at 400000 x 2048 (upper-triangle Gram tiles + fp64 slice sums)"""
 import sys
 
 import torch
@@ -64,6 +66,18 @@ def main():
         x = torch.rand(40_000, 18, device="cuda")
         for _ in range(3):
             ops.cdist(x, x, exact=True)
+    elif which == "gemm_small":
+        from heat_amd.core.linalg import basics
+
+        for n in (1024, 2048):
+            a = torch.randn(n, n, device="cuda")
+            b = torch.randn(n, n, device="cuda")
+            for _ in range(5):
+                basics.fgemm(a, b)
+    elif which == "gram":
+        A = ht.random.randn(400_000, 2048, split=0)
+        for _ in range(3):
+            ht.matmul(A.T, A)
     elif which == "hh":
         # round 4: two-level Householder QR pieces (panel steps, sliced V^T C, library update)
         a = torch.randn(400_000, 1024, device="cuda")
