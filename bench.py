@@ -60,6 +60,26 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    """A bindable rendezvous port below Linux's ephemeral range (heat_amd.run.free_port; not
+    imported from there: importing heat_amd in the launcher would initialise the GPU)."""
+    import random
+    import socket
+
+    rng = random.Random()
+    for _ in range(64):
+        port = rng.randrange(15000, 32768)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def launch_or_check(args) -> int:
     """Rank bookkeeping BEFORE anything touches the GPU (no torch.cuda call other than
     device_count here, never exec): -1 = this process is a rank, go on; else an exit code.
@@ -82,14 +102,10 @@ def launch_or_check(args) -> int:
         print("bench.py: --gpus {} but only {} GPUs are visible".format(args.gpus, ndev), file=sys.stderr, flush=True)
         return 2
     import signal
-    import socket
     import subprocess
     import threading
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = _free_port()
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_RANK=str(r),
@@ -324,17 +340,13 @@ def comm_ab_isolated(comm, sizes) -> dict:
     """Run :func:`comm_ab` in a child job of the same ranks (every rank starts one child with the
     launcher's RANK / WORLD_SIZE / LOCAL_RANK and a fresh MASTER_PORT from rank 0), bounded by
     ``HEAT_BENCH_AB_TIMEOUT`` seconds; rank 0's child prints the record."""
-    import socket
     import subprocess
 
     import heat_amd as ht
 
     port = None
     if comm.rank == 0:
-        sk = socket.socket()
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-        sk.close()
+        port = _free_port()
     port = comm.bcast(port, root=0)
     # a fresh rendezvous: not torchrun's agent store (TORCHELASTIC_USE_AGENT_STORE would make the
     # child connect to the agent's store on the new port, where nobody listens)

@@ -204,5 +204,20 @@ __device__ __forceinline__ floatx2 h3_score2(floatx2 acc, floatx2 r, floatx2 u, 
 
 int h3_fpad(int f) { return f <= 16 ? 16 : f <= 32 ? 32 : f <= 64 ? 64 : f <= 128 ? 128 : -1; }
 
+// sorted insertion into a lane's descending top-KN list (the kNN kernels)
+template <int KN>
+__device__ __forceinline__ void topk_insert(float (&tv)[KN], int (&ti)[KN], float v, int id) {
+#pragma unroll
+  for (int s = KN - 1; s >= 1; --s) {
+    const bool ap = v > tv[s - 1];
+    const bool ac = v > tv[s];
+    tv[s] = ap ? tv[s - 1] : (ac ? v : tv[s]);
+    ti[s] = ap ? ti[s - 1] : (ac ? id : ti[s]);
+  }
+  const bool a0 = v > tv[0];
+  tv[0] = a0 ? v : tv[0];
+  ti[0] = a0 ? id : ti[0];
+}
+
 }  // namespace
 

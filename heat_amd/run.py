@@ -19,12 +19,24 @@ import sys
 import threading
 
 
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def free_port() -> int:
+    """A bindable port BELOW the kernel's ephemeral range (32768+ on Linux): a port the OS hands
+    out for bind(0) can be taken again, before rank 0 listens on it, as the source port of some
+    outgoing connection (gloo opens many) - random picks from 15000-32767 cannot."""
+    import random
+
+    rng = random.Random()
+    for _ in range(64):
+        port = rng.randrange(15000, 32768)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def _pump(stream, rank: int, out, prefix: bool):
@@ -32,6 +44,7 @@ def _pump(stream, rank: int, out, prefix: bool):
         text = line.decode(errors="replace")
         out.write("[{}] {}".format(rank, text) if prefix else text)
         out.flush()
+
 
 
 def main(argv=None) -> int:
@@ -47,7 +60,7 @@ def main(argv=None) -> int:
     ns = p.parse_args(argv)
     if ns.module is None and ns.target is None:
         p.error("a script or -m module is required")
-    port = ns.port or _free_port()
+    port = ns.port or free_port()
     cmd_tail = (["-m", ns.module] + ([ns.target] if ns.target else []) if ns.module else [ns.target]) + ns.args
     procs = []
     for r in range(ns.nprocs):

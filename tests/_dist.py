@@ -7,7 +7,6 @@ which initialises the process group, then runs the function. Any rank failing fa
 from __future__ import annotations
 
 import os
-import socket
 import subprocess
 import sys
 
@@ -15,11 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from heat_amd.run import free_port
+
+    return free_port()
 
 
 def run_distributed(target: str, nprocs: int, timeout: int = 300, env_extra=None, keep_gpu: bool = False):

@@ -3,7 +3,6 @@ gloo ranks, rendezvous on 127.0.0.1), rank 0 prints exactly ONE JSON line with t
 the whole-job aggregate."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -13,11 +12,9 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from heat_amd.run import free_port
+
+    return free_port()
 
 
 def _json_lines(out):
