@@ -17,46 +17,107 @@ __device__ __forceinline__ void vm_wait() {
 // LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4; LDS address = lds + 16 lane) issued
 // through inline asm: for the builtin the compiler's wait-count pass cannot tell which LDS bytes
 // the transfer writes and puts s_waitcnt vmcnt(0) before the next LDS read - i.e. it waits for
-// the prefetched chunk too. The asm form is invisible to that pass (its own vmcnt waits only
+// the prefetched chunks too. The asm form is invisible to that pass (its own vmcnt waits only
 // become more conservative); the kernel waits for its transfers with counted vm_wait<N>().
+// M0 (the LDS address of the transfer) is saved and restored around it: the compiler treats M0 as
+// reserved and would not see a clobber.
 __device__ __forceinline__ void lds_dma16(const void* g, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+  unsigned saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+
+// Sorted insertion into a descending list with the eviction recorded in rej (the caller has
+// checked v > tv[KP - 1]). Slot s keeps median(tv[s - 1], v, tv[s]) - one v_med3_f32 instead of
+// two selects - and the index follows with two selects on the shared compares.
+template <int KP>
+__device__ __forceinline__ void topk_insert_ev(float (&tv)[KP], int (&ti)[KP], float v, int id, float& rej) {
+  rej = fmaxf(rej, tv[KP - 1]);  // the evicted last entry (-inf while the list is not full)
+#pragma unroll
+  for (int s = KP - 1; s >= 1; --s) {
+    const bool ap = v > tv[s - 1];
+    const bool ac = v > tv[s];
+    ti[s] = ap ? ti[s - 1] : (ac ? id : ti[s]);
+    tv[s] = __builtin_amdgcn_fmed3f(tv[s - 1], v, tv[s]);
+  }
+  ti[0] = v > tv[0] ? id : ti[0];
+  tv[0] = fmaxf(tv[0], v);
+}
+
+// Uniform centroid scale for h1_topk: r_c = 2^e for EVERY live row, e from max_c max_i |c_i|
+// (meta[1], posted by h3_cscale), and the rank-1 fragments -u_c / r_c re-split to match. Then a
+// tile's accumulator is the score / r, the same r for all rows: the kernel's epilogue compares
+// raw accumulators (no per-row multiply, no r staging) and scales its lists once at the end.
+// The h1 error bound E is unchanged: it is already stated with the global c_max, and the fp16
+// subnormal range (components below 2^-14 of the largest) adds at most f 2^-25 r |x_s|_inf <=
+// 2^-17 c_max, inside E's 2^-15 c_max term.
+template <int FPAD>
+__global__ __launch_bounds__(256) void h3_uniform_r(int k, float* __restrict__ ur, const float* __restrict__ meta,
+                                                    unsigned* __restrict__ vimg) {
+  constexpr int CB = H3Cfg<FPAD>::CB;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= k) return;
+  const float mx = meta[1];
+  int e = 0;
+  if (mx > 0.f && mx < __builtin_huge_valf()) frexpf(mx, &e);
+  float* urc = ur + (int64_t)(c / CB) * 2 * CB + c % CB;
+  urc[CB] = ldexpf(1.f, e);
+  const float y = -ldexpf(urc[0], -e);  // -u_c / r, split into hi + mid + lo bf16 (24 bits)
+  const unsigned hi = h3_bf16_rn(y);
+  const float r1 = y - h3_bf16_f(hi);
+  const unsigned mid = h3_bf16_rn(r1);
+  const unsigned lo = h3_bf16_rn(r1 - h3_bf16_f(mid));
+  unsigned* vc = vimg + ((int64_t)(c / 32) * 64 + c % 32) * 2;
+  vc[0] = hi | (mid << 16);
+  vc[1] = lo;
 }
 
 // Certified one-term top-k ("h1"), the kNN form of h1_filter: scores from hi_c . hi_x only (ONE
 // MFMA per k-step instead of three) plus the exact rank-1 u term, each within E of the fp32 score
-// (E: h1_filter's bound). A lane keeps its KP best approximate scores and `rej`, the largest score
-// it let go (rejected or evicted). After the halves merge, a point is CERTIFIED when
-//     rej < a_KN - 2 E          (a_KN = the KN-th best approximate score in the list):
-// then every candidate outside the list is, exactly, below KN candidates inside it, so the true
-// top-KN is a subset of the KP-list, which the caller rescores exactly. Uncertain points are
+// (E: h1_filter's bound). A lane keeps its KH best approximate scores and `rej`, an upper bound
+// of every score it let go (rejected or evicted). After the halves merge, a point is CERTIFIED when
+//     rej < a_kn - 2 E          (a_kn = the kn-th best approximate score in the list):
+// then every candidate outside the list is, exactly, below kn candidates inside it, so the true
+// top-kn is a subset of the KO-list, which the caller rescores exactly. Uncertain points are
 // flagged (cert = 0) and re-run through the 3-term kernel by the caller.
-// Output per point: KP approximate squared distances (ascending) and int32 indices, cert flag.
-template <int KP>
-__device__ __forceinline__ void topk_insert_ev(float (&tv)[KP], int (&ti)[KP], float v, int id, float& rej) {
-  rej = fmaxf(rej, tv[KP - 1]);  // the evicted last entry (-inf while the list is not full)
-  topk_insert<KP>(tv, ti, v, id);
-}
-
-// KH: list length per lane half (each half sees half of the rows of C); the two half lists are
-// merged into the output list of 16. Measured (bench knn, 1e6 x 1e6 x 128): KH = 16 -> 373 ms +
-// 10.8 % of the queries re-checked (81 ms); KH = 8 -> 350 ms but 32.7 % re-checked (222 ms).
-// The insertions, not the MFMAs, bound this kernel (7-9 VALU per MFMA): a lane whose tile beats
-// its threshold makes the whole wave run the insertion. Parking such tiles in LDS and draining
-// them for all lanes together (2 parked tiles per lane) was 5x SLOWER: a drain runs the union of
-// the lanes' insertion positions, so batching sparse, uncorrelated insertions does not pay.
-// KO: output candidates per point (16: the two half lists merged into 16, what the merge lets go
-// raises rej; 32: both half lists kept whole, rej = the halves' own - a wider certification margin,
-// so fewer queries fall back to the 3-term kernel, for twice the rescoring input).
-template <int FPAD, int KH, int KN, int NPB_, int KO_ = 16>
-__global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+// Output per point: KO approximate squared distances (ascending) and int32 indices, cert flag.
+//
+// Round 5 structure (round 4: 31-35 % MFMA-busy at 2 waves / SIMD; its ISA shows every A
+// fragment read from LDS into the SAME registers right before its MFMA - 256 VGPRs in use, so
+// the LDS latency was exposed 8 times per tile - and the epilogue in a branch of its own):
+//  * one workgroup of 4 waves per CU, 512 registers per wave, 2 x 32 points per wave (NPB = 2:
+//    each A fragment read feeds two MFMAs, 256 points per workgroup as before per CU);
+//  * the next tile's A fragments are read while the current tile's MFMAs run;
+//  * chunks of 4 tiles staged by LDS-DMA into a ring of 4 buffers, 3 chunks in flight, one
+//    barrier per chunk (the ring slot refilled is the one every wave finished before it);
+//  * uniform centroid scale (h3_uniform_r): the epilogue is a max3 tree, one med3 for rej and a
+//    compare per 16 scores, branch-free so it fills the MFMA gaps;
+//  * selection through a per-lane queue of Q candidates above the threshold: the sorted insertion
+//    (the expensive part: a wave runs the union of its lanes' insertions) runs only when some
+//    lane's queue is full, for Q candidates of every lane at once.
+// rej bookkeeping: the epilogue sets rej = med3(rej, m, thr) = max(rej, min(m, thr)) with m the
+// tile max and thr the list's last entry (rej <= thr always holds): it covers every score of the
+// tile that is not queued. Queued scores that no longer beat the list at merge time go to rej
+// exactly; evictions too.
+template <int FPAD, int KH, int KO>
+__global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
-                                                  int nchunks, float* __restrict__ dist, int* __restrict__ idx,
+                                                  int nch, int kn, float* __restrict__ dist, int* __restrict__ idx,
                                                   unsigned char* __restrict__ cert) {
-  using K = H3Cfg<FPAD, NPB_>;
-  constexpr int F2 = K::F2, KS = K::KS, CB = K::CB, NPB = K::NPB, CHUNK_H = K::CHUNK_H;
+  using K = H3Cfg<FPAD, 2>;
+  constexpr int F2 = K::F2, KS = K::KS, NPB = 2;
+  constexpr int TPI = 4;                  // 32-centroid tiles per staged chunk
+  constexpr int PIECES = TPI * KS;        // 1 KB hi-fragment pieces per chunk (piece q <- image piece 2q)
+  constexpr int VP = TPI * 512 / 1024;    // rank-1 fragment pieces per chunk (512 B per tile)
+  constexpr int BUF = (PIECES + VP) * 1024;
+  constexpr int NB = 4, AHEAD = 3;        // ring slots, chunks in flight
+  constexpr int IMGW = PIECES / 4;        // image pieces per wave per chunk
+  constexpr int Q = 4;                    // queue slots per list
   constexpr float NINF = -__builtin_huge_valf();
+  static_assert(PIECES % 4 == 0 && VP <= 4, "pieces per wave");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -91,144 +152,184 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     const u32x4 bw = {h ? 0u : (sb | (sb << 16)), h ? 0u : sb, 0u, 0u};
     bsx[pb] = __builtin_bit_cast(bf16x8, bw);
   }
-  constexpr int KO = KO_;  // output candidates per point
-  float tv[NPB][KH], rej[NPB];
-  int ti[NPB][KH];
+  float tv[NPB][KH], rej[NPB], thr0[NPB], qv[NPB][Q];
+  int ti[NPB][KH], qi[NPB][Q], qn[NPB];
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
     rej[pb] = NINF;
+    thr0[pb] = NINF;
+    qn[pb] = 0;
 #pragma unroll
-    for (int s2 = 0; s2 < KH; ++s2) {
-      tv[pb][s2] = NINF;
-      ti[pb][s2] = -1;
+    for (int s = 0; s < KH; ++s) {
+      tv[pb][s] = NINF;
+      ti[pb][s] = -1;
+    }
+#pragma unroll
+    for (int s = 0; s < Q; ++s) {
+      qv[pb][s] = NINF;
+      qi[pb][s] = -1;
     }
   }
-  // only the hi half of every (cb, ks) fragment pair is staged (piece 2q of the chunk -> LDS q)
-  constexpr int PIECES = CHUNK_H * 2 / 1024 / 2;
-  constexpr int VPIECES = CB * 16 / 1024;
-  constexpr int BUF = CHUNK_H + CB * 8 + CB * 16;
-  const unsigned* vimg = reinterpret_cast<const unsigned*>(meta + 4);
+  // accumulators: [tile parity][pb]; the "previous tile" of the first one scores -inf everywhere
   floatx16 acc[2][NPB];
-  float w[NPB][16];
-  bool need = false;
-  const float* pu = nullptr;
-  int ptile = -1;
-  auto epilogue = [&](const floatx16 (&ac)[NPB], const float* pu_) {
-    floatx4 cr[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) cr[g] = *reinterpret_cast<const floatx4*>(pu_ + CB + 8 * g + 4 * h);
+  for (int pb = 0; pb < NPB; ++pb) {
+    acc[0][pb] = (floatx16)(NINF);
+    acc[1][pb] = (floatx16)(NINF);
+  }
+  bool need = false;
+  int ptile = 0;
+  // branch-free epilogue of a finished tile: per list, tile max -> threshold test, rej
+  auto epilogue = [&](const floatx16 (&ac)[NPB]) {
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb) {
+      float m = fmaxf(fmaxf(ac[pb][0], ac[pb][1]), ac[pb][2]);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) w[pb][q] = ac[pb][q] * cr[q >> 2][q & 3];
-      float m = w[pb][0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) m = fmaxf(m, w[pb][r]);
-      const bool nd = m > tv[pb][KH - 1];
-      rej[pb] = nd ? rej[pb] : fmaxf(rej[pb], m);  // the whole tile is let go
-      need |= nd;
+      for (int r = 3; r < 15; r += 2) m = fmaxf(fmaxf(m, ac[pb][r]), ac[pb][r + 1]);
+      m = fmaxf(m, ac[pb][15]);
+      const float thr = tv[pb][KH - 1];
+      thr0[pb] = thr;
+      rej[pb] = __builtin_amdgcn_fmed3f(rej[pb], m, thr);
+      need |= m > thr;
     }
   };
-  auto insert = [&](int tile) {
+  auto merge = [&](int pb) {
+#pragma unroll
+    for (int s = 0; s < Q; ++s) {
+      const float v = qv[pb][s];
+      if (s < qn[pb]) {
+        if (v > tv[pb][KH - 1]) topk_insert_ev<KH>(tv[pb], ti[pb], v, qi[pb][s], rej[pb]);
+        else rej[pb] = fmaxf(rej[pb], v);
+      }
+    }
+    qn[pb] = 0;
+  };
+  // queue the scores of a finished tile that beat the threshold seen by its epilogue. Compact on
+  // purpose (the loop body is unrolled 4 tiles deep): one ballot per position builds the
+  // wave-uniform mask of positions holding a candidate in SOME lane, and a scalar loop visits only
+  // those; the score of a visited position comes out through a select chain (no indexed registers).
+  // A full queue (some lane at Q) is merged into the sorted lists right away.
+  auto select = [&](const floatx16 (&ac)[NPB], int tile) {
     if (__builtin_amdgcn_ballot_w64(need) == 0ull) return;
+    need = false;
     const int tbase = tile * 32 + 4 * h;
 #pragma unroll
-    for (int pb = 0; pb < NPB; ++pb)
+    for (int pb = 0; pb < NPB; ++pb) {
+      unsigned rmask = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (w[pb][r] > tv[pb][KH - 1])
-          topk_insert_ev<KH>(tv[pb], ti[pb], w[pb][r], tbase + (r & 3) + 8 * (r >> 2), rej[pb]);
-        else
-          rej[pb] = fmaxf(rej[pb], w[pb][r]);
+      for (int r = 0; r < 16; ++r) rmask |= (__builtin_amdgcn_ballot_w64(ac[pb][r] > thr0[pb]) != 0ull ? 1u : 0u) << r;
+      while (rmask) {
+        const int r = __builtin_ctz(rmask);
+        rmask &= rmask - 1;
+        float v = ac[pb][0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) v = r == q ? ac[pb][q] : v;
+        const bool a = v > thr0[pb];
+        const int id = tbase + (r & 3) + 8 * (r >> 2);
+#pragma unroll
+        for (int s = Q - 1; s >= 1; --s) {
+          qv[pb][s] = a ? qv[pb][s - 1] : qv[pb][s];
+          qi[pb][s] = a ? qi[pb][s - 1] : qi[pb][s];
+        }
+        qv[pb][0] = a ? v : qv[pb][0];
+        qi[pb][0] = a ? id : qi[pb][0];
+        qn[pb] += a ? 1 : 0;
+        if (__builtin_amdgcn_ballot_w64(qn[pb] == Q) != 0ull) merge(pb);
       }
-    need = false;
+    }
   };
-  // chunk staging: FOUR LDS buffers, two chunks in flight. Round 4 waited for each chunk's DMA
-  // right after issuing it, and the 3-buffer / one-ahead version measured only 2 % faster (368 ms,
-  // 31 % MFMA-busy): a workgroup streams the whole training image (the L2 serves ~92 % of it,
-  // FETCH_SIZE), so the chunk rate is latency x bytes in flight - 17.5 KB per workgroup was not
-  // enough. Now chunk ch + 2 is issued while ch is computed (35 KB per workgroup, 70 KB per CU in
-  // flight). One barrier per chunk: at the barrier of chunk ch every wave has finished chunk
-  // ch - 1, the last reader of buffer (ch + 2) % 4 (chunk ch - 2's deferred last-tile epilogue).
-  // Per wave the u / v pieces are issued before the image pieces (vmcnt retires in order).
-  constexpr int IMGW = PIECES / 4;
-  static_assert(PIECES % 4 == 0 && IMGW >= 1 && IMGW <= 4, "image pieces per wave");
-  static_assert(VPIECES <= 4, "v pieces per chunk");
-  // DMA instructions per chunk issued by this wave (u: wave 0; v piece pc: wave pc; image: IMGW)
-  const int per_chunk = (wave == 0 ? 1 : 0) + (wave < VPIECES ? 1 : 0) + IMGW;
+
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem);
+  const char* gimg = reinterpret_cast<const char*>(image) + lane * 16;
+  const char* gv = reinterpret_cast<const char*>(meta + 4) + lane * 16;
+  // this wave's DMA instructions per chunk: image pieces wave, wave + 4, ...; v piece `wave`
+  const bool vw = wave < VP;
   auto issue = [&](int ch) {
-    const char* src = reinterpret_cast<const char*>(image + (int64_t)ch * CHUNK_H) + lane * 16;
-    const unsigned dst = lds0 + (ch & 3) * BUF;
-    if (wave == 0 && lane < CB / 2) lds_dma16(reinterpret_cast<const char*>(u + ch * 2 * CB) + lane * 16, dst + CHUNK_H);
+    const unsigned dst = lds0 + (ch % NB) * BUF;
 #pragma unroll
-    for (int pc = wave; pc < VPIECES; pc += 4)
-      lds_dma16(reinterpret_cast<const char*>(vimg) + (int64_t)ch * CB * 16 + pc * 1024 + lane * 16,
-                dst + CHUNK_H + CB * 8 + pc * 1024);
-#pragma unroll
-    for (int pc = wave; pc < PIECES; pc += 4) lds_dma16(src + 2 * pc * 1024, dst + pc * 1024);
+    for (int pc = 0; pc < IMGW; ++pc) {
+      const int q = wave + 4 * pc;
+      lds_dma16(gimg + ((int64_t)ch * PIECES + q) * 2048, dst + q * 1024);
+    }
+    if (vw) lds_dma16(gv + ((int64_t)ch * VP + wave) * 1024, dst + (PIECES + wave) * 1024);
   };
-  if (nchunks > 0) issue(0);
-  if (nchunks > 1) issue(1);
-  for (int ch = 0; ch < nchunks; ++ch) {
+  // the point fragments are in registers before the ring starts: otherwise the compiler's waits
+  // for them land inside the loop (first use), where they would also wait for the DMA in flight
+  vm_wait<0>();
+#pragma unroll
+  for (int c = 0; c < AHEAD; ++c)
+    if (c < nch) issue(c);
+  for (int ch = 0; ch < nch; ++ch) {
     __builtin_amdgcn_sched_barrier(0);
-    // this wave's pieces of chunk ch have landed once at most chunk ch + 1's are outstanding
-    if (ch + 1 < nchunks) {
-      if (per_chunk == IMGW) vm_wait<IMGW>();
-      else if (per_chunk == IMGW + 1) vm_wait<IMGW + 1>();
-      else vm_wait<IMGW + 2>();
+    // this wave's pieces of chunk ch have landed once at most the later chunks' are outstanding
+    const int later = min(nch - 1 - ch, AHEAD - 1);
+    if (later >= 2) {
+      if (vw) vm_wait<2 * IMGW + 2>();
+      else vm_wait<2 * IMGW>();
+    } else if (later == 1) {
+      if (vw) vm_wait<IMGW + 1>();
+      else vm_wait<IMGW>();
     } else {
       vm_wait<0>();
     }
-    // a raw barrier: __syncthreads() would add s_waitcnt vmcnt(0), i.e. wait for the prefetch too
+    // a raw barrier: __syncthreads() would add s_waitcnt vmcnt(0), i.e. wait for the prefetch too.
+    // Past it every wave has finished chunk ch - 1, whose slot the next DMA refills.
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (ch + 2 < nchunks) issue(ch + 2);
+    if (ch + AHEAD < nch) issue(ch + AHEAD);
     __builtin_amdgcn_sched_barrier(0);
-    const unsigned char* buf = smem + (ch & 3) * BUF;
-    const _Float16* img = reinterpret_cast<const _Float16*>(buf);
-    const float* ub = reinterpret_cast<const float*>(buf + CHUNK_H);
-    const unsigned* vb = reinterpret_cast<const unsigned*>(buf + CHUNK_H + CB * 8);
+    const unsigned char* buf = smem + (ch % NB) * BUF;
+    halfx8 af[2][KS];
 #pragma unroll
-    for (int cb = 0; cb < CB / 32; ++cb) {
-      const int cur = cb & 1;
+    for (int ks = 0; ks < KS; ++ks) af[0][ks] = *reinterpret_cast<const halfx8*>(buf + ks * 1024 + lane * 16);
+#pragma unroll
+    for (int tt = 0; tt < TPI; ++tt) {
+      const int cur = tt & 1;
+      const uint2 vv = *reinterpret_cast<const uint2*>(buf + PIECES * 1024 + tt * 512 + lane * 8);
+      const u32x4 aw = {vv.x, vv.y, 0u, 0u};
+      const bf16x8 av = __builtin_bit_cast(bf16x8, aw);
 #pragma unroll
       for (int pb = 0; pb < NPB; ++pb) acc[cur][pb] = (floatx16)(0.f);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const halfx8 ahi = *reinterpret_cast<const halfx8*>(img + ((cb * KS + ks) * 64 + lane) * 8);
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int pb = 0; pb < NPB; ++pb)
-          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi[pb][ks], acc[cur][pb], 0, 0, 0);
-      }
-      {
-        const uint2 vv = *reinterpret_cast<const uint2*>(vb + (cb * 64 + lane) * 2);
-        const u32x4 aw = {vv.x, vv.y, 0u, 0u};
-        const bf16x8 av = __builtin_bit_cast(bf16x8, aw);
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][ks], bhi[pb][ks], acc[cur][pb], 0, 0, 0);
 #pragma unroll
-        for (int pb = 0; pb < NPB; ++pb)
-          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bsx[pb], acc[cur][pb], 0, 0, 0);
-      }
-      if (ptile >= 0) epilogue(acc[cur ^ 1], pu);
+      for (int pb = 0; pb < NPB; ++pb)
+        acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bsx[pb], acc[cur][pb], 0, 0, 0);
+      epilogue(acc[cur ^ 1]);
 #pragma unroll
       for (int i = 0; i < (KS + 1) * NPB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // then up to 12 VALU
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // then up to 2 VALU
       }
-      if (ptile >= 0) insert(ptile);
-      ptile = ch * (CB / 32) + cb;
-      pu = ub + cb * 32;
+      // the next tile's A fragments, read under this tile's MFMAs
+      if (tt + 1 < TPI) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          af[cur ^ 1][ks] = *reinterpret_cast<const halfx8*>(buf + ((tt + 1) * KS + ks) * 1024 + lane * 16);
+      }
+      select(acc[cur ^ 1], ptile);
+      ptile = ch * TPI + tt;
     }
   }
-  if (ptile >= 0) {
-    epilogue(acc[((CB / 32) - 1) & 1], pu);
-    insert(ptile);
-  }
+  // the last tile, then whatever the queues still hold
+  epilogue(acc[(TPI - 1) & 1]);
+  select(acc[(TPI - 1) & 1], ptile);
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb)
+    if (__builtin_amdgcn_ballot_w64(qn[pb] > 0) != 0ull) merge(pb);
+  // lists are in accumulator units (score / r, one r for every row): back to scores
+  const float R = u[K::CB];
   const float umax = meta[2];
   const float cmax = sqrtf(2.f * umax);
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
+#pragma unroll
+    for (int s = 0; s < KH; ++s) tv[pb][s] *= R;
+    rej[pb] *= R;
     // merge the two half lists (disjoint candidates) into the output list of KO: whatever the
     // merge lets go raises rej
     float mv[KO];
@@ -255,6 +356,14 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
     const float xs = xsq[pb] + __shfl_xor(xsq[pb], 32, 64);
     const float xc = xn * cmax;
     const float E = 1.01f * 0x1p-10f * xc + 0x1p-16f * (xc + sx[pb] * umax) + 0x1p-15f * cmax;
+    // the kn-th best entry (kn is a runtime argument: a select chain, no indexed registers)
+    float akn = mv[0];
+    int ikn = mi[0];
+#pragma unroll
+    for (int s2 = 1; s2 < KO; ++s2) {
+      akn = s2 == kn - 1 ? mv[s2] : akn;
+      ikn = s2 == kn - 1 ? mi[s2] : ikn;
+    }
     const int64_t pi = pbase + pb * 32 + j;
     if (h == 0 && pi < n) {
       const float isx = 1.f / sx[pb];
@@ -264,54 +373,64 @@ __global__ __launch_bounds__(256, 2) void h1_topk(const _Float16* __restrict__ p
         dist[pi * KO + s2] = ok ? fmaxf(xs * isx * isx - 2.f * mv[s2] * isx, 0.f) : __builtin_huge_valf();
         idx[pi * KO + s2] = mi[s2];
       }
-      cert[pi] = (mi[KN - 1] >= 0 && rej[pb] < mv[KN - 1] - 2.f * E) ? 1 : 0;
+      cert[pi] = (ikn >= 0 && rej[pb] < akn - 2.f * E) ? 1 : 0;
     }
   }
 }
 
 }  // namespace
 
+// Rows of C padded for h1_topk: whole 4-tile chunks (128 rows).
+static inline int64_t h1_kpad(int m) { return ((int64_t)m + 127) / 128 * 128; }
+
+// Workspace of ha_h1_topk (>= ha_h3_workspace_bytes(m, f): the same layout over 128-row padding).
+HA_EXPORT int64_t ha_h1_workspace_bytes(int m, int f) {
+  const int fpad = h3_fpad(f);
+  if (fpad < 0 || m <= 0) return -1;
+  const int64_t kpad = h1_kpad(m);
+  return kpad * fpad * 2 * 2 + kpad * 8 + 16 + kpad * 16;
+}
+
 // Certified one-term k nearest rows of C (see h1_topk): dist / idx [n, kp] approximate squared
 // distances ascending + int32 row indices (the caller rescores them exactly), cert [n] uint8 (1 =
-// the true kn nearest are among the kp). kn <= 8 with kp = 16 or 32. workspace: ha_h3_workspace_bytes.
+// the true kn nearest are among the kp). kn <= 8 with kp = 16 or 32. workspace: ha_h1_workspace_bytes.
 HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, const float* C, int m, int64_t ldc,
                          void* workspace, int kn, int kp, float* dist, int* idx, unsigned char* cert, void* stream) {
   const int fpad = h3_fpad(f);
   if (fpad < 0 || m <= 0 || kn < 1 || kn > 8 || (kp != 16 && kp != 32)) return HA_UNSUPPORTED;
   if (n <= 0) return HA_OK;
   hipStream_t s = (hipStream_t)stream;
-  const int cb = fpad >= 128 ? 64 : 128;
-  const int kpad = (m + cb - 1) / cb * cb;
+  const int64_t kpad64 = h1_kpad(m);
+  if (kpad64 > (int64_t)1 << 30) return HA_UNSUPPORTED;
+  const int kpad = (int)kpad64;
   _Float16* image = (_Float16*)workspace;
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
   float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
-  // the error bound needs max |c| and max u (atomicMax into zeroed words)
+  // the error bound and the uniform scale need max |c| and max u (atomicMax into zeroed words)
   if (hipMemsetAsync(meta, 0, 16, s) != hipSuccess) return HA_LAUNCH;
-#define HA_H1TK_KO(FP, KN, KO)                                                                                 \
-  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KN, NPBT, KO>),                             \
+#define HA_H1TK_KO(FP, KO)                                                                                     \
+  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO>),                                       \
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                    \
-  hipLaunchKernelGGL((h1_topk<FP, 16, KN, NPBT, KO>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,  \
-                     kpad / KC::CB, dist, idx, cert)
-#define HA_H1TK_KN(FP, KN)                                                                                     \
-  if (kp == 32) {                                                                                              \
-    HA_H1TK_KO(FP, KN, 32);                                                                                    \
-  } else {                                                                                                     \
-    HA_H1TK_KO(FP, KN, 16);                                                                                    \
-  }
+  hipLaunchKernelGGL((h1_topk<FP, 16, KO>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,           \
+                     kpad / 128, kn, dist, idx, cert)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
-    constexpr int NPBT = FP >= 128 ? 1 : 2;                                                                      \
-    using KC = H3Cfg<FP, NPBT>;                                                                                  \
+    using KC = H3Cfg<FP, 2>;                                                                                     \
     hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, m, f, ldc, kpad, u,  \
                        meta, (unsigned*)(meta + 4));                                                             \
+    hipLaunchKernelGGL(h3_uniform_r<FP>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m, u, meta,         \
+                       (unsigned*)(meta + 4));                                                                   \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),       \
                        dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                           \
-    const size_t lds = 4 * ((size_t)KC::CHUNK_H + KC::CB * 8 + KC::CB * 16);  /* 4 chunk buffers */            \
+    /* 4 ring slots of 4 tiles: hi fragments + rank-1 fragments */                                               \
+    const size_t lds = 4 * ((size_t)4 * KC::KS * 1024 + 2 * 1024);                                              \
     const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                              \
-    if (kn <= 1) { HA_H1TK_KN(FP, 1); }                                                                          \
-    else if (kn <= 4) { HA_H1TK_KN(FP, 4); }                                                                     \
-    else { HA_H1TK_KN(FP, 8); }                                                                                  \
+    if (kp == 32) {                                                                                              \
+      HA_H1TK_KO(FP, 32);                                                                                        \
+    } else {                                                                                                     \
+      HA_H1TK_KO(FP, 16);                                                                                        \
+    }                                                                                                            \
     break;                                                                                                       \
   }
   switch (fpad) {
@@ -323,7 +442,6 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
       return HA_UNSUPPORTED;
   }
 #undef HA_H1TK
-#undef HA_H1TK_KN
 #undef HA_H1TK_KO
   return ha_launch_status();
 }

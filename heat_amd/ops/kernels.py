@@ -349,7 +349,9 @@ def knn_topk(Q: torch.Tensor, T: torch.Tensor, k: int, packed: Optional[PackedPo
         if packed is None or packed.key != _points_key(Q):
             packed = kmeans_pack_points(Q)
         Tc = T if T.stride(-1) == 1 else T.contiguous()
-        ws = torch.empty(L.ha_h3_workspace_bytes(nt, f), dtype=torch.uint8, device=dev)
+        # the certified pass pads the training rows to whole 128-row chunks: size for both kernels
+        ws = torch.empty(max(L.ha_h3_workspace_bytes(nt, f), L.ha_h1_workspace_bytes(nt, f)), dtype=torch.uint8,
+                         device=dev)
         # fill the GPU: with few query blocks, divide the training chunks over workgroup columns
         # (>= 4 waves of 128 queries per CU overall) and merge the partial lists
         qblocks = (nq + 127) // 128

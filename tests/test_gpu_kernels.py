@@ -979,8 +979,8 @@ def test_knn_rescore_kernel(c, k, f, idx64):
         assert torch.equal(valid.sum(1), nvalid)
 
 
-@pytest.mark.parametrize("f", [128, 64, 18])
-def test_knn_certified_one_term(f):
+@pytest.mark.parametrize("f,k", [(128, 8), (64, 8), (18, 8), (16, 1), (128, 4)])
+def test_knn_certified_one_term(f, k):
     """The certified one-term pass (h1_topk: 16 candidates per query from hi.hi scores + a rigorous
     bound, uncertain queries re-run through the 3-term kernel, exact rescoring) gives the exact
     fp64 k nearest neighbours, including on duplicated training rows (exact ties: the uncertain
@@ -990,7 +990,7 @@ def test_knn_certified_one_term(f):
 
     dev = _dev()
     g = torch.Generator(device="cpu").manual_seed(f)
-    nq, nt, k = 140_000, 20_000, 8          # enough query blocks for the single-split path
+    nq, nt = 140_000, 20_000                # enough query blocks for the single-split path
     Q = torch.randn(nq, f, generator=g).to(dev)
     T = torch.randn(nt, f, generator=g).to(dev)
     T[:600] = T[600:1200]                                   # exact duplicates -> ties
@@ -1019,6 +1019,30 @@ def test_knn_certified_one_term(f):
     clear = (torch.sort(d, dim=1).values[:, k] - rd[:, -1]) > 1e-4 * rd[:, -1].clamp(min=1)
     same = (torch.sort(idx[sel], 1).values == torch.sort(ri, 1).values).all(1)
     assert bool(same[clear].all()), int((~same[clear]).sum())
+
+
+def test_knn_certified_heterogeneous_norms():
+    """Training rows whose norms span 1e-3..1e3 (the certified pass scales all of them by ONE power
+    of two, so small rows sit in fp16's subnormal range): the result is still the exact fp64 k
+    nearest neighbours - whatever the one-term pass cannot certify goes through the 3-term kernel."""
+    from heat_amd import ops
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    nq, nt, f, k = 140_000, 9_000, 40, 5
+    T = torch.randn(nt, f, generator=g) * torch.pow(10.0, torch.empty(nt, 1).uniform_(-3, 3, generator=g))
+    Q = T[torch.randint(0, nt, (nq,), generator=g)] * (1 + 1e-2 * torch.randn(nq, 1, generator=g))
+    Q, T = Q.to(dev), T.to(dev)
+    before = dict(K._KNN_STATS)
+    dist, idx = ops.knn_topk(Q, T, k)
+    assert K._KNN_STATS["queries"] - before["queries"] == nq
+    sel = torch.randint(0, nq, (4000,), generator=g).to(dev)
+    d = torch.cdist(Q[sel].double(), T.double()) ** 2
+    rd, ri = torch.sort(d, dim=1, stable=True)
+    rd = rd[:, :k]
+    assert torch.allclose(dist[sel].double(), rd, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(d.gather(1, idx[sel]), rd, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "gaussian", "manhattan"])
