@@ -101,23 +101,22 @@ __global__ __launch_bounds__(256) void h3_uniform_r(int k, float* __restrict__ u
 // tile max and thr the list's last entry (rej <= thr always holds): it covers every score of the
 // tile that is not queued. Queued scores that no longer beat the list at merge time go to rej
 // exactly; evictions too.
-template <int FPAD, int KH, int KO>
-__global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB>
+__global__ __launch_bounds__(256, MINB) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
                                                   int nch, int kn, float* __restrict__ dist, int* __restrict__ idx,
-                                                  unsigned char* __restrict__ cert) {
-  using K = H3Cfg<FPAD, 2>;
-  constexpr int F2 = K::F2, KS = K::KS, NPB = 2;
-  constexpr int TPI = 4;                  // 32-centroid tiles per staged chunk
+                                                  unsigned char* __restrict__ cert, int dbg) {
+  using K = H3Cfg<FPAD, NPB>;
+  constexpr int F2 = K::F2, KS = K::KS;
+  // NPB: 32-point blocks per wave; TPI: 32-centroid tiles per staged chunk; MINB: workgroups / CU
   constexpr int PIECES = TPI * KS;        // 1 KB hi-fragment pieces per chunk (piece q <- image piece 2q)
-  constexpr int VP = TPI * 512 / 1024;    // rank-1 fragment pieces per chunk (512 B per tile)
-  constexpr int BUF = (PIECES + VP) * 1024;
-  constexpr int NB = 4, AHEAD = 3;        // ring slots, chunks in flight
+  constexpr int BUF = PIECES * 1024 + TPI * 512;  // + rank-1 fragments (512 B per tile)
+  constexpr int AHEAD = TPI >= 3 ? 2 : 3, NB = AHEAD + 1;  // chunks in flight, ring slots
   constexpr int IMGW = PIECES / 4;        // image pieces per wave per chunk
   constexpr int Q = 4;                    // queue slots per list
   constexpr float NINF = -__builtin_huge_valf();
-  static_assert(PIECES % 4 == 0 && VP <= 4, "pieces per wave");
+  static_assert(PIECES % 4 == 0 && TPI <= 4, "pieces per wave");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -180,7 +179,7 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
   bool need = false;
   int ptile = 0;
   // branch-free epilogue of a finished tile: per list, tile max -> threshold test, rej
-  auto epilogue = [&](const floatx16 (&ac)[NPB]) {
+  auto epilogue = [&](const floatx16 (&ac)[NPB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb) {
       float m = fmaxf(fmaxf(ac[pb][0], ac[pb][1]), ac[pb][2]);
@@ -193,14 +192,26 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
       need |= m > thr;
     }
   };
-  auto merge = [&](int pb) {
+  // merge a full queue into the sorted list - branch-free (a rejected or empty slot inserts -inf,
+  // which leaves the list as it is): no divergent blocks, so no copies of the lists at joins
+  auto merge = [&](int pb) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < Q; ++s) {
       const float v = qv[pb][s];
-      if (s < qn[pb]) {
-        if (v > tv[pb][KH - 1]) topk_insert_ev<KH>(tv[pb], ti[pb], v, qi[pb][s], rej[pb]);
-        else rej[pb] = fmaxf(rej[pb], v);
+      const bool has = s < qn[pb];
+      const bool ins = has && v > tv[pb][KH - 1];
+      rej[pb] = ins ? fmaxf(rej[pb], tv[pb][KH - 1]) : (has ? fmaxf(rej[pb], v) : rej[pb]);
+      const float ve = ins ? v : NINF;
+      const int id = qi[pb][s];
+#pragma unroll
+      for (int t = KH - 1; t >= 1; --t) {
+        const bool ap = ve > tv[pb][t - 1];
+        const bool ac = ve > tv[pb][t];
+        ti[pb][t] = ap ? ti[pb][t - 1] : (ac ? id : ti[pb][t]);
+        tv[pb][t] = __builtin_amdgcn_fmed3f(tv[pb][t - 1], ve, tv[pb][t]);
       }
+      ti[pb][0] = ve > tv[pb][0] ? id : ti[pb][0];
+      tv[pb][0] = fmaxf(tv[pb][0], ve);
     }
     qn[pb] = 0;
   };
@@ -209,8 +220,8 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
   // wave-uniform mask of positions holding a candidate in SOME lane, and a scalar loop visits only
   // those; the score of a visited position comes out through a select chain (no indexed registers).
   // A full queue (some lane at Q) is merged into the sorted lists right away.
-  auto select = [&](const floatx16 (&ac)[NPB], int tile) {
-    if (__builtin_amdgcn_ballot_w64(need) == 0ull) return;
+  auto select = [&](const floatx16 (&ac)[NPB], int tile) __attribute__((always_inline)) {
+    if (__builtin_amdgcn_ballot_w64(need) == 0ull || (dbg & 1)) return;
     need = false;
     const int tbase = tile * 32 + 4 * h;
 #pragma unroll
@@ -243,16 +254,24 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem);
   const char* gimg = reinterpret_cast<const char*>(image) + lane * 16;
   const char* gv = reinterpret_cast<const char*>(meta + 4) + lane * 16;
-  // this wave's DMA instructions per chunk: image pieces wave, wave + 4, ...; v piece `wave`
-  const bool vw = wave < VP;
-  auto issue = [&](int ch) {
+  // this wave's DMA instructions per chunk: image pieces wave, wave + 4, ...; the rank-1
+  // fragments of tile `wave` (512 B: one half-wave instruction)
+  const bool vw = wave < TPI;
+  // the DMA of chunk ch, part tt of TPI (image pieces pc = tt, tt + TPI, ... of this wave; the
+  // rank-1 fragments of tile tt by wave tt): spread over the tiles of the chunk being computed so the issue
+  // cost (tens of cycles per piece) sits in MFMA gaps instead of stalling at the chunk start
+  auto issue_part = [&](int ch, int tt) __attribute__((always_inline)) {
     const unsigned dst = lds0 + (ch % NB) * BUF;
 #pragma unroll
-    for (int pc = 0; pc < IMGW; ++pc) {
+    for (int pc = tt; pc < IMGW; pc += TPI) {
       const int q = wave + 4 * pc;
       lds_dma16(gimg + ((int64_t)ch * PIECES + q) * 2048, dst + q * 1024);
     }
-    if (vw) lds_dma16(gv + ((int64_t)ch * VP + wave) * 1024, dst + (PIECES + wave) * 1024);
+    if (tt == wave && lane < 32) lds_dma16(gv + ((int64_t)ch * TPI + tt) * 512, dst + PIECES * 1024 + tt * 512);
+  };
+  auto issue = [&](int ch) __attribute__((always_inline)) {
+#pragma unroll
+    for (int tt = 0; tt < TPI; ++tt) issue_part(ch, tt);
   };
   // the point fragments are in registers before the ring starts: otherwise the compiler's waits
   // for them land inside the loop (first use), where they would also wait for the DMA in flight
@@ -275,14 +294,15 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
     }
     // a raw barrier: __syncthreads() would add s_waitcnt vmcnt(0), i.e. wait for the prefetch too.
     // Past it every wave has finished chunk ch - 1, whose slot the next DMA refills.
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (!(dbg & 2)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (ch + AHEAD < nch) issue(ch + AHEAD);
-    __builtin_amdgcn_sched_barrier(0);
+    const bool refill = ch + AHEAD < nch;
     const unsigned char* buf = smem + (ch % NB) * BUF;
-    halfx8 af[2][KS];
+    // A fragments of the current tile; fragment ks is replaced by the next tile's as soon as its
+    // two MFMAs are issued, so every read has about a tile of MFMA time to land
+    halfx8 af[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) af[0][ks] = *reinterpret_cast<const halfx8*>(buf + ks * 1024 + lane * 16);
+    for (int ks = 0; ks < KS; ++ks) af[ks] = *reinterpret_cast<const halfx8*>(buf + ks * 1024 + lane * 16);
 #pragma unroll
     for (int tt = 0; tt < TPI; ++tt) {
       const int cur = tt & 1;
@@ -292,10 +312,14 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
 #pragma unroll
       for (int pb = 0; pb < NPB; ++pb) acc[cur][pb] = (floatx16)(0.f);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
         for (int pb = 0; pb < NPB; ++pb)
-          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][ks], bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+          acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[ks], bhi[pb][ks], acc[cur][pb], 0, 0, 0);
+        if (tt + 1 < TPI) af[ks] = *reinterpret_cast<const halfx8*>(buf + ((tt + 1) * KS + ks) * 1024 + lane * 16);
+        // this tile's share of the refill DMA (ring slot of chunk ch - 1: free past the barrier)
+        if (ks == (KS > 1 ? 1 : 0) && refill) issue_part(ch + AHEAD, tt);
+      }
 #pragma unroll
       for (int pb = 0; pb < NPB; ++pb)
         acc[cur][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bsx[pb], acc[cur][pb], 0, 0, 0);
@@ -304,12 +328,6 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
       for (int i = 0; i < (KS + 1) * NPB; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // then up to 2 VALU
-      }
-      // the next tile's A fragments, read under this tile's MFMAs
-      if (tt + 1 < TPI) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          af[cur ^ 1][ks] = *reinterpret_cast<const halfx8*>(buf + ((tt + 1) * KS + ks) * 1024 + lane * 16);
       }
       select(acc[cur ^ 1], ptile);
       ptile = ch * TPI + tt;
@@ -380,10 +398,10 @@ __global__ __launch_bounds__(256, 1) void h1_topk(const _Float16* __restrict__ p
 
 }  // namespace
 
-// Rows of C padded for h1_topk: whole 4-tile chunks (128 rows).
-static inline int64_t h1_kpad(int m) { return ((int64_t)m + 127) / 128 * 128; }
+// Rows of C padded for h1_topk: whole chunks of 2, 3 or 4 tiles (384 rows).
+static inline int64_t h1_kpad(int m) { return ((int64_t)m + 383) / 384 * 384; }
 
-// Workspace of ha_h1_topk (>= ha_h3_workspace_bytes(m, f): the same layout over 128-row padding).
+// Workspace of ha_h1_topk (>= ha_h3_workspace_bytes(m, f): the same layout over 384-row padding).
 HA_EXPORT int64_t ha_h1_workspace_bytes(int m, int f) {
   const int fpad = h3_fpad(f);
   if (fpad < 0 || m <= 0) return -1;
@@ -407,29 +425,40 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
   float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
+  // HEAT_H1_DEBUG (measurement only, results invalid): 1 = no selection, 2 = no chunk barrier
+  static const int dbg = getenv("HEAT_H1_DEBUG") ? atoi(getenv("HEAT_H1_DEBUG")) : 0;
   // the error bound and the uniform scale need max |c| and max u (atomicMax into zeroed words)
   if (hipMemsetAsync(meta, 0, 16, s) != hipSuccess) return HA_LAUNCH;
-#define HA_H1TK_KO(FP, KO)                                                                                     \
-  hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO>),                                       \
-                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                    \
-  hipLaunchKernelGGL((h1_topk<FP, 16, KO>), dim3(blocks), dim3(256), lds, s, p, sx, n, image, u, meta,           \
-                     kpad / 128, kn, dist, idx, cert)
+  // HEAT_H1_CFG=a (A/B): one workgroup per CU of 4 waves x 64 points, 4-tile chunks
+  static const bool cfg_a = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'a';
+#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB)                                                                  \
+  do {                                                                                                         \
+    using KC = H3Cfg<FP, NPB>;                                                                                 \
+    const size_t lds = (TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* ring slots */        \
+    const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                            \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB>),                     \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                  \
+    hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB>), dim3(blocks), dim3(256), lds, s, p, sx, n, image,  \
+                       u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                                   \
+  } while (0)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
-    using KC = H3Cfg<FP, 2>;                                                                                     \
     hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, m, f, ldc, kpad, u,  \
                        meta, (unsigned*)(meta + 4));                                                             \
     hipLaunchKernelGGL(h3_uniform_r<FP>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m, u, meta,         \
                        (unsigned*)(meta + 4));                                                                   \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),       \
                        dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                           \
-    /* 4 ring slots of 4 tiles: hi fragments + rank-1 fragments */                                               \
-    const size_t lds = 4 * ((size_t)4 * KC::KS * 1024 + 2 * 1024);                                              \
-    const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                              \
-    if (kp == 32) {                                                                                              \
-      HA_H1TK_KO(FP, 32);                                                                                        \
+    /* 2-tile chunks, 3 in flight (4-tile for f = 16: whole 1 KB image pieces per wave). Measured at */       \
+    /* f = 128 (tools/microbench/h1_ab.py): 294 ms; 3-tile chunks / 2 in flight 301 ms; one workgroup */         \
+    /* of 4 x 64 points per CU (HEAT_H1_CFG=a) 383 ms */                                                         \
+    constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
+    if (FP == 128 && cfg_a && kp == 32) {                                                                        \
+      HA_H1TK_LAUNCH(128, 32, 2, 4, 1);                                                                          \
+    } else if (kp == 32) {                                                                                       \
+      HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2);                                                                         \
     } else {                                                                                                     \
-      HA_H1TK_KO(FP, 16);                                                                                        \
+      HA_H1TK_LAUNCH(FP, 16, 1, TPB, 2);                                                                         \
     }                                                                                                            \
     break;                                                                                                       \
   }
@@ -442,6 +471,6 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
       return HA_UNSUPPORTED;
   }
 #undef HA_H1TK
-#undef HA_H1TK_KO
+#undef HA_H1TK_LAUNCH
   return ha_launch_status();
 }
