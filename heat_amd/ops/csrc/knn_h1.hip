@@ -101,8 +101,8 @@ __global__ __launch_bounds__(256) void h3_uniform_r(int k, float* __restrict__ u
 // tile max and thr the list's last entry (rej <= thr always holds): it covers every score of the
 // tile that is not queued. Queued scores that no longer beat the list at merge time go to rej
 // exactly; evictions too.
-template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB>
-__global__ __launch_bounds__(256, MINB) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
+template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
                                                   int nch, int kn, float* __restrict__ dist, int* __restrict__ idx,
@@ -113,15 +113,16 @@ __global__ __launch_bounds__(256, MINB) void h1_topk(const _Float16* __restrict_
   constexpr int PIECES = TPI * KS;        // 1 KB hi-fragment pieces per chunk (piece q <- image piece 2q)
   constexpr int BUF = PIECES * 1024 + TPI * 512;  // + rank-1 fragments (512 B per tile)
   constexpr int AHEAD = TPI >= 3 ? 2 : 3, NB = AHEAD + 1;  // chunks in flight, ring slots
-  constexpr int IMGW = PIECES / 4;        // image pieces per wave per chunk
+  constexpr int IMGW = PIECES / WAVES;    // image pieces per wave per chunk
+  constexpr int PTS_PER_WG = WAVES * NPB * 32;
   constexpr int Q = 4;                    // queue slots per list
   constexpr float NINF = -__builtin_huge_valf();
-  static_assert(PIECES % 4 == 0 && TPI <= 4, "pieces per wave");
+  static_assert(PIECES % WAVES == 0 && TPI <= WAVES, "pieces per wave");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * K::PTS_PER_WG + (int64_t)wave * (NPB * 32);
+  const int64_t pbase = (int64_t)blockIdx.x * PTS_PER_WG + (int64_t)wave * (NPB * 32);
 
   halfx8 bhi[NPB][KS];
   bf16x8 bsx[NPB];
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(256, MINB) void h1_topk(const _Float16* __restrict_
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem);
   const char* gimg = reinterpret_cast<const char*>(image) + lane * 16;
   const char* gv = reinterpret_cast<const char*>(meta + 4) + lane * 16;
-  // this wave's DMA instructions per chunk: image pieces wave, wave + 4, ...; the rank-1
+  // this wave's DMA instructions per chunk: image pieces wave, wave + WAVES, ...; the rank-1
   // fragments of tile `wave` (512 B: one half-wave instruction)
   const bool vw = wave < TPI;
   // the DMA of chunk ch, part tt of TPI (image pieces pc = tt, tt + TPI, ... of this wave; the
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256, MINB) void h1_topk(const _Float16* __restrict_
     const unsigned dst = lds0 + (ch % NB) * BUF;
 #pragma unroll
     for (int pc = tt; pc < IMGW; pc += TPI) {
-      const int q = wave + 4 * pc;
+      const int q = wave + WAVES * pc;
       lds_dma16(gimg + ((int64_t)ch * PIECES + q) * 2048, dst + q * 1024);
     }
     if (tt == wave && lane < 32) lds_dma16(gv + ((int64_t)ch * TPI + tt) * 512, dst + PIECES * 1024 + tt * 512);
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(256, MINB) void h1_topk(const _Float16* __restrict_
     // Past it every wave has finished chunk ch - 1, whose slot the next DMA refills.
     if (!(dbg & 2)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    const bool refill = ch + AHEAD < nch;
+    const bool refill = ch + AHEAD < nch && !(dbg & 4);
     const unsigned char* buf = smem + (ch % NB) * BUF;
     // A fragments of the current tile; fragment ks is replaced by the next tile's as soon as its
     // two MFMAs are issued, so every read has about a tile of MFMA time to land
@@ -425,21 +426,25 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   float* u = (float*)((char*)workspace + (int64_t)kpad * fpad * 4);
   float* meta = u + 2 * kpad;
   const _Float16* p = (const _Float16*)planes;
-  // HEAT_H1_DEBUG (measurement only, results invalid): 1 = no selection, 2 = no chunk barrier
+  // HEAT_H1_DEBUG (measurement only, results invalid): 1 = no selection, 2 = no chunk barrier,
+  // 4 = no refill DMA (the ring keeps its first chunks)
   static const int dbg = getenv("HEAT_H1_DEBUG") ? atoi(getenv("HEAT_H1_DEBUG")) : 0;
   // the error bound and the uniform scale need max |c| and max u (atomicMax into zeroed words)
   if (hipMemsetAsync(meta, 0, 16, s) != hipSuccess) return HA_LAUNCH;
   // HEAT_H1_CFG=a (A/B): one workgroup per CU of 4 waves x 64 points, 4-tile chunks
   static const bool cfg_a = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'a';
-#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB)                                                                  \
+  // HEAT_H1_CFG=w8 (A/B): one workgroup per CU of 8 waves x 32 points (half the image reads per point)
+  static const bool cfg_w8 = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'w';
+#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB, WV)                                                              \
   do {                                                                                                         \
     using KC = H3Cfg<FP, NPB>;                                                                                 \
     const size_t lds = (TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* ring slots */        \
-    const unsigned blocks = (unsigned)((n + KC::PTS_PER_WG - 1) / KC::PTS_PER_WG);                            \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB>),                     \
+    const int ppw = WV * NPB * 32;                                                                             \
+    const unsigned blocks = (unsigned)((n + ppw - 1) / ppw);                                                   \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB, WV>),                 \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                  \
-    hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB>), dim3(blocks), dim3(256), lds, s, p, sx, n, image,  \
-                       u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                                   \
+    hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB, WV>), dim3(blocks), dim3(64 * WV), lds, s, p, sx, n, \
+                       image, u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                            \
   } while (0)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
@@ -454,11 +459,13 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
     /* of 4 x 64 points per CU (HEAT_H1_CFG=a) 383 ms */                                                         \
     constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
     if (FP == 128 && cfg_a && kp == 32) {                                                                        \
-      HA_H1TK_LAUNCH(128, 32, 2, 4, 1);                                                                          \
+      HA_H1TK_LAUNCH(128, 32, 2, 4, 1, 4);                                                                       \
+    } else if (FP == 128 && cfg_w8 && kp == 32) {                                                                \
+      HA_H1TK_LAUNCH(128, 32, 1, 2, 1, 8);                                                                       \
     } else if (kp == 32) {                                                                                       \
-      HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2);                                                                         \
+      HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2, 4);                                                                      \
     } else {                                                                                                     \
-      HA_H1TK_LAUNCH(FP, 16, 1, TPB, 2);                                                                         \
+      HA_H1TK_LAUNCH(FP, 16, 1, TPB, 2, 4);                                                                      \
     }                                                                                                            \
     break;                                                                                                       \
   }
