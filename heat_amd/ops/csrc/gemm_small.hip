@@ -47,7 +47,21 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
 
   floatx4 ra[4], rb[4];
   // piece p = tid + 256 i of a stage (1024 16-byte pieces per operand)
+  // interior tiles (every stage of a slice is whole: kps is a multiple of 32) take the unguarded
+  // 16-byte loads; only edge tiles and the last partial stage evaluate per-piece bounds
+  const bool inner = m0 + GB <= M && n0 + GB <= N;
   auto gload = [&](int64_t k0) {
+    if (inner && k0 + GK <= ke) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tid + 256 * i;
+        ra[i] = !AK ? *reinterpret_cast<const floatx4*>(A + (m0 + (p >> 3)) * lda + k0 + 4 * (p & 7))
+                    : *reinterpret_cast<const floatx4*>(A + (k0 + (p >> 5)) * lda + m0 + 4 * (p & 31));
+        rb[i] = !BN ? *reinterpret_cast<const floatx4*>(B + (k0 + (p >> 5)) * ldb + n0 + 4 * (p & 31))
+                    : *reinterpret_cast<const floatx4*>(B + (n0 + (p >> 3)) * ldb + k0 + 4 * (p & 7));
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int p = tid + 256 * i;
@@ -122,22 +136,31 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
     const float* Bs = As + A_SZ;
     floatx4 fa[2][4];
     float fb[2][16];
-#pragma unroll
-    for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        fa[bm][q] = *reinterpret_cast<const floatx4*>(As + (wm * 64 + bm * 32 + r) * A_LD + 16 * h + 4 * q);
-#pragma unroll
-    for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-      for (int s = 0; s < 16; ++s) fb[bn][s] = Bs[(16 * h + s) * B_LD + wn * 64 + bn * 32 + r];
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
+    // fragments in 4 groups of 4 k-steps; group q + 1 is read while group q's 16 MFMAs run
+    // (reading all 40 first exposed the LDS latency once per stage, 38 % of wave cycles waiting)
+    auto frag = [&](int q) __attribute__((always_inline)) {
 #pragma unroll
       for (int bm = 0; bm < 2; ++bm)
+        fa[bm][q] = *reinterpret_cast<const floatx4*>(As + (wm * 64 + bm * 32 + r) * A_LD + 16 * h + 4 * q);
 #pragma unroll
-        for (int bn = 0; bn < 2; ++bn)
-          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[bm][s >> 2][s & 3], fb[bn][s], acc[bm][bn], 0, 0, 0);
+      for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+        for (int s = 4 * q; s < 4 * q + 4; ++s) fb[bn][s] = Bs[(16 * h + s) * B_LD + wn * 64 + bn * 32 + r];
+    };
+    frag(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q + 1 < 4) frag(q + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 4 * q; s < 4 * q + 4; ++s)
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[bm][q][s & 3], fb[bn][s], acc[bm][bn], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
   const int64_t nk = (ke - kb + GK - 1) / GK;

@@ -31,6 +31,6 @@ print(json.dumps({"update": os.environ["HEAT_HH_UPDATE"], "m": m, "n": n, "s": m
                   "orth": orth, "rec_200k_rows": rec}), flush=True)
 '''
 
-for upd in ("blas", "h3", "f32t"):
+for upd in (sys.argv[1:] or ["blas", "h3", "f32t", "small"]):
     env = dict(os.environ, HEAT_HH_UPDATE=upd)
     subprocess.run([sys.executable, "-u", "-c", CHILD], env=env, timeout=400)
