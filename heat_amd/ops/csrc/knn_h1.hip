@@ -21,11 +21,14 @@ __device__ __forceinline__ void vm_wait() {
 // become more conservative); the kernel waits for its transfers with counted vm_wait<N>().
 // M0 (the LDS address of the transfer) is saved and restored around it: the compiler treats M0 as
 // reserved and would not see a clobber.
+// The LDS address is wave-uniform; readfirstlane pins it to an SGPR (inside a lane-divergent
+// branch the compiler may otherwise hand the "s" operand a VGPR).
 __device__ __forceinline__ void lds_dma16(const void* g, unsigned lds) {
   unsigned saved;
+  const unsigned base = __builtin_amdgcn_readfirstlane(lds);
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(saved)
-               : "v"(g), "s"(lds)
+               : "v"(g), "s"(base)
                : "memory");
 }
 
