@@ -120,7 +120,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
   constexpr int PTS_PER_WG = WAVES * NPB * 32;
   constexpr int Q = 4;                    // queue slots per list
   constexpr float NINF = -__builtin_huge_valf();
-  static_assert(PIECES % WAVES == 0 && TPI <= WAVES, "pieces per wave");
+  static_assert(PIECES % WAVES == 0 && (TPI + 1) / 2 <= WAVES, "pieces per wave");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -258,11 +258,12 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem);
   const char* gimg = reinterpret_cast<const char*>(image) + lane * 16;
   const char* gv = reinterpret_cast<const char*>(meta + 4) + lane * 16;
-  // this wave's DMA instructions per chunk: image pieces wave, wave + WAVES, ...; the rank-1
-  // fragments of tile `wave` (512 B: one half-wave instruction)
-  const bool vw = wave < TPI;
-  // the DMA of chunk ch, part tt of TPI (image pieces pc = tt, tt + TPI, ... of this wave; the
-  // rank-1 fragments of tile tt by wave tt): spread over the tiles of the chunk being computed so the issue
+  // this wave's DMA instructions per chunk: image pieces wave, wave + WAVES, ...; rank-1 piece
+  // `wave` (1 KB = 2 tiles; a half-wave instruction for the last tile of an odd TPI)
+  constexpr int VP = (TPI + 1) / 2;
+  const bool vw = wave < VP;
+  // the DMA of chunk ch, part tt of TPI (image pieces pc = tt, tt + TPI, ... of this wave; its
+  // rank-1 piece with part 0): spread over the tiles of the chunk being computed so the issue
   // cost (tens of cycles per piece) sits in MFMA gaps instead of stalling at the chunk start
   auto issue_part = [&](int ch, int tt) __attribute__((always_inline)) {
     const unsigned dst = lds0 + (ch % NB) * BUF;
@@ -271,7 +272,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
       const int q = wave + WAVES * pc;
       lds_dma16(gimg + ((int64_t)ch * PIECES + q) * 2048, dst + q * 1024);
     }
-    if (tt == wave && lane < 32) lds_dma16(gv + ((int64_t)ch * TPI + tt) * 512, dst + PIECES * 1024 + tt * 512);
+    if (tt == 0 && vw && (2 * wave + 1 < TPI || lane < 32))
+      lds_dma16(gv + ((int64_t)ch * TPI + 2 * wave) * 512, dst + PIECES * 1024 + 2 * wave * 512);
   };
   auto issue = [&](int ch) __attribute__((always_inline)) {
 #pragma unroll
