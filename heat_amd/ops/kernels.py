@@ -1552,6 +1552,10 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
     L = lib() if native else None
     nb = L.ha_hh_nb() if native else 32
     outer = _hh_outer(native, nb)
+    if native and os.environ.get("HEAT_HH_NB"):
+        # narrower column panels inside the same outer block (A/B): each column step streams an
+        # m x nb panel, so nb = 16 halves the panel traffic for twice the in-block updates
+        nb = max(4, min(nb, int(os.environ["HEAT_HH_NB"]) // 4 * 4))
     slen = L.ha_hh_slen() if native else 2 * nb  # replicated accumulators (the host path: one)
     dev = local.device
     dt = local.dtype
