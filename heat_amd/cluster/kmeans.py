@@ -42,6 +42,12 @@ class KMeans(_KCluster):
     def _centroid_step(self, X: torch.Tensor, C: torch.Tensor, comm, distributed: bool):
         """One Lloyd step on the local block: returns (new centroids, int32 labels)."""
         k = C.shape[0]
+        if not distributed:
+            # one process: the whole step is the pass over the points + one epilogue launch
+            step = ops.kmeans_lloyd_small(X, C)
+            if step is not None:
+                labels, newC, self._step_shift = step
+                return newC, labels
         fused = ops.kmeans_step_small(X, C)   # exact fp32: serves both precisions
         if fused is not None:   # few clusters: assignment and sums in one pass over the points
             labels, sums, counts = fused

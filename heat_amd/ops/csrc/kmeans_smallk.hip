@@ -574,6 +574,66 @@ __global__ __launch_bounds__(256) void ks_reduce(const float* __restrict__ sums_
   }
 }
 
+// The Lloyd epilogue fused into the partial-sum reduction (world of one): every block reduces one
+// sum / count like ks_reduce, in fp64, into `red`; the last block to arrive (self-resetting counter)
+// forms the new centroids (empty clusters keep theirs), the squared shift (fp64, fixed order) and
+// the padded centroid chunks of the NEXT pass in place of this pass's. One launch instead of
+// ks_reduce + km_finalize + the next pass's ks_pad_centroids: measured, every extra small launch
+// between two passes over the points made the next pass slower (a fit loop with the separate
+// finalize alternated 0.58 / 0.71 ms per pass, back-to-back passes ran 0.62 ms; tools/microbench/
+// smallk_fitloop2.py).
+template <int KP>
+__global__ __launch_bounds__(256) void ks_reduce_fin(const float* __restrict__ sums_part,
+                                                     const float* __restrict__ counts_part, int nblk, int k, int f,
+                                                     const float* __restrict__ C, int64_t ldc, float* __restrict__ newC,
+                                                     double* __restrict__ shift, double* __restrict__ red,
+                                                     unsigned* __restrict__ arrived, float* __restrict__ cpad) {
+  __shared__ double wred[4];
+  __shared__ bool last;
+  const int e = blockIdx.x;
+  const int kf = k * f;
+  const bool is_sum = e < kf;
+  const int c = is_sum ? e / f : e - kf, j = is_sum ? e - c * f : 0;
+  double a = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 256)
+    a += is_sum ? (double)sums_part[((int64_t)b * KP + c) * KS_FMAX + j] : (double)counts_part[(int64_t)b * KP + c];
+  a = ha_wave_sum_d(a);
+  if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    red[e] = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+    __threadfence();
+    last = atomicAdd(arrived, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < kf; i += 256) {
+    const int ci = i / f, ji = i - ci * f;
+    const double cnt = red[kf + ci];
+    const float old = C[(int64_t)ci * ldc + ji];
+    const float nv = cnt > 0.0 ? (float)(red[i] / cnt) : old;
+    newC[i] = nv;
+    const double d = (double)old - (double)nv;
+    acc = fma(d, d, acc);
+  }
+  acc = ha_wave_sum_d(acc);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = acc;
+  __syncthreads();  // also: newC of every thread of this block is visible below
+  if (threadIdx.x == 0) {
+    *shift = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+    *arrived = 0u;  // ready for the next launch on this workspace
+  }
+  // the next pass's padded chunks (ks_pad_centroids' layout) from the new centroids
+  const int fp = ks_fp(f);
+  for (int e2 = threadIdx.x; e2 < KP * (fp + 4); e2 += 256) {
+    const int q = e2 / (4 * KP), c2 = (e2 / 4) % KP, j2 = 4 * q + (e2 & 3);
+    cpad[e2] = c2 < k ? (j2 < f ? newC[c2 * f + j2] : 0.f) : (j2 == 0 ? __builtin_huge_valf() : 0.f);
+  }
+}
+
 int ks_kp(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : 16; }
 
 template <int KP, int MODE, bool U>
@@ -590,9 +650,21 @@ void ks_launch_generic(int nblk, hipStream_t s, const float* X, int64_t n, int f
 // one pass: ks_step64 over the whole tiles when it applies (f = 64, aligned rows) plus the
 // generic kernel on the remaining rows as ONE extra partial slot, else the generic kernel alone;
 // then the fp64 reduction of the partials
+// Fused Lloyd epilogue of ha_ks_lloyd (null: the plain sums / counts reduction)
+struct KsFin {
+  const float* C;
+  int64_t ldc;
+  float* newC;
+  double* shift;
+  double* red;
+  unsigned* arrived;
+  float* cpad;
+};
+
 template <int KP, bool U>
 void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, int f, int64_t ldx, const float* cpad,
-               int* labels, float* mind, float* sp, float* cp, int k, float* sums, float* counts) {
+               int* labels, float* mind, float* sp, float* cp, int k, float* sums, float* counts,
+               const KsFin* fin = nullptr) {
   int nblk = 0;
   int64_t done = 0;
   if (mode == KS_ROW4 && f == KS_FMAX) {
@@ -643,7 +715,11 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
       ks_launch_generic<KP, KS_SCALAR, U>(g, s, Xr, rest, f, ldx, cpad, lr, mr, spr, cpr);
     nblk += g;
   }
-  if (U) hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, sums, counts);
+  if (U && fin)
+    hipLaunchKernelGGL((ks_reduce_fin<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, fin->C,
+                       fin->ldc, fin->newC, fin->shift, fin->red, fin->arrived, fin->cpad);
+  else if (U)
+    hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, sums, counts);
 }
 
 // partial slots: up to 9 per CU + one for the tail rows of the f = 64 kernels
@@ -696,5 +772,45 @@ HA_EXPORT int ha_ks_step(const float* X, int64_t n, int f, int64_t ldx, const fl
     HA_KS(16)
   }
 #undef HA_KS
+  return ha_launch_status();
+}
+
+// Workspace floats of ha_ks_lloyd: ha_ks_workspace_floats + the fp64 reduction (k f + k) and the
+// arrival counter. Zero it once (the counter self-resets); keep it between the calls of one fit.
+HA_EXPORT int64_t ha_ks_lloyd_workspace_floats(int k, int num_cus) {
+  const int64_t base = ha_ks_workspace_floats(k, num_cus);
+  if (base < 0) return -1;
+  return base + 2 * ((int64_t)k * KS_FMAX + k) + 4;
+}
+
+// One Lloyd step for few clusters on a world of one (k <= 16, f <= 64): labels (int32, optional),
+// newC [k, f] (contiguous) = the means of the assigned points (empty clusters keep their centroid),
+// shift = sum (C - newC)^2 (fp64). pad_ready != 0: the workspace already holds the padded chunks of
+// C (the previous call's newC, written by its epilogue) - no pad launch.
+HA_EXPORT int ha_ks_lloyd(const float* X, int64_t n, int f, int64_t ldx, const float* C, int k, int64_t ldc,
+                          int* labels, float* newC, double* shift, float* workspace, int num_cus, int pad_ready,
+                          void* stream) {
+  if (k <= 0 || k > 16 || f <= 0 || f > KS_FMAX || ldx < f || ldc < f || num_cus <= 0 || n <= 0) return HA_BAD_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int kp = ks_kp(k);
+  const bool al = ((uintptr_t)X & 15) == 0;
+  const int mode = (f % 4 == 0 && ldx % 4 == 0 && al) ? KS_ROW4 : (ldx == f && f >= 4 && al) ? KS_FLAT : KS_SCALAR;
+  const int64_t slots = ks_slots(num_cus);
+  float* sp = workspace;
+  float* cp = workspace + slots * kp * KS_FMAX;
+  float* cpad = workspace + slots * kp * (KS_FMAX + 1);
+  double* red = reinterpret_cast<double*>(workspace + ha_ks_workspace_floats(k, num_cus) + 1);
+  red = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(red) + 7) & ~(uintptr_t)7);
+  unsigned* arrived = reinterpret_cast<unsigned*>(red + (int64_t)k * KS_FMAX + k);
+  if (!pad_ready)
+    hipLaunchKernelGGL(ks_pad_centroids, dim3((unsigned)((kp * (ks_fp(f) + 4) + 255) / 256)), dim3(256), 0, s, C, k,
+                       f, ldc, kp, cpad);
+  const KsFin fin{C, ldc, newC, shift, red, arrived, cpad};
+  if (kp == 4)
+    ks_launch<4, true>(mode, num_cus, s, X, n, f, ldx, cpad, labels, nullptr, sp, cp, k, nullptr, nullptr, &fin);
+  else if (kp == 8)
+    ks_launch<8, true>(mode, num_cus, s, X, n, f, ldx, cpad, labels, nullptr, sp, cp, k, nullptr, nullptr, &fin);
+  else
+    ks_launch<16, true>(mode, num_cus, s, X, n, f, ldx, cpad, labels, nullptr, sp, cp, k, nullptr, nullptr, &fin);
   return ha_launch_status();
 }

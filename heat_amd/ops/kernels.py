@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import weakref
 import os
 import threading
 from typing import NamedTuple, Optional, Tuple
@@ -17,7 +18,7 @@ import torch.nn.functional as F
 from . import check, lib, stream_ptr, use_native
 
 __all__ = ["kmeans_finalize", "pack_blocks", "unpack_blocks", "pack_supported", "kmeans_assign", "kmeans_pack_points", "PackedPoints", "cdist_pack", "PackedRows", "kmeans_update", "moments", "merge_moments", "num_cus", "cdist", "lasso_epoch", "lasso_prepare", "LassoSweep", "gemm_f16x3",
-           "split_planes", "gram_product", "gemm_f32_small", "knn_topk", "kmeans_step_small", "lasso_gram", "lasso_cd", "argreduce_keys",
+           "split_planes", "gram_product", "gemm_f32_small", "knn_topk", "kmeans_step_small", "kmeans_lloyd_small", "lasso_gram", "lasso_cd", "argreduce_keys",
            "argreduce_decode", "argreduce_supported", "topk_rows", "gemm_f32", "gemm_h3", "h3_planes", "H3Planes",
            "gemm_h3_planes", "gemm64", "cholesky_upper", "tri_inv_upper", "householder_qr",
            "householder_factor", "householder_apply", "householder_block", "vtc64", "gram64",
@@ -108,6 +109,44 @@ def _ks_step(X: torch.Tensor, C: torch.Tensor, want_mind: bool, update: bool):
     check(L.ha_ks_step(_ptr(X), n, f, X.stride(0), _ptr(Cc), k, Cc.stride(0), _ptr(labels), _ptr(mind), _ptr(sums),
                        _ptr(counts), _ptr(ws), ncu, ctypes.c_void_p(stream_ptr(dev))), "ha_ks_step")
     return labels, mind, sums, counts
+
+
+_KS_LLOYD = {}   # (device, k) -> [workspace, (data_ptr, version) of the centroids padded in it]
+
+
+def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+    """One whole Lloyd step for few clusters on ONE process (k <= 16, f <= 64, device fp32): (int32
+    labels, new centroids [k, f] fp32, squared shift 0-d fp64) from one pass over the points plus ONE
+    epilogue launch (``csrc/kmeans_smallk.hip: ha_ks_lloyd`` - reduction, new centroids, shift and
+    the next pass's padded centroids), instead of the pass's reduction + ``kmeans_finalize`` + the
+    next pass's padding. None where it does not apply."""
+    if not _small_k_ok(X, C.shape[0]) or X.shape[0] == 0 or not hasattr(lib(), "ha_ks_lloyd"):
+        return None
+    if torch.cuda.is_current_stream_capturing():
+        return None   # the pad reuse below is host state: not for graph capture
+    L = lib()
+    n, f = X.shape
+    k = C.shape[0]
+    dev = X.device
+    Cc = C.to(device=dev, dtype=torch.float32)
+    Cc = Cc if Cc.stride(-1) == 1 else Cc.contiguous()
+    ncu = num_cus(dev)
+    state = _KS_LLOYD.get((dev, k))
+    if state is None:
+        ws = torch.zeros(max(1, L.ha_ks_lloyd_workspace_floats(k, ncu)), dtype=torch.float32, device=dev)
+        state = _KS_LLOYD[(dev, k)] = [ws, None]
+    # the padded chunks in the workspace belong to the previous call's newC: valid for this call
+    # only if C IS that tensor object (alive, unmodified) - an address match alone could be a new
+    # tensor in the freed block
+    prev = state[1]
+    pad_ready = prev is not None and prev[0]() is Cc and prev[1] == Cc._version
+    labels = torch.empty(n, dtype=torch.int32, device=dev)
+    newC = torch.empty((k, f), dtype=torch.float32, device=dev)
+    shift = torch.empty((), dtype=torch.float64, device=dev)
+    check(L.ha_ks_lloyd(_ptr(X), n, f, X.stride(0), _ptr(Cc), k, Cc.stride(0), _ptr(labels), _ptr(newC), _ptr(shift),
+                        _ptr(state[0]), ncu, int(pad_ready), ctypes.c_void_p(stream_ptr(dev))), "ha_ks_lloyd")
+    state[1] = (weakref.ref(newC), newC._version)
+    return labels, newC, shift
 
 
 def kmeans_step_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:

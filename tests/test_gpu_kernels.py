@@ -906,6 +906,40 @@ def test_kmeans_step_small(n, f, k):
         assert torch.equal(counts.long(), torch.bincount(lab.long(), minlength=k))
 
 
+@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (129, 64), (100000, 64)])
+@pytest.mark.parametrize("k", [1, 3, 8, 16])
+def test_kmeans_lloyd_small(n, f, k):
+    """One-launch-epilogue Lloyd step: new centroids == fp64 means of the assigned points (an empty
+    cluster keeps its centroid), shift == sum of squared moves, labels == fp64 argmin; chained calls
+    reuse the padded centroids the previous epilogue wrote, and an in-place change of C or a new
+    tensor is noticed."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + 7 * k + f)
+    X = torch.randn(n, f, generator=g).to(dev)
+    C = torch.randn(k, f, generator=g).to(dev)
+    if k > 1:
+        C[-1] = 1e4   # far away: empty cluster
+    for it in range(4):
+        lab, newC, shift = ops.kmeans_lloyd_small(X, C)
+        d = torch.cdist(X.double(), C.double()) ** 2
+        chosen = d.gather(1, lab.long().unsqueeze(1)).squeeze(1)
+        assert torch.all(chosen - d.min(1).values <= 1e-5 * (1 + d.min(1).values))
+        cnt = torch.bincount(lab.long(), minlength=k).double()
+        sums = torch.zeros(k, f, dtype=torch.float64, device=dev).index_add_(0, lab.long(), X.double())
+        ref = torch.where(cnt.unsqueeze(1) > 0, sums / cnt.clamp(min=1).unsqueeze(1), C.double())
+        assert torch.allclose(newC.double(), ref, rtol=1e-5, atol=1e-6)
+        if k > 1:
+            assert torch.equal(newC[-1], C[-1])
+        assert abs(float(shift) - float(((newC.double() - C.double()) ** 2).sum())) <= 1e-6 * (1 + float(shift))
+        if it == 1:
+            newC.mul_(0.5)          # in place: the padded copy is stale, must be rebuilt
+        elif it == 2:
+            newC = newC.clone()     # another tensor with the same values
+        C = newC
+
+
 @pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (3000, 128), (777, 200)])
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
 def test_kmeans_assign_small_k(n, f, k):
