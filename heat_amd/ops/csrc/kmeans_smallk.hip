@@ -587,40 +587,14 @@ __global__ __launch_bounds__(256) void ks_reduce_fin(const float* __restrict__ s
                                                      const float* __restrict__ counts_part, int nblk, int k, int f,
                                                      const float* __restrict__ C, int64_t ldc, float* __restrict__ newC,
                                                      double* __restrict__ shift, double* __restrict__ red,
-                                                     unsigned* __restrict__ arrived, float* __restrict__ cpad,
-                                                     const float* __restrict__ X, int64_t ldx, int64_t row0, int rest,
-                                                     int* __restrict__ labels) {
+                                                     unsigned* __restrict__ arrived, float* __restrict__ cpad) {
   __shared__ double wred[4];
   __shared__ bool last;
-  __shared__ int tl[64];
   const int e = blockIdx.x;
   const int kf = k * f;
   const bool is_sum = e < kf;
   const int c = is_sum ? e / f : e - kf, j = is_sum ? e - c * f : 0;
-  // the < 64 rows after the last whole 64-row tile (no separate launch for them): every block
-  // assigns them (k f multiply-adds per row) and adds its own sum / count over them
-  if (rest > 0 && threadIdx.x < rest) {
-    const float* xr = X + (row0 + threadIdx.x) * ldx;
-    float best = __builtin_huge_valf();
-    int bi = 0;
-    for (int cc = 0; cc < k; ++cc) {
-      float d = 0.f;
-      for (int jj = 0; jj < f; ++jj) {
-        const float t = xr[jj] - C[(int64_t)cc * ldc + jj];
-        d = fmaf(t, t, d);
-      }
-      if (d < best) {
-        best = d;
-        bi = cc;
-      }
-    }
-    tl[threadIdx.x] = bi;
-    if (e == 0 && labels) labels[row0 + threadIdx.x] = bi;
-  }
-  if (rest > 0) __syncthreads();
   double a = 0.0;
-  if (threadIdx.x < rest && tl[threadIdx.x] == c)
-    a = is_sum ? (double)X[(row0 + threadIdx.x) * ldx + j] : 1.0;
   for (int b = threadIdx.x; b < nblk; b += 256)
     a += is_sum ? (double)sums_part[((int64_t)b * KP + c) * KS_FMAX + j] : (double)counts_part[(int64_t)b * KP + c];
   a = ha_wave_sum_d(a);
@@ -685,7 +659,6 @@ struct KsFin {
   double* red;
   unsigned* arrived;
   float* cpad;
-  int* labels;
 };
 
 template <int KP, bool U>
@@ -726,9 +699,7 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
     }
   }
   const int64_t rest = n - done;
-  // fused epilogue after whole 64-row tiles: it takes the (< 64) remaining rows itself
-  const bool tail_in_fin = U && fin && done > 0 && rest < 64;
-  if (rest > 0 && !tail_in_fin) {
+  if (rest > 0) {
     const int64_t ntiles = (rest + KS_ROWS - 1) / KS_ROWS;
     const int g = done > 0 ? 1 : (int)(ntiles < 4 * num_cus ? ntiles : 4 * num_cus);
     const float* Xr = X + done * ldx;
@@ -746,8 +717,7 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
   }
   if (U && fin)
     hipLaunchKernelGGL((ks_reduce_fin<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, fin->C,
-                       fin->ldc, fin->newC, fin->shift, fin->red, fin->arrived, fin->cpad, X, ldx, done,
-                       tail_in_fin ? (int)rest : 0, fin->labels);
+                       fin->ldc, fin->newC, fin->shift, fin->red, fin->arrived, fin->cpad);
   else if (U)
     hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, sums, counts);
 }
@@ -835,7 +805,7 @@ HA_EXPORT int ha_ks_lloyd(const float* X, int64_t n, int f, int64_t ldx, const f
   if (!pad_ready)
     hipLaunchKernelGGL(ks_pad_centroids, dim3((unsigned)((kp * (ks_fp(f) + 4) + 255) / 256)), dim3(256), 0, s, C, k,
                        f, ldc, kp, cpad);
-  const KsFin fin{C, ldc, newC, shift, red, arrived, cpad, labels};
+  const KsFin fin{C, ldc, newC, shift, red, arrived, cpad};
   if (kp == 4)
     ks_launch<4, true>(mode, num_cus, s, X, n, f, ldx, cpad, labels, nullptr, sp, cp, k, nullptr, nullptr, &fin);
   else if (kp == 8)
