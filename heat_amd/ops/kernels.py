@@ -111,7 +111,7 @@ def _ks_step(X: torch.Tensor, C: torch.Tensor, want_mind: bool, update: bool):
     return labels, mind, sums, counts
 
 
-_KS_LLOYD = {}   # (device, k) -> [workspace, (data_ptr, version) of the centroids padded in it]
+_KS_LLOYD = {}   # (device, stream, k) -> [workspace, (weakref, version) of the centroids padded in it]
 
 
 def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
@@ -131,10 +131,13 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch
     Cc = C.to(device=dev, dtype=torch.float32)
     Cc = Cc if Cc.stride(-1) == 1 else Cc.contiguous()
     ncu = num_cus(dev)
-    state = _KS_LLOYD.get((dev, k))
+    sp = stream_ptr(dev)
+    # one workspace per stream: launches on one stream are ordered, so its partial slots, arrival
+    # counter and padded centroids are never used by two passes at once
+    state = _KS_LLOYD.get((dev, sp, k))
     if state is None:
         ws = torch.zeros(max(1, L.ha_ks_lloyd_workspace_floats(k, ncu)), dtype=torch.float32, device=dev)
-        state = _KS_LLOYD[(dev, k)] = [ws, None]
+        state = _KS_LLOYD[(dev, sp, k)] = [ws, None]
     # the padded chunks in the workspace belong to the previous call's newC: valid for this call
     # only if C IS that tensor object (alive, unmodified) - an address match alone could be a new
     # tensor in the freed block
@@ -144,7 +147,7 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch
     newC = torch.empty((k, f), dtype=torch.float32, device=dev)
     shift = torch.empty((), dtype=torch.float64, device=dev)
     check(L.ha_ks_lloyd(_ptr(X), n, f, X.stride(0), _ptr(Cc), k, Cc.stride(0), _ptr(labels), _ptr(newC), _ptr(shift),
-                        _ptr(state[0]), ncu, int(pad_ready), ctypes.c_void_p(stream_ptr(dev))), "ha_ks_lloyd")
+                        _ptr(state[0]), ncu, int(pad_ready), ctypes.c_void_p(sp)), "ha_ks_lloyd")
     state[1] = (weakref.ref(newC), newC._version)
     return labels, newC, shift
 
