@@ -252,6 +252,10 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
   }
   const int jl = j & 3, jq = j >> 2;              // lane group slot holding column j
   const bool wr = 4 * q + 3 >= j;  // columns < j are read (sums), never changed: no store
+  // Y null: the caller forms V^T V itself (one GEMM after the panel), so the finished columns
+  // (all 4 of this lane's < j) are not even loaded - the column steps stream only the part of the
+  // panel still changing (their S / rowd entries are left zero and unused)
+  const bool skip = Y == nullptr && !wr;
   const int j1 = j + 1, j1l = j1 & 3, j1q = j1 >> 2;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * 32;
@@ -260,7 +264,14 @@ __global__ __launch_bounds__(256) void hh_step(T* __restrict__ A, int64_t m, int
 #pragma unroll
     for (int u = 0; u < HH_ROWS; ++u) {
       const int64_t i = i0 + u * stride;
-      if (i < m && g0 + i >= d) a[u] = hh_load4(A + i * lda + coff + 4 * q, nh);
+      if (i < m && g0 + i >= d) {
+        if (skip) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) a[u].v[c] = (T)0;
+        } else {
+          a[u] = hh_load4(A + i * lda + coff + 4 * q, nh);
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < HH_ROWS; ++u) {
@@ -415,7 +426,9 @@ HA_EXPORT int ha_hh_colsums(const void* A, int dtype, int64_t m, int64_t lda, in
 // Reflector j of the panel (see the header); Sout (zeroed, 2 NB doubles) receives column j + 1's
 // partial sums unless it is null.
 // coff: the panel's first column within a row of A (k0 for the matrix itself, 0 for a compact
-// panel copy); Y (nullable, ncols x ncols fp64 row-major): receives column j of V^T V.
+// panel copy); Y (nullable, ncols x ncols fp64 row-major): receives column j of V^T V. Y null:
+// the finished columns (< j) are not loaded and their S entries stay zero (the caller computes
+// V^T V after the panel).
 HA_EXPORT int ha_hh_step(void* A, int dtype, int64_t m, int64_t lda, int64_t g0, int64_t k0, int64_t coff, int ncols,
                          int j, const double* Sin, double* Sout, void* tau, double* Y, double* part, unsigned* cnt,
                          void* stream) {

@@ -1564,6 +1564,11 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
     return Q * d.unsqueeze(0), R
 
 
+# Column steps skip the panel's finished columns and V^T V is one GEMM after the panel
+# (HEAT_HH_SKIP=0: the round-4 in-kernel V^T V, every step streams the whole m x 32 panel)
+_HH_SKIP = os.environ.get("HEAT_HH_SKIP", "1") != "0"
+
+
 def _hh_outer(native: bool, nb: int) -> int:
     """Width of the aggregated block reflector of the two-level Householder factorisation: the
     trailing matrix is updated once per outer block (W = V^T C on the fp64 matrix cores, then one
@@ -1635,8 +1640,8 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
                 last = j + 1 == nc
                 if native:
                     check(L.ha_hh_step(_ptr(Pb), code, m_r, nc, g0, k0, 0, nc, j, _ptr(S[j]),
-                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau), _ptr(Y), _ptr(hpart),
-                                       _ptr(hcnt), st), "ha_hh_step")
+                                       _ptr(None) if last else _ptr(S[j + 1]), _ptr(tau),
+                                       _ptr(None) if _HH_SKIP else _ptr(Y), _ptr(hpart), _ptr(hcnt), st), "ha_hh_step")
                 else:
                     _hh_step_host(A, rows, k0, nc, j, S[j], None if last else S[j + 1], tau, Y)
                 if not last:
@@ -1648,6 +1653,11 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
             else:
                 V = _hh_v(A, rows, k0, nc, g0)
             Tm = torch.empty((nc, nc), dtype=dt, device=dev)
+            if native and _HH_SKIP:
+                # V^T V in one pass over the finished panel (the steps skipped the done columns)
+                Y = _vtc(V, V, native, st)
+                red(Y)
+                Y = Y.contiguous()
             if native:
                 check(L.ha_hh_larft(_ptr(Y), _ptr(tau), nc, code, _ptr(Tm), st), "ha_hh_larft")
             else:
