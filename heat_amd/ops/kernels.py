@@ -1564,9 +1564,10 @@ def householder_qr(local: torch.Tensor, g0: int, m_total: int, calc_q: bool = Tr
     return Q * d.unsqueeze(0), R
 
 
-# Column steps skip the panel's finished columns and V^T V is one GEMM after the panel
-# (HEAT_HH_SKIP=0: the round-4 in-kernel V^T V, every step streams the whole m x 32 panel)
-_HH_SKIP = os.environ.get("HEAT_HH_SKIP", "1") != "0"
+# HEAT_HH_SKIP=1 (A/B): the column steps skip the panel's finished columns and V^T V is one GEMM
+# after the panel. Measured 1.25e6 x 4096 QR: 1.41 s vs 1.29 s for the default (the per-panel
+# V^T V launches cost more than the skipped loads save; `profiles/hh_profile_r05.txt`)
+_HH_SKIP = os.environ.get("HEAT_HH_SKIP", "0") == "1"
 
 
 def _hh_outer(native: bool, nb: int) -> int:
