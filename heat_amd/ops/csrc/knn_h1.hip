@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void h3_uniform_r(int k, float* __restrict__ u
 // tile max and thr the list's last entry (rej <= thr always holds): it covers every score of the
 // tile that is not queued. Queued scores that no longer beat the list at merge time go to rej
 // exactly; evictions too.
-template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB, int WAVES = 4>
+template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB, int WAVES = 4, bool PAIRB = false>
 __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
@@ -115,7 +115,9 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
   // NPB: 32-point blocks per wave; TPI: 32-centroid tiles per staged chunk; MINB: workgroups / CU
   constexpr int PIECES = TPI * KS;        // 1 KB hi-fragment pieces per chunk (piece q <- image piece 2q)
   constexpr int BUF = PIECES * 1024 + TPI * 512;  // + rank-1 fragments (512 B per tile)
-  constexpr int AHEAD = TPI >= 3 ? 2 : 3, NB = AHEAD + 1;  // chunks in flight, ring slots
+  // chunks in flight, ring slots. PAIRB: one barrier per PAIR of chunks (both landed), chunk
+  // ch + 2 issued during chunk ch (the barrier waits are a quarter of a chunk's time: stamps)
+  constexpr int AHEAD = PAIRB ? 2 : TPI >= 3 ? 2 : 3, NB = PAIRB ? 4 : AHEAD + 1;
   constexpr int IMGW = PIECES / WAVES;    // image pieces per wave per chunk
   constexpr int PTS_PER_WG = WAVES * NPB * 32;
   constexpr int Q = 4;                    // queue slots per list
@@ -254,6 +256,21 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
     }
   };
 
+#ifdef HEAT_H1_STAMPS
+  // measurement build only (tools/probes/h1_stamps.py): s_memtime per phase of chunks
+  // [H1S_CH0, H1S_CH0 + H1S_NCH) of the waves of workgroups 0..7, into `idx` (not written then)
+  constexpr int H1S_CH0 = 2000, H1S_NCH = 64, H1S_NPH = 8;
+  unsigned* h1s_out = reinterpret_cast<unsigned*>(idx);
+  auto stamp = [&](int ch, int ph) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned t = (unsigned)__builtin_amdgcn_s_memtime();
+    if (blockIdx.x < 8 && ch >= H1S_CH0 && ch < H1S_CH0 + H1S_NCH && lane == 0)
+      h1s_out[(((int)blockIdx.x * WAVES + wave) * H1S_NCH + (ch - H1S_CH0)) * H1S_NPH + ph] = t;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#else
+  auto stamp = [](int, int) {};
+#endif
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem);
   const char* gimg = reinterpret_cast<const char*>(image) + lane * 16;
@@ -287,9 +304,12 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
     if (c < nch) issue(c);
   for (int ch = 0; ch < nch; ++ch) {
     __builtin_amdgcn_sched_barrier(0);
+    stamp(ch, 0);
     // this wave's pieces of chunk ch have landed once at most the later chunks' are outstanding
     const int later = min(nch - 1 - ch, AHEAD - 1);
-    if (later >= 2) {
+    if (PAIRB) {
+      if ((ch & 1) == 0) vm_wait<0>();   // chunks ch and ch + 1: everything outstanding
+    } else if (later >= 2) {
       if (vw) vm_wait<2 * IMGW + 2>();
       else vm_wait<2 * IMGW>();
     } else if (later == 1) {
@@ -300,8 +320,10 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
     }
     // a raw barrier: __syncthreads() would add s_waitcnt vmcnt(0), i.e. wait for the prefetch too.
     // Past it every wave has finished chunk ch - 1, whose slot the next DMA refills.
-    if (!(dbg & 2)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stamp(ch, 1);
+    if (!(dbg & 2) && (!PAIRB || (ch & 1) == 0)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    stamp(ch, 2);
     const bool refill = ch + AHEAD < nch && !(dbg & 4);
     const unsigned char* buf = smem + (ch % NB) * BUF;
     // A fragments of the current tile; fragment ks is replaced by the next tile's as soon as its
@@ -335,7 +357,9 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // then up to 2 VALU
       }
+      stamp(ch, 3 + 2 * tt);
       select(acc[cur ^ 1], ptile);
+      stamp(ch, 4 + 2 * tt);
       ptile = ch * TPI + tt;
     }
   }
@@ -395,7 +419,9 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
       for (int s2 = 0; s2 < KO; ++s2) {
         const bool ok = mi[s2] >= 0;
         dist[pi * KO + s2] = ok ? fmaxf(xs * isx * isx - 2.f * mv[s2] * isx, 0.f) : __builtin_huge_valf();
+#ifndef HEAT_H1_STAMPS
         idx[pi * KO + s2] = mi[s2];
+#endif
       }
       cert[pi] = (ikn >= 0 && rej[pb] < akn - 2.f * E) ? 1 : 0;
     }
@@ -440,17 +466,20 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   static const bool cfg_a = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'a';
   // HEAT_H1_CFG=w8 (A/B): one workgroup per CU of 8 waves x 32 points (half the image reads per point)
   static const bool cfg_w8 = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'w';
-#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB, WV)                                                              \
+  // HEAT_H1_CFG=b (A/B): one barrier per chunk instead of per pair of chunks
+  static const bool cfg_b = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'b';
+#define HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, PB)                                                        \
   do {                                                                                                         \
     using KC = H3Cfg<FP, NPB>;                                                                                 \
-    const size_t lds = (TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* ring slots */        \
+    const size_t lds = (!PB && TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* ring slots */ \
     const int ppw = WV * NPB * 32;                                                                             \
     const unsigned blocks = (unsigned)((n + ppw - 1) / ppw);                                                   \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB, WV>),                 \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB, WV, PB>),             \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                  \
-    hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB, WV>), dim3(blocks), dim3(64 * WV), lds, s, p, sx, n, \
-                       image, u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                            \
+    hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB, WV, PB>), dim3(blocks), dim3(64 * WV), lds, s, p,   \
+                       sx, n, image, u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                     \
   } while (0)
+#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB, WV) HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, false)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
     hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, m, f, ldc, kpad, u,  \
@@ -459,18 +488,22 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
                        (unsigned*)(meta + 4));                                                                   \
     hipLaunchKernelGGL(h3_pack_centroids<FP>, dim3((unsigned)(((int64_t)kpad * (FP / 8) + 255) / 256)),       \
                        dim3(256), 0, s, C, m, f, ldc, kpad, image, u);                                           \
-    /* 2-tile chunks, 3 in flight (4-tile for f = 16: whole 1 KB image pieces per wave). Measured at */       \
-    /* f = 128 (tools/microbench/h1_ab.py): 294 ms; 3-tile chunks / 2 in flight 301 ms; one workgroup */         \
-    /* of 4 x 64 points per CU (HEAT_H1_CFG=a) 383 ms */                                                         \
+    /* 2-tile chunks, one barrier per pair of chunks, chunk ch + 2 issued during ch (4-tile chunks, one */   \
+    /* barrier each, 3 in flight for f = 16: whole 1 KB image pieces per wave). Measured at f = 128 */            \
+    /* (tools/microbench/h1_ab.py, one box): pair 309-310 ms, per-chunk barrier (HEAT_H1_CFG=b) 313-315; */     \
+    /* 3-tile chunks / 2 in flight +2%; one workgroup of 4 x 64 points per CU (HEAT_H1_CFG=a) +30% */           \
     constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
+    constexpr bool PAIR = TPB == 2;                                                                              \
     if (FP == 128 && cfg_a && kp == 32) {                                                                        \
       HA_H1TK_LAUNCH(128, 32, 2, 4, 1, 4);                                                                       \
     } else if (FP == 128 && cfg_w8 && kp == 32) {                                                                \
       HA_H1TK_LAUNCH(128, 32, 1, 2, 1, 8);                                                                       \
-    } else if (kp == 32) {                                                                                       \
+    } else if (cfg_b && kp == 32) {                                                                              \
       HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2, 4);                                                                      \
+    } else if (kp == 32) {                                                                                       \
+      HA_H1TK_LAUNCH_X(FP, 32, 1, TPB, 2, 4, PAIR);                                                              \
     } else {                                                                                                     \
-      HA_H1TK_LAUNCH(FP, 16, 1, TPB, 2, 4);                                                                      \
+      HA_H1TK_LAUNCH_X(FP, 16, 1, TPB, 2, 4, PAIR);                                                              \
     }                                                                                                            \
     break;                                                                                                       \
   }
@@ -484,5 +517,6 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   }
 #undef HA_H1TK
 #undef HA_H1TK_LAUNCH
+#undef HA_H1TK_LAUNCH_X
   return ha_launch_status();
 }
