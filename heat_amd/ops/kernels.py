@@ -1325,6 +1325,10 @@ def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
 
 _GRAM_KCHUNK = max(16, int(os.environ.get("HEAT_GRAM_KCHUNK", "4096")) // 16 * 16)
 _GRAM_PARTIAL_BYTES = 1 << 30
+# K slice of the Gram behind ht.matmul(X.T, X) (fp32 result): 16384 rows per fp32 slice sum, a
+# quarter of the partial-sum traffic of CholeskyQR's 4096 (1.25e6 x 4096, tools/r5/gpu_gramk.sh:
+# 172 / 166 / 163 / 164 ms at 4096 / 8192 / 16384 / 32768) - still far finer than one fp32 sum
+_GRAM_MATMUL_KCHUNK = max(16, int(os.environ.get("HEAT_GRAM_MATMUL_KCHUNK", "16384")) // 16 * 16)
 
 
 def gram_product(a: torch.Tensor, b: torch.Tensor) -> Optional[torch.Tensor]:
@@ -1336,16 +1340,17 @@ def gram_product(a: torch.Tensor, b: torch.Tensor) -> Optional[torch.Tensor]:
     if not (a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32:
         return None
     if _is_gram(a, b):
-        g = gram64(b)
+        g = gram64(b, kchunk=_GRAM_MATMUL_KCHUNK)
     elif _is_gram(b, a):
-        g = gram64(a, rows=True)
+        g = gram64(a, rows=True, kchunk=_GRAM_MATMUL_KCHUNK)
     else:
         return None
     u = torch.triu(g)
     return (u + torch.triu(u, 1).t()).float()
 
 
-def gram64(x: torch.Tensor, exact: Optional[bool] = None, rows: bool = False) -> torch.Tensor:
+def gram64(x: torch.Tensor, exact: Optional[bool] = None, rows: bool = False,
+           kchunk: Optional[int] = None) -> torch.Tensor:
     """Upper triangle (lower triangle zero) of the Gram matrix x^T x of a tall fp32 block as an
     fp64 [n, n] tensor - the CholeskyQR Gram. One 256-tile MFMA launch per group of K slices
     (``csrc/gemm_tiled.hip``: upper-triangle tiles only, split-K over ``HEAT_GRAM_KCHUNK`` = 4096
@@ -1354,7 +1359,8 @@ def gram64(x: torch.Tensor, exact: Optional[bool] = None, rows: bool = False) ->
     = 4e-5 relative on the diagonal at m = 1.25e6) drops to ~u chunk / (3 sqrt(m)) = 7e-8. ``exact``: exact fp32
     products (``gemm_f32t``) instead of the fp16x3 split (``gemm_h3t``); default from
     torch.get_float32_matmul_precision() ("highest" -> exact). Host / fp64: an fp64 GEMM.
-    ``rows``: the Gram of the ROWS, x x^T (x [n, m] row-major, contraction along its columns)."""
+    ``rows``: the Gram of the ROWS, x x^T (x [n, m] row-major, contraction along its columns).
+    ``kchunk``: rows per fp32 slice (a multiple of 16; default ``HEAT_GRAM_KCHUNK``)."""
     if rows:
         n, m = x.shape
     else:
@@ -1369,7 +1375,7 @@ def gram64(x: torch.Tensor, exact: Optional[bool] = None, rows: bool = False) ->
         exact = torch.get_float32_matmul_precision() == "highest"
     L = lib()
     st = ctypes.c_void_p(stream_ptr(x.device))
-    kc = _GRAM_KCHUNK
+    kc = _GRAM_KCHUNK if kchunk is None else max(16, int(kchunk) // 16 * 16)
     group = max(1, min(-(-m // kc), _GRAM_PARTIAL_BYTES // (4 * n * n)))
     P = torch.empty(group * n * n, dtype=torch.float32, device=x.device)
     pa = None
