@@ -404,8 +404,10 @@ __global__ __launch_bounds__(KS_ROWS, 2) void ks_step64(const float* __restrict_
 // with its next tile in flight, instead of 4 two-wave workgroups stepping through 3 barriers per
 // tile. The wave does the whole update of its tile: 4 feature blocks x 16 row steps of
 // v_mfma_f32_16x16x4_f32; the counts come from ballots of the lane's own label.
-template <int KP, bool UPDATE>
-__global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
+// AH = 2: two register buffers, the loads of tiles t + G and t + 2 G in flight during tile t (twice
+// the bytes in flight per wave; 149 -> ~213 VGPRs, still two waves per SIMD).
+template <int KP, bool UPDATE, int AH = 1>
+__global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, int64_t n, int64_t ntiles, int64_t ldx,
                                                    const float* __restrict__ Cp, int* __restrict__ labels,
                                                    float* __restrict__ mind, float* __restrict__ sums_part,
                                                    float* __restrict__ counts_part) {
@@ -424,13 +426,17 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) u4[g][s4] = (floatx4)(0.f);
   float ucnt = 0.f;
-  floatx4 buf[16];
+  floatx4 buf[16], buf2[AH == 2 ? 16 : 1];
   typedef const floatx4 __attribute__((address_space(1)))* gptr;
-  auto load = [&](int64_t t) {
-    gptr p = (gptr)(X + (t * 64 + rb) * ldx + 4 * c4);
+  // the partial last tile is read as the LAST 64 rows (n >= 64); its rows below 64 t belong to the
+  // previous tile and are excluded (valid) - no branch in the load (a branch cost the loop head its
+  // vmcnt(16) and 26 VGPRs)
+  auto tile_row0 = [&](int64_t t) __attribute__((always_inline)) { return t * 64 < n - 64 ? t * 64 : n - 64; };
+  auto load = [&](floatx4* b, int64_t t) __attribute__((always_inline)) {
+    gptr p = (gptr)(X + (tile_row0(t) + rb) * ldx + 4 * c4);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      buf[i] = __builtin_nontemporal_load(p);
+      b[i] = __builtin_nontemporal_load(p);
       p += ldx;  // 4 rows on (4 ldx floats)
       asm volatile("" : "+v"(p));
     }
@@ -438,13 +444,18 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
   float* const st = tile + rb * LD + 4 * c4;
   const floatx4* Cq = reinterpret_cast<const floatx4*>(Cp);
   constexpr int CPI = KP <= 8 ? 2 : 1;
-  int64_t t = blockIdx.x;
-  if (t < ntiles) load(t);
-  for (; t < ntiles; t += gridDim.x) {
+  const int64_t G = gridDim.x;
+  // stage tile t from buffer b, refill b with tile t + AH G, then assign (and sum) tile t
+  auto body = [&](floatx4* b, int64_t t) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) *reinterpret_cast<floatx4*>(st + i * 4 * LD) = buf[i];
-    if (t + gridDim.x < ntiles) load(t + gridDim.x);
-    const int64_t row0 = t * 64;
+    for (int i = 0; i < 16; ++i) *reinterpret_cast<floatx4*>(st + i * 4 * LD) = b[i];
+    // AH = 2: the refill is unconditional (past the end: the last tile again, an L2 hit) so that the
+    // compiler's vmcnt at the loop head counts the other buffer's loads as younger (a conditional
+    // refill made it wait for all of them)
+    if (AH == 2) load(b, t + AH * G < ntiles ? t + AH * G : ntiles - 1);
+    else if (t + AH * G < ntiles) load(b, t + AH * G);
+    const int64_t row0 = tile_row0(t);
+    const bool valid = row0 + lane >= t * 64;
     int bi = 0;
     {
       const float* xr = tile + lane * LD;
@@ -469,11 +480,11 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
         best = better ? d : best;
         bi = better ? c : bi;
       }
-      if (labels) labels[row0 + lane] = bi;
-      if (mind) mind[row0 + lane] = best;
+      if (valid && labels) labels[row0 + lane] = bi;
+      if (valid && mind) mind[row0 + lane] = best;
     }
     if (UPDATE) {
-      lab[lane] = bi;
+      lab[lane] = valid ? bi : -1;
       if constexpr (KP <= 8) {
         // onehot^T X on v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4, one row each; layout probed
         // by tools/probes/mfma4x4_probe.hip: A_b[m] / B_b[n] in lane 4 b + m / 4 b + n, D reg m of
@@ -512,10 +523,26 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
       }
 #pragma unroll
       for (int c = 0; c < KP; ++c) {
-        const int cnt = __popcll(__ballot(bi == c));
+        const int cnt = __popcll(__ballot(valid && bi == c));
         ucnt += lane == c ? (float)cnt : 0.f;
       }
     }
+  };
+  int64_t t = blockIdx.x;
+  if constexpr (AH == 2) {
+    load(buf, t < ntiles ? t : ntiles - 1);  // the launch has at most ntiles workgroups
+    load(buf2, t + G < ntiles ? t + G : ntiles - 1);
+    // whole pairs in the loop, an odd last tile after it (a break between the two bodies made the
+    // loop head a merge point of both buffers' states: full vmcnt waits)
+    const int64_t cnt = (ntiles - t + G - 1) / G;
+    for (int64_t i = 0; i + 1 < cnt; i += 2, t += 2 * G) {
+      body(buf, t);
+      body(buf2, t + G);
+    }
+    if (cnt & 1) body(buf, t);
+  } else {
+    if (t < ntiles) load(buf, t);
+    for (; t < ntiles; t += G) body(buf, t);
   }
   if (UPDATE) {
     if constexpr (KP <= 8) {
@@ -548,6 +575,27 @@ __global__ __launch_bounds__(64, 2) void ks_wave64(const float* __restrict__ X, 
   }
 }
 
+// this thread's share (partials threadIdx.x + 256 i) of one output's partial sums, in fp64: eight
+// independent loads in flight per round (one at a time the loop was latency-bound: 10.5 us for the
+// 2049 partials of k = 8, f = 64 in the r5kstrace trace); fixed order for a given nblk
+template <int KP>
+__device__ __forceinline__ double ks_part_sum(const float* __restrict__ sums_part, const float* __restrict__ counts_part,
+                                             int nblk, bool is_sum, int c, int j) {
+  const float* base = is_sum ? sums_part + (int64_t)c * KS_FMAX + j : counts_part + c;
+  const int64_t stride = is_sum ? (int64_t)KP * KS_FMAX : KP;
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int b = threadIdx.x;
+  for (; b + 7 * 256 < nblk; b += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(b + 256 * u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += (double)v[u];
+  }
+  for (int u = 0; b < nblk; b += 256, ++u) a[u & 7] += (double)base[(int64_t)b * stride];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
 // sums[c][j] = sum over the workgroups' partials (fp64), counts[c] likewise: one workgroup per
 // output, its threads stride over the partials (a thread-per-output loop over ~1000 partials was
 // latency-bound at ~0.5 ms)
@@ -559,9 +607,7 @@ __global__ __launch_bounds__(256) void ks_reduce(const float* __restrict__ sums_
   const int e = blockIdx.x;
   const bool is_sum = e < k * f;
   const int c = is_sum ? e / f : e - k * f, j = is_sum ? e - c * f : 0;
-  double a = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += 256)
-    a += is_sum ? (double)sums_part[((int64_t)b * KP + c) * KS_FMAX + j] : (double)counts_part[(int64_t)b * KP + c];
+  double a = ks_part_sum<KP>(sums_part, counts_part, nblk, is_sum, c, j);
   a = ha_wave_sum_d(a);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
   __syncthreads();
@@ -571,6 +617,40 @@ __global__ __launch_bounds__(256) void ks_reduce(const float* __restrict__ sums_
       sums[e] = (float)t;
     else
       counts[c] = (float)t;
+  }
+}
+
+// new centroids (empty clusters keep theirs), the squared shift (fp64, fixed order) and the next
+// pass's padded centroid chunks from the fp64 sums / counts in red; one block
+template <int KP>
+__device__ __forceinline__ void ks_fin_body(int k, int f, const float* __restrict__ C, int64_t ldc,
+                                            float* __restrict__ newC, double* __restrict__ shift,
+                                            const double* __restrict__ red, unsigned* __restrict__ arrived,
+                                            float* __restrict__ cpad, double* wred) {
+  const int kf = k * f;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < kf; i += 256) {
+    const int ci = i / f, ji = i - ci * f;
+    const double cnt = red[kf + ci];
+    const float old = C[(int64_t)ci * ldc + ji];
+    const float nv = cnt > 0.0 ? (float)(red[i] / cnt) : old;
+    newC[i] = nv;
+    const double d = (double)old - (double)nv;
+    acc = fma(d, d, acc);
+  }
+  acc = ha_wave_sum_d(acc);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = acc;
+  __syncthreads();  // also: newC of every thread of this block is visible below
+  if (threadIdx.x == 0) {
+    *shift = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+    if (arrived) *arrived = 0u;  // ready for the next launch on this workspace
+  }
+  // the next pass's padded chunks (ks_pad_centroids' layout) from the new centroids
+  const int fp = ks_fp(f);
+  for (int e2 = threadIdx.x; e2 < KP * (fp + 4); e2 += 256) {
+    const int q = e2 / (4 * KP), c2 = (e2 / 4) % KP, j2 = 4 * q + (e2 & 3);
+    cpad[e2] = c2 < k ? (j2 < f ? newC[c2 * f + j2] : 0.f) : (j2 == 0 ? __builtin_huge_valf() : 0.f);
   }
 }
 
@@ -594,46 +674,36 @@ __global__ __launch_bounds__(256) void ks_reduce_fin(const float* __restrict__ s
   const int kf = k * f;
   const bool is_sum = e < kf;
   const int c = is_sum ? e / f : e - kf, j = is_sum ? e - c * f : 0;
-  double a = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += 256)
-    a += is_sum ? (double)sums_part[((int64_t)b * KP + c) * KS_FMAX + j] : (double)counts_part[(int64_t)b * KP + c];
+  double a = ks_part_sum<KP>(sums_part, counts_part, nblk, is_sum, c, j);
   a = ha_wave_sum_d(a);
   if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = a;
   __syncthreads();
   if (threadIdx.x == 0) {
     red[e] = (wred[0] + wred[1]) + (wred[2] + wred[3]);
-    __threadfence();
-    last = atomicAdd(arrived, 1u) == gridDim.x - 1;
+    if (arrived) {
+      __threadfence();
+      last = atomicAdd(arrived, 1u) == gridDim.x - 1;
+    } else {
+      last = false;
+    }
   }
   __syncthreads();
   if (!last) return;
   __threadfence();
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < kf; i += 256) {
-    const int ci = i / f, ji = i - ci * f;
-    const double cnt = red[kf + ci];
-    const float old = C[(int64_t)ci * ldc + ji];
-    const float nv = cnt > 0.0 ? (float)(red[i] / cnt) : old;
-    newC[i] = nv;
-    const double d = (double)old - (double)nv;
-    acc = fma(d, d, acc);
-  }
-  acc = ha_wave_sum_d(acc);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = acc;
-  __syncthreads();  // also: newC of every thread of this block is visible below
-  if (threadIdx.x == 0) {
-    *shift = (wred[0] + wred[1]) + (wred[2] + wred[3]);
-    *arrived = 0u;  // ready for the next launch on this workspace
-  }
-  // the next pass's padded chunks (ks_pad_centroids' layout) from the new centroids
-  const int fp = ks_fp(f);
-  for (int e2 = threadIdx.x; e2 < KP * (fp + 4); e2 += 256) {
-    const int q = e2 / (4 * KP), c2 = (e2 / 4) % KP, j2 = 4 * q + (e2 & 3);
-    cpad[e2] = c2 < k ? (j2 < f ? newC[c2 * f + j2] : 0.f) : (j2 == 0 ? __builtin_huge_valf() : 0.f);
-  }
+  ks_fin_body<KP>(k, f, C, ldc, newC, shift, red, arrived, cpad, wred);
 }
 
+// The last step of the Lloyd epilogue as its own one-block launch (after ks_reduce_fin with
+// arrived = null): with two tiles of loads in flight per wave (ks_wave64<.., 2>) the pass no longer
+// slows down after small launches, and the fused form's per-block agent-scope fence + atomic on one
+// counter cost more than this launch (tools/r5/gpu_ksw2.sh, tools/r5/gpu_ksfin.sh)
+template <int KP>
+__global__ __launch_bounds__(256) void ks_fin(int k, int f, const float* __restrict__ C, int64_t ldc,
+                                              float* __restrict__ newC, double* __restrict__ shift,
+                                              const double* __restrict__ red, float* __restrict__ cpad) {
+  __shared__ double wred[4];
+  ks_fin_body<KP>(k, f, C, ldc, newC, shift, red, nullptr, cpad, wred);
+}
 int ks_kp(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : 16; }
 
 template <int KP, int MODE, bool U>
@@ -669,24 +739,32 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
   int64_t done = 0;
   if (mode == KS_ROW4 && f == KS_FMAX) {
     const int64_t full = n / KS_ROWS;
-    // HEAT_KS_VARIANT: "wave" (default: one-wave workgroups, 64-row tiles), "a1" / "a2" (two-wave
+    // HEAT_KS_VARIANT: "w2" (default: one-wave workgroups, 64-row tiles, two tiles of loads in flight
+    // per wave: 0.614-0.62 vs 0.616-0.70 ms per pass in the Lloyd-loop variants of
+    // smallk_fitloop2.py, tools/r5/gpu_ksw2.sh), "wave" (one tile in flight), "a1" / "a2" (two-wave
     // workgroups, 128-row tiles, one / two tiles of loads in flight). Measured on one box
     // (smallk_ab_r05.jsonl), n = 12.5M, f = 64, fused pass: wave 0.734 / 0.978 / 0.611 ms at
     // k = 8 / 16 / 3 vs a1 0.767 / 1.018 / 0.654 and a2 0.780 / 1.048 / 0.663.
     static const int variant = [] {
       const char* e = getenv("HEAT_KS_VARIANT");
-      return !e ? 0 : e[0] == 'w' ? 0 : e[1] == '2' ? 2 : 1;
+      return !e ? 3 : e[0] == 'w' ? (e[1] == '2' ? 3 : 0) : e[1] == '2' ? 2 : 1;
     }();
-    if (variant == 0 && n / 64 > 0) {
-      const int64_t full64 = n / 64;
+    if ((variant == 0 || variant == 3) && n / 64 > 0) {
+      // w2 also takes the partial last tile (no tail launch: 13.7 us per pass in the r5kstrace trace)
+      const int64_t full64 = variant == 3 ? (n + 63) / 64 : n / 64;
       static const int wpc = [] {  // waves per CU (LDS holds 9 of 17.7 KB)
         const char* e = getenv("HEAT_KS_WPC");
         const int v = e ? atoi(e) : 8;
         return v < 1 ? 1 : v > 9 ? 9 : v;
       }();
       nblk = (int)(full64 < (int64_t)wpc * num_cus ? full64 : (int64_t)wpc * num_cus);
-      hipLaunchKernelGGL((ks_wave64<KP, U>), dim3(nblk), dim3(64), 0, s, X, full64, ldx, cpad, labels, mind, sp, cp);
-      done = full64 * 64;
+      if (variant == 3)  // HEAT_KS_VARIANT=w2: two tiles of loads in flight per wave
+        hipLaunchKernelGGL((ks_wave64<KP, U, 2>), dim3(nblk), dim3(64), 0, s, X, n, full64, ldx, cpad, labels, mind,
+                           sp, cp);
+      else
+        hipLaunchKernelGGL((ks_wave64<KP, U>), dim3(nblk), dim3(64), 0, s, X, full64 * 64, full64, ldx, cpad, labels,
+                           mind, sp, cp);
+      done = variant == 3 ? n : full64 * 64;
     } else if (full > 0) {
       nblk = (int)(full < 4 * num_cus ? full : 4 * num_cus);
       if (variant == 2)
@@ -715,9 +793,21 @@ void ks_launch(int mode, int num_cus, hipStream_t s, const float* X, int64_t n, 
       ks_launch_generic<KP, KS_SCALAR, U>(g, s, Xr, rest, f, ldx, cpad, lr, mr, spr, cpr);
     nblk += g;
   }
-  if (U && fin)
+  // HEAT_KS_FIN=fused: the last-arriving reduction block finishes the step (one launch; the default
+  // is the reduction and a one-block ks_fin)
+  static const bool fin_fused = [] {
+    const char* e = getenv("HEAT_KS_FIN");
+    return e && e[0] == 'f';
+  }();
+  if (U && fin && fin_fused) {
     hipLaunchKernelGGL((ks_reduce_fin<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, fin->C,
                        fin->ldc, fin->newC, fin->shift, fin->red, fin->arrived, fin->cpad);
+  } else if (U && fin) {
+    hipLaunchKernelGGL((ks_reduce_fin<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, fin->C,
+                       fin->ldc, fin->newC, fin->shift, fin->red, (unsigned*)nullptr, fin->cpad);
+    hipLaunchKernelGGL((ks_fin<KP>), dim3(1), dim3(256), 0, s, k, f, fin->C, fin->ldc, fin->newC, fin->shift, fin->red,
+                       fin->cpad);
+  }
   else if (U)
     hipLaunchKernelGGL((ks_reduce<KP>), dim3((unsigned)(k * f + k)), dim3(256), 0, s, sp, cp, nblk, k, f, sums, counts);
 }

@@ -906,7 +906,7 @@ def test_kmeans_step_small(n, f, k):
         assert torch.equal(counts.long(), torch.bincount(lab.long(), minlength=k))
 
 
-@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (129, 64), (100000, 64)])
+@pytest.mark.parametrize("n,f", [(1000, 3), (70001, 64), (5000, 18), (129, 64), (100000, 64), (64, 64), (65, 64), (127, 64)])
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
 def test_kmeans_lloyd_small(n, f, k):
     """One-launch-epilogue Lloyd step: new centroids == fp64 means of the assigned points (an empty

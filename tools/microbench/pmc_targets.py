@@ -10,6 +10,7 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   smallk  - 10 fused small-k passes, k = 8, 1.25e7 x 64 (kmeans_smallk.hip: ks_step64, the reference protocol)
   cdist_exact - exact (difference) cdist, SUSY size 40k x 18, 3 calls (cdist.hip: cdist_vx)
   gemm_small - 1024^3 and 2048^3 exact fp32 through fgemm's plan (gemm_small.hip / gemm_tiled.hip split-K)
+  gemm_f32s_big - gemm_f32s alone at 6144^3 and 8192^3 (one K slice)
   gram    - ht.matmul(A.T, A) at 400000 x 2048 (upper-triangle Gram tiles + fp64 slice sums)"""
 import sys
 
@@ -74,6 +75,15 @@ def main():
             b = torch.randn(n, n, device="cuda")
             for _ in range(5):
                 basics.fgemm(a, b)
+    elif which == "gemm_f32s_big":
+        # the 128-tile kernel alone on large products (6144^3, 8192^3, one K slice)
+        from heat_amd.ops import kernels as K
+
+        for n in (6144, 8192):
+            a = torch.randn(n, n, device="cuda")
+            b = torch.randn(n, n, device="cuda")
+            for _ in range(3):
+                K.gemm_f32_small(a, b, slices=1)
     elif which == "gram":
         A = ht.random.randn(400_000, 2048, split=0)
         for _ in range(3):

@@ -73,3 +73,4 @@ run("step_finalize_newC", step_finalize)
 run("step_finalize_fixedC", step_finalize_fixed)
 run("step_torch_update_newC", step_torch_update)
 run("step_finalize_copy_into_C", step_copy_back)
+run("lloyd_fused_newC_last", lambda C: ops.kmeans_lloyd_small(X, C)[1])   # again, clocks warm
