@@ -29,7 +29,7 @@ __device__ __forceinline__ int64_t gs_xcd_remap(int64_t orig, int64_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-template <bool AK, bool BN>
+template <bool AK, bool BN, bool PRIO = false>
 __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
@@ -154,6 +154,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
         for (int s = 4 * q; s < 4 * q + 4; ++s) fb[bn][s] = Bs[(16 * h + s) * B_LD + wn * 64 + bn * 32 + r];
     };
     frag(0);
+    // PRIO (A/B, HEAT_GS_PRIO=1): the wave in its MFMA phase wins issue arbitration over the other
+    // workgroup's wave on the SIMD, which then runs its loads / barrier meanwhile (the two
+    // workgroups drift out of phase instead of reaching their barriers together)
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q + 1 < 4) frag(q + 1);
@@ -167,6 +171,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
             acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[bm][q][s & 3], fb[bn][s], acc[bm][bn], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   const int64_t nk = (ke - kb + GK - 1) / GK;
@@ -234,6 +239,22 @@ HA_EXPORT int ha_gemm_f32s(const float* A, const float* B, float* C, int64_t M, 
   if (tiles > 0x7fffffffLL || ns > 65535) return HA_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
+  static const bool prio = getenv("HEAT_GS_PRIO") && getenv("HEAT_GS_PRIO")[0] == '1';
+  if (prio) {
+    if (!a_kmajor && !b_nmajor)
+      hipLaunchKernelGGL((gemm_f32s<false, false, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
+                         cslice);
+    else if (!a_kmajor && b_nmajor)
+      hipLaunchKernelGGL((gemm_f32s<false, true, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
+                         cslice);
+    else if (a_kmajor && !b_nmajor)
+      hipLaunchKernelGGL((gemm_f32s<true, false, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
+                         cslice);
+    else
+      hipLaunchKernelGGL((gemm_f32s<true, true, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
+                         cslice);
+    return ha_launch_status();
+  }
   if (!a_kmajor && !b_nmajor)
     hipLaunchKernelGGL((gemm_f32s<false, false>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
   else if (!a_kmajor && b_nmajor)
