@@ -3,7 +3,7 @@
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 export PYTHONPATH="$ROOT"
-OUT="$ROOT/gpurun_out/r5final"
+OUT="$ROOT/gpurun_out/${R5FINAL_DIR:-r5final}"
 mkdir -p "$OUT"
 cd "$ROOT"
 export TMPDIR=/tmp
