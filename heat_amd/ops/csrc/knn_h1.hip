@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void h3_uniform_r(int k, float* __restrict__ u
 // tile max and thr the list's last entry (rej <= thr always holds): it covers every score of the
 // tile that is not queued. Queued scores that no longer beat the list at merge time go to rej
 // exactly; evictions too.
-template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB, int WAVES = 4, bool PAIRB = false>
+template <int FPAD, int KH, int KO, int NPB, int TPI, int MINB, int WAVES = 4, int GRP = 1>
 __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __restrict__ planes, const float* __restrict__ sxv,
                                                   int64_t n, const _Float16* __restrict__ image,
                                                   const float* __restrict__ u, const float* __restrict__ meta,
@@ -115,9 +115,10 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
   // NPB: 32-point blocks per wave; TPI: 32-centroid tiles per staged chunk; MINB: workgroups / CU
   constexpr int PIECES = TPI * KS;        // 1 KB hi-fragment pieces per chunk (piece q <- image piece 2q)
   constexpr int BUF = PIECES * 1024 + TPI * 512;  // + rank-1 fragments (512 B per tile)
-  // chunks in flight, ring slots. PAIRB: one barrier per PAIR of chunks (both landed), chunk
-  // ch + 2 issued during chunk ch (the barrier waits are a quarter of a chunk's time: stamps)
-  constexpr int AHEAD = PAIRB ? 2 : TPI >= 3 ? 2 : 3, NB = PAIRB ? 4 : AHEAD + 1;
+  // chunks in flight, ring slots. GRP > 1: one barrier per GROUP of GRP chunks (all landed), chunk
+  // ch + GRP issued during chunk ch into a 2 GRP-slot ring (the barrier waits were a quarter of a
+  // chunk's time: stamps). GRP = 1: a barrier per chunk, 3 (2) chunks in flight.
+  constexpr int AHEAD = GRP > 1 ? GRP : TPI >= 3 ? 2 : 3, NB = GRP > 1 ? 2 * GRP : AHEAD + 1;
   constexpr int IMGW = PIECES / WAVES;    // image pieces per wave per chunk
   constexpr int PTS_PER_WG = WAVES * NPB * 32;
   constexpr int Q = 4;                    // queue slots per list
@@ -307,8 +308,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
     stamp(ch, 0);
     // this wave's pieces of chunk ch have landed once at most the later chunks' are outstanding
     const int later = min(nch - 1 - ch, AHEAD - 1);
-    if (PAIRB) {
-      if ((ch & 1) == 0) vm_wait<0>();   // chunks ch and ch + 1: everything outstanding
+    if (GRP > 1) {
+      if (ch % GRP == 0) vm_wait<0>();   // chunks ch .. ch + GRP - 1: everything outstanding
     } else if (later >= 2) {
       if (vw) vm_wait<2 * IMGW + 2>();
       else vm_wait<2 * IMGW>();
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void h1_topk(const _Float16* __re
     // a raw barrier: __syncthreads() would add s_waitcnt vmcnt(0), i.e. wait for the prefetch too.
     // Past it every wave has finished chunk ch - 1, whose slot the next DMA refills.
     stamp(ch, 1);
-    if (!(dbg & 2) && (!PAIRB || (ch & 1) == 0)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (!(dbg & 2) && ch % GRP == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(ch, 2);
     const bool refill = ch + AHEAD < nch && !(dbg & 4);
@@ -468,10 +469,13 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   static const bool cfg_w8 = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'w';
   // HEAT_H1_CFG=b (A/B): one barrier per chunk instead of per pair of chunks
   static const bool cfg_b = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'b';
+  // HEAT_H1_CFG=q (A/B): one barrier per 4 chunks (8-slot ring, 73.7 KB of LDS per workgroup):
+  // 368-370 vs 297 ms for the pair form on one box (knn_h1_ab_r05.jsonl)
+  static const bool cfg_q = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'q';
 #define HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, PB)                                                        \
   do {                                                                                                         \
     using KC = H3Cfg<FP, NPB>;                                                                                 \
-    const size_t lds = (!PB && TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* ring slots */ \
+    const size_t lds = (PB > 1 ? 2 * PB : TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* slots */ \
     const int ppw = WV * NPB * 32;                                                                             \
     const unsigned blocks = (unsigned)((n + ppw - 1) / ppw);                                                   \
     hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB, WV, PB>),             \
@@ -479,7 +483,7 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
     hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB, WV, PB>), dim3(blocks), dim3(64 * WV), lds, s, p,   \
                        sx, n, image, u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                     \
   } while (0)
-#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB, WV) HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, false)
+#define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB, WV) HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, 1)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
     hipLaunchKernelGGL(h3_cscale<FP>, dim3(h3_cscale_grid(kpad, FP / 8)), dim3(256), 0, s, C, m, f, ldc, kpad, u,  \
@@ -493,11 +497,13 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
     /* (tools/microbench/h1_ab.py, one box): pair 309-310 ms, per-chunk barrier (HEAT_H1_CFG=b) 313-315; */     \
     /* 3-tile chunks / 2 in flight +2%; one workgroup of 4 x 64 points per CU (HEAT_H1_CFG=a) +30% */           \
     constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
-    constexpr bool PAIR = TPB == 2;                                                                              \
+    constexpr int PAIR = TPB == 2 ? 2 : 1;                                                                       \
     if (FP == 128 && cfg_a && kp == 32) {                                                                        \
       HA_H1TK_LAUNCH(128, 32, 2, 4, 1, 4);                                                                       \
     } else if (FP == 128 && cfg_w8 && kp == 32) {                                                                \
       HA_H1TK_LAUNCH(128, 32, 1, 2, 1, 8);                                                                       \
+    } else if (FP == 128 && cfg_q && kp == 32) {                                                                 \
+      HA_H1TK_LAUNCH_X(128, 32, 1, 2, 2, 4, 4);                                                                  \
     } else if (cfg_b && kp == 32) {                                                                              \
       HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2, 4);                                                                      \
     } else if (kp == 32) {                                                                                       \
