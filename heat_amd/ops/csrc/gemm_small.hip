@@ -17,23 +17,26 @@
 
 namespace {
 
-constexpr int GB = 128, GK = 32;
-constexpr int A_LD = GK + 4;    // As[row][k]: 144-byte rows (conflict-free row-per-lane b128 reads)
+constexpr int GB = 128, GK = 32;  // GK: the slice granularity (kps is a multiple of it)
 constexpr int B_LD = GB + 4;    // Bs[k][n]
-constexpr int A_SZ = GB * A_LD;
-constexpr int B_SZ = GK * B_LD;
-constexpr int ST_SZ = A_SZ + B_SZ;  // floats per stage
 
 __device__ __forceinline__ int64_t gs_xcd_remap(int64_t orig, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8, xcd = orig % 8, loc = orig / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-template <bool AK, bool BN, bool PRIO = false>
-__global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A, const float* __restrict__ B,
+// GKT: k per LDS stage - 32 (default: 70.6 KB of LDS, two workgroups per CU) or 16 (A/B,
+// HEAT_GS_K16=1: 37.4 KB and fewer registers, three workgroups per CU, twice the barriers)
+template <bool AK, bool BN, bool PRIO = false, int GKT = 32>
+__global__ __launch_bounds__(256, GKT == 16 ? 3 : 2) void gemm_f32s(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
                                                     int64_t kps, int64_t cslice) {
+  constexpr int A_LD = GKT + 4;  // As[row][k]: 144 / 80-byte rows (conflict-free row-per-lane b128 reads)
+  constexpr int A_SZ = GB * A_LD, B_SZ = GKT * B_LD, ST_SZ = A_SZ + B_SZ;  // floats per stage
+  constexpr int NP = GKT / 8;     // 16-byte pieces per thread per operand and stage
+  constexpr int PR = GKT / 4;     // 16-byte pieces per row of a k-contiguous operand stage
+  constexpr int HS = GKT / 2;     // k steps per stage; lane half h owns k = HS h + s at step s
   __shared__ __attribute__((aligned(16))) float sm[2 * ST_SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -51,28 +54,28 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
   const int64_t ke = K - kb < kps ? K : kb + kps;
   C += (int64_t)blockIdx.y * cslice;
 
-  floatx4 ra[4], rb[4];
+  floatx4 ra[NP], rb[NP];
   // piece p = tid + 256 i of a stage (1024 16-byte pieces per operand)
   // interior tiles (every stage of a slice is whole: kps is a multiple of 32) take the unguarded
   // 16-byte loads; only edge tiles and the last partial stage evaluate per-piece bounds
   const bool inner = m0 + GB <= M && n0 + GB <= N;
   auto gload = [&](int64_t k0) {
-    if (inner && k0 + GK <= ke) {
+    if (inner && k0 + GKT <= ke) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NP; ++i) {
         const int p = tid + 256 * i;
-        ra[i] = !AK ? *reinterpret_cast<const floatx4*>(A + (m0 + (p >> 3)) * lda + k0 + 4 * (p & 7))
+        ra[i] = !AK ? *reinterpret_cast<const floatx4*>(A + (m0 + p / PR) * lda + k0 + 4 * (p % PR))
                     : *reinterpret_cast<const floatx4*>(A + (k0 + (p >> 5)) * lda + m0 + 4 * (p & 31));
         rb[i] = !BN ? *reinterpret_cast<const floatx4*>(B + (k0 + (p >> 5)) * ldb + n0 + 4 * (p & 31))
-                    : *reinterpret_cast<const floatx4*>(B + (n0 + (p >> 3)) * ldb + k0 + 4 * (p & 7));
+                    : *reinterpret_cast<const floatx4*>(B + (n0 + p / PR) * ldb + k0 + 4 * (p % PR));
       }
       return;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NP; ++i) {
       const int p = tid + 256 * i;
-      if (!AK) {  // row-major: row p >> 3, k 4 (p & 7)
-        const int64_t gr = m0 + (p >> 3), gk = k0 + 4 * (p & 7);
+      if (!AK) {  // row-major: row p / PR, k 4 (p % PR)
+        const int64_t gr = m0 + p / PR, gk = k0 + 4 * (p % PR);
         const float* s = A + gr * lda + gk;
         if (gr < M && gk + 4 <= ke) {
           ra[i] = *reinterpret_cast<const floatx4*>(s);
@@ -99,8 +102,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
 #pragma unroll
           for (int j = 0; j < 4; ++j) rb[i][j] = (gk < ke && gc + j < N) ? s[j] : 0.f;
         }
-      } else {    // n-major [N][K]: column p >> 3, k 4 (p & 7)
-        const int64_t gc = n0 + (p >> 3), gk = k0 + 4 * (p & 7);
+      } else {    // n-major [N][K]: column p / PR, k 4 (p % PR)
+        const int64_t gc = n0 + p / PR, gk = k0 + 4 * (p % PR);
         const float* s = B + gc * ldb + gk;
         if (gc < N && gk + 4 <= ke) {
           rb[i] = *reinterpret_cast<const floatx4*>(s);
@@ -115,10 +118,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
     float* As = sm + buf * ST_SZ;
     float* Bs = As + A_SZ;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NP; ++i) {
       const int p = tid + 256 * i;
       if (!AK) {
-        *reinterpret_cast<floatx4*>(As + (p >> 3) * A_LD + 4 * (p & 7)) = ra[i];
+        *reinterpret_cast<floatx4*>(As + (p / PR) * A_LD + 4 * (p % PR)) = ra[i];
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) As[(4 * (p & 31) + j) * A_LD + (p >> 5)] = ra[i][j];
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
         *reinterpret_cast<floatx4*>(Bs + (p >> 5) * B_LD + 4 * (p & 31)) = rb[i];
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Bs[(4 * (p & 7) + j) * B_LD + (p >> 3)] = rb[i][j];
+        for (int j = 0; j < 4; ++j) Bs[(4 * (p % PR) + j) * B_LD + p / PR] = rb[i][j];
       }
     }
   };
@@ -140,18 +143,18 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
   auto compute = [&](int buf) {
     const float* As = sm + buf * ST_SZ;
     const float* Bs = As + A_SZ;
-    floatx4 fa[2][4];
-    float fb[2][16];
+    floatx4 fa[2][HS / 4];
+    float fb[2][HS];
     // fragments in 4 groups of 4 k-steps; group q + 1 is read while group q's 16 MFMAs run
     // (reading all 40 first exposed the LDS latency once per stage, 38 % of wave cycles waiting)
     auto frag = [&](int q) __attribute__((always_inline)) {
 #pragma unroll
       for (int bm = 0; bm < 2; ++bm)
-        fa[bm][q] = *reinterpret_cast<const floatx4*>(As + (wm * 64 + bm * 32 + r) * A_LD + 16 * h + 4 * q);
+        fa[bm][q] = *reinterpret_cast<const floatx4*>(As + (wm * 64 + bm * 32 + r) * A_LD + HS * h + 4 * q);
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn)
 #pragma unroll
-        for (int s = 4 * q; s < 4 * q + 4; ++s) fb[bn][s] = Bs[(16 * h + s) * B_LD + wn * 64 + bn * 32 + r];
+        for (int s = 4 * q; s < 4 * q + 4; ++s) fb[bn][s] = Bs[(HS * h + s) * B_LD + wn * 64 + bn * 32 + r];
     };
     frag(0);
     // PRIO (A/B, HEAT_GS_PRIO=1): the wave in its MFMA phase wins issue arbitration over the other
@@ -159,8 +162,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
     // workgroups drift out of phase instead of reaching their barriers together)
     if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q + 1 < 4) frag(q + 1);
+    for (int q = 0; q < HS / 4; ++q) {
+      if (q + 1 < HS / 4) frag(q + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 4 * q; s < 4 * q + 4; ++s)
@@ -174,14 +177,14 @@ __global__ __launch_bounds__(256, 2) void gemm_f32s(const float* __restrict__ A,
     if (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
-  const int64_t nk = (ke - kb + GK - 1) / GK;
+  const int64_t nk = (ke - kb + GKT - 1) / GKT;
   if (nk > 0) {
     gload(kb);
     sstore(0);
     __syncthreads();
   }
   for (int64_t t = 0; t < nk; ++t) {
-    if (t + 1 < nk) gload(kb + (t + 1) * GK);  // in flight during this stage's MFMAs
+    if (t + 1 < nk) gload(kb + (t + 1) * GKT);  // in flight during this stage's MFMAs
     compute(t & 1);
     if (t + 1 < nk) sstore((t + 1) & 1);
     __syncthreads();
@@ -240,6 +243,39 @@ HA_EXPORT int ha_gemm_f32s(const float* A, const float* B, float* C, int64_t M, 
   hipStream_t s = (hipStream_t)stream;
   const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
   static const bool prio = getenv("HEAT_GS_PRIO") && getenv("HEAT_GS_PRIO")[0] == '1';
+  // 16-k stages (three workgroups per CU) or 32-k (two): HEAT_GS_K16 = 1 / 0 forces one; by default
+  // the wave quantisation decides - W = workgroups / (CUs x workgroups per CU), e(W) = W / ceil(W),
+  // 16-k when 1.04 e16 > e32 (measured, tools/r5/gpu_k16.sh: 16-k is ~3-4 % faster per wave on
+  // large grids - 1.25e6 x 3840 x 256 21.8 vs 22.6 ms - and 6144^3 3.90 vs 4.37 ms at 3.0 vs 4.5
+  // waves, but slower where it leaves a partial wave: 4096^3 1.19 vs 1.11 ms)
+  static const int k16_env = getenv("HEAT_GS_K16") ? (getenv("HEAT_GS_K16")[0] == '1' ? 1 : 0) : -1;
+  static const int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  bool k16 = k16_env == 1;
+  if (k16_env < 0) {
+    const double nwg = (double)tiles * (double)ns;
+    auto eff = [](double w) { const double c = w > 1.0 ? (double)(int64_t)(w + 0.999999) : 1.0; return w / c; };
+    k16 = 1.04 * eff(nwg / (3.0 * ncu)) > eff(nwg / (2.0 * ncu));
+  }
+  if (k16) {
+    if (!a_kmajor && !b_nmajor)
+      hipLaunchKernelGGL((gemm_f32s<false, false, false, 16>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta,
+                         kps, cslice);
+    else if (!a_kmajor && b_nmajor)
+      hipLaunchKernelGGL((gemm_f32s<false, true, false, 16>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta,
+                         kps, cslice);
+    else if (a_kmajor && !b_nmajor)
+      hipLaunchKernelGGL((gemm_f32s<true, false, false, 16>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta,
+                         kps, cslice);
+    else
+      hipLaunchKernelGGL((gemm_f32s<true, true, false, 16>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta,
+                         kps, cslice);
+    return ha_launch_status();
+  }
   if (prio) {
     if (!a_kmajor && !b_nmajor)
       hipLaunchKernelGGL((gemm_f32s<false, false, true>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
