@@ -87,6 +87,8 @@ class _KCluster(ClusteringMixin, BaseEstimator):
 
     @property
     def cluster_centers_(self) -> DNDarray:
+        # handed out: the caller may write into it by any path, so the next step re-pads it
+        self._own_newC = None
         return self._cluster_centers
 
     @property

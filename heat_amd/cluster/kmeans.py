@@ -44,9 +44,11 @@ class KMeans(_KCluster):
         k = C.shape[0]
         if not distributed:
             # one process: the whole step is the pass over the points + one epilogue launch
-            step = ops.kmeans_lloyd_small(X, C)
+            # the padded centroids of the previous step are reused only for this loop's own output
+            step = ops.kmeans_lloyd_small(X, C, reuse_pad=C is getattr(self, "_own_newC", None))
             if step is not None:
                 labels, newC, self._step_shift = step
+                self._own_newC = newC
                 return newC, labels
         fused = ops.kmeans_step_small(X, C)   # exact fp32: serves both precisions
         if fused is not None:   # few clusters: assignment and sums in one pass over the points

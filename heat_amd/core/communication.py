@@ -39,7 +39,7 @@ from ..parallel import backend as _backend
 from ..parallel import staging as _SD
 
 # device buffers are handed straight to RCCL unless the world group is gloo-only (host staging)
-CUDA_AWARE_MPI = os.environ.get("HEAT_COMM_BACKEND", "").lower() != "gloo"
+CUDA_AWARE_MPI = _backend.backend_name() != "gloo"
 
 #: collective -> data path counters ("allreduce:ipc", "allreduce:native", "allreduce:pg",
 #: "allgatherv:...", "reduce_scatter:..."); ``bench.py`` reports them so a run records which

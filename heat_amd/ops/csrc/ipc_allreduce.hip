@@ -20,6 +20,17 @@
 // (no hang). ha_ipc_error_async copies the word into pinned host memory behind every call; the
 // host raises at the next call (or at an explicit check) and the communicator is poisoned, since
 // the two-slot reuse argument no longer holds after a missed barrier.
+//
+// Coherence of the data slots. The slots are ordinary coarse-grained hipMalloc memory (only the
+// signal words are uncached): a rank writes only its OWN slot, with plain stores that may sit
+// dirty in its L2, and peers read it over xGMI, possibly through lines of THEIR L2. Both sides
+// are covered by the system-scope fences of ipc_block_barrier: on gfx950 the release fence is
+// `buffer_wbl2 sc0 sc1` (every dirty L2 line of the writer written back to HBM before its epoch
+// is stored) and the acquire fence `buffer_inv sc0 sc1` (the reader's L2 invalidated at system
+// scope after it saw every peer's epoch, so no stale line of a previous call's slot survives).
+// tests/test_ipc_coherence.py compiles this file for gfx950 and checks that every IPC kernel
+// carries that write-back / invalidate pair, so a compiler or scope change cannot drop it
+// silently. The MALL sits on the memory side and is coherent for all agents.
 #include "common.h"
 
 #include <cstring>

@@ -114,7 +114,8 @@ def _ks_step(X: torch.Tensor, C: torch.Tensor, want_mind: bool, update: bool):
 _KS_LLOYD = {}   # (device, stream, k) -> [workspace, (weakref, version) of the centroids padded in it]
 
 
-def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor,
+                       reuse_pad: bool = False) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
     """One whole Lloyd step for few clusters on ONE process (k <= 16, f <= 64, device fp32): (int32
     labels, new centroids [k, f] fp32, squared shift 0-d fp64) from one pass over the points plus ONE
     epilogue launch (``csrc/kmeans_smallk.hip: ha_ks_lloyd`` - reduction, new centroids, shift and
@@ -139,10 +140,12 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor) -> Optional[Tuple[torch
         ws = torch.zeros(max(1, L.ha_ks_lloyd_workspace_floats(k, ncu)), dtype=torch.float32, device=dev)
         state = _KS_LLOYD[(dev, sp, k)] = [ws, None]
     # the padded chunks in the workspace belong to the previous call's newC: valid for this call
-    # only if C IS that tensor object (alive, unmodified) - an address match alone could be a new
-    # tensor in the freed block
+    # only if the caller owns C as that output (``reuse_pad``: the KMeans loop, which never writes
+    # its centroids by a path that skips ``_version`` - .data, DLPack, raw-pointer kernels) and C
+    # IS that tensor object, alive and unmodified; an address match alone could be a new tensor in
+    # the freed block
     prev = state[1]
-    pad_ready = prev is not None and prev[0]() is Cc and prev[1] == Cc._version
+    pad_ready = bool(reuse_pad) and prev is not None and prev[0]() is Cc and prev[1] == Cc._version
     labels = torch.empty(n, dtype=torch.int32, device=dev)
     newC = torch.empty((k, f), dtype=torch.float32, device=dev)
     shift = torch.empty((), dtype=torch.float64, device=dev)

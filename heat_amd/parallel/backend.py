@@ -35,6 +35,15 @@ def backend_name() -> str:
         return "gloo"
     if forced in ("rccl", "nccl"):
         return "nccl"
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "0") or 0)
+    if local_world > torch.cuda.device_count() and not forced:
+        # more ranks on this node than GPUs: ranks would share a device, which RCCL refuses
+        # ("Duplicate GPU detected") - run the world on gloo (device buffers host-staged)
+        import warnings
+
+        warnings.warn("{} local ranks on {} GPUs: ranks share devices, using the gloo backend".format(
+            local_world, torch.cuda.device_count()))
+        return "gloo"
     # device tensors -> RCCL over xGMI, host tensors (object collectives, CPU arrays) -> gloo
     return "cpu:gloo,cuda:nccl"
 

@@ -166,11 +166,13 @@ def _symmetric_half_ring(x: torch.Tensor, out: torch.Tensor, counts, displs, com
     tile and the tiles (r, r - s) for s = 1 .. floor(p / 2) (for even p the pair r, r + p/2 is
     computed by the lower half only), and receives the mirrored tiles (r, r + s) from its partners.
 
-    Overlap (round 5): the floor(p/2) block exchanges are posted at once up front (every rank
-    sends its own block to r + 1 .. r + p/2 - all links of the node busy), the diagonal tile is
-    computed while they fly; then each received block's tile is computed and its transpose posted
-    back (paired with the receive of the mirrored tile from r + s) while the next tile computes.
-    Nothing is waited for until the end."""
+    Overlap with bounded memory: the block exchange of step s + 1 is posted before tile s is
+    computed, and each tile's transpose goes back (paired with the receive of the mirrored tile
+    from r + s) while the next tile computes. At most two block exchanges and two tile exchanges
+    are in flight: step s - 1's exchange is waited for, its mirrored tile copied into ``out`` and
+    its buffers dropped right after step s is posted (the path runs when memory is the constraint,
+    so holding every block or every transposed tile until the end is not an option). Every rank
+    posts the same step sequence, so the point-to-point pairs match in order."""
     import torch.distributed as dist
 
     from ..parallel import staging as _SD
@@ -184,47 +186,51 @@ def _symmetric_half_ring(x: torch.Tensor, out: torch.Tensor, counts, displs, com
     def computes(s_):  # does rank r compute the pair (r, r - s_)?
         return not (even and s_ == half) or r < half
 
-    # phase 1: every block exchange at once
-    ops, blocks = [], {}
-    for s_ in range(1, half + 1):
+    def post_block(s_):
+        """Step s_'s block exchange: own block to r + s_, block of r - s_ in (-> (buffer, works))."""
         dst, src = (r + s_) % p, (r - s_) % p
-        if even and s_ == half:
-            if r < half:
-                blocks[s_] = torch.empty((counts[src],) + rest, dtype=xs.dtype, device=xs.device)
-                ops.append(dist.P2POp(dist.irecv, blocks[s_], comm._g(src), comm.group))
-            else:
-                ops.append(dist.P2POp(dist.isend, xs, comm._g(dst), comm.group))
-            continue
-        blocks[s_] = torch.empty((counts[src],) + rest, dtype=xs.dtype, device=xs.device)
-        ops.append(dist.P2POp(dist.isend, xs, comm._g(dst), comm.group))
-        ops.append(dist.P2POp(dist.irecv, blocks[s_], comm._g(src), comm.group))
-    works = _SD.batch_isend_irecv(ops) if ops else []
-    out[:, displs[r]: displs[r] + counts[r]] = tile(xs, xs)    # overlaps the block transfers
-    for w in works:
-        w.wait()
-    # phase 2: tiles in step order, each transpose posted back with the mirrored tile's receive
-    pending, mirrors = [], []
-    for s_ in range(1, half + 1):
-        dst, src = (r + s_) % p, (r - s_) % p
-        tops = []
+        ops_, buf = [], None
         if computes(s_):
-            t = tile(xs, blocks.pop(s_))
+            buf = torch.empty((counts[src],) + rest, dtype=xs.dtype, device=xs.device)
+            ops_.append(dist.P2POp(dist.irecv, buf, comm._g(src), comm.group))
+        if not (even and s_ == half and r < half):
+            ops_.insert(0, dist.P2POp(dist.isend, xs, comm._g(dst), comm.group))
+        return buf, _SD.batch_isend_irecv(ops_)
+
+    def finish(step):
+        """Wait for a tile exchange, copy its mirrored tile into ``out``; its buffers die here."""
+        works, dst, got, _tt = step
+        for w in works:
+            w.wait()
+        if got is not None:
+            out[:, displs[dst]: displs[dst] + counts[dst]] = got
+
+    nxt = post_block(1) if half >= 1 else None
+    out[:, displs[r]: displs[r] + counts[r]] = tile(xs, xs)    # overlaps the first block transfer
+    prev = None
+    for s_ in range(1, half + 1):
+        dst, src = (r + s_) % p, (r - s_) % p
+        block, works = nxt
+        for w in works:
+            w.wait()
+        nxt = post_block(s_ + 1) if s_ < half else None      # lands under this step's tile
+        tops, tt, got = [], None, None
+        if computes(s_):
+            t = tile(xs, block)
+            del block
             out[:, displs[src]: displs[src] + counts[src]] = t
             tt = t.t().contiguous()
+            del t
             tops.append(dist.P2POp(dist.isend, tt, comm._g(src), comm.group))
-            pending.append(tt)
         if not (even and s_ == half and r < half):
             got = torch.empty((counts[r], counts[dst]), dtype=xs.dtype, device=xs.device)
             tops.append(dist.P2POp(dist.irecv, got, comm._g(dst), comm.group))
-            mirrors.append((dst, got))
-        works = _SD.batch_isend_irecv(tops)
-        pending.append(works)
-    for item in pending:
-        if isinstance(item, list):
-            for w in item:
-                w.wait()
-    for dst, got in mirrors:
-        out[:, displs[dst]: displs[dst] + counts[dst]] = got
+        cur = (_SD.batch_isend_irecv(tops), dst, got, tt)   # tt stays alive until its send is done
+        if prev is not None:
+            finish(prev)
+        prev = cur
+    if prev is not None:
+        finish(prev)
 
 
 def _dist_callable(X: DNDarray, Y: Optional[DNDarray], fn: Callable) -> DNDarray:

@@ -182,7 +182,8 @@ class PartialH5Dataset(torch_data.Dataset):
                     return
                 if not self._put(out, (lo, self._read(lo, hi)), cancel):
                     return
-                self.loads_remaining -= 1
+                if not cancel.is_set():  # a cancelled thread must not touch the next epoch's counter
+                    self.loads_remaining -= 1
         except BaseException as e:  # surfaced in the consumer
             self._put(out, ("error", e), cancel)
             return
@@ -232,8 +233,8 @@ class PartialH5DataLoaderIter:
         self._win = 0
         self._order = []
         self._pos = 0
-        ds.loads_remaining = ds.loads_needed
         ds._stop_loader()  # the previous epoch's thread: finished, or cancelled if abandoned
+        ds.loads_remaining = ds.loads_needed
         if ds.windows and ds.resident_start != ds.windows[0][0]:
             first = getattr(ds, "_next_first", None)
             lo, hi = ds.windows[0]
@@ -278,9 +279,11 @@ class PartialH5DataLoaderIter:
 
     def __next__(self):
         if self._num_yielded >= self.length:
-            # every batch of the epoch was yielded: the loader only has its end marker and the
-            # pre-read of the next epoch's first window left (both fit), so it is not abandoned
-            self.dataset._epoch_done = True
+            # every batch of the epoch was yielded. The loader is finished only once its end marker
+            # was taken off the queue: with drop_last the leftover rows can sit in windows nobody
+            # fetched, and a loader blocked on them must be cancelled by the next epoch, not joined
+            if self._queue is None:
+                self.dataset._epoch_done = True
             raise StopIteration
         items = self._carry
         while len(items) < self.batch_size:

@@ -149,6 +149,28 @@ def check_partial_h5_break_then_full_epoch():
     assert ds.load_thread is None or not ds.load_thread.is_alive() or ds._epoch_done
 
 
+def check_partial_h5_drop_last_big_batches():
+    """drop_last with batch_size > load_length: the leftover rows of an epoch sit in windows the
+    consumer never fetched, so the loader is still blocked on its bounded queue when the epoch
+    ends. The next epoch must cancel it (not join it) and still see every full batch."""
+    comm = ht.MPI_WORLD
+    n = 67 * comm.size
+    path = _h5_file(comm, n)
+    ds = ht.utils.data.PartialH5Dataset(path, comm=comm, dataset_names=["data", "labels"], use_gpu=False,
+                                        initial_load=6, load_length=3)
+    share = n // comm.size
+    lo = comm.rank * share
+    t0 = time.time()
+    for epoch in range(3):
+        loader = ht.utils.data.DataLoader(ds, batch_size=16, drop_last=True)
+        got = torch.cat([y for _, y in loader]).long().tolist()
+        assert len(got) == len(set(got)) == (share // 16) * 16, (epoch, len(got))
+        assert set(got) <= set(range(lo, lo + share))
+        time.sleep(0.1)                 # the loader fills its queue with the unfetched windows
+    assert time.time() - t0 < 60
+    assert ds.loads_remaining >= 0
+
+
 def check_partial_h5_validate_set():
     comm = ht.MPI_WORLD
     n = 9 * comm.size + 1

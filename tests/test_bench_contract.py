@@ -45,6 +45,10 @@ def test_bench_multi_rank_one_json_line(ranks):
     assert rec["extra"]["count_sum_ok"] is True
     assert rec["extra"]["centroid_max_rel_err_vs_fp64"] < 1e-5
     assert rec["extra"]["allreduce_us"] > 0
+    # the labels are the fp64 argmin (sampled on every rank)
+    assert rec["extra"]["labels_checked"] == 3000 * ranks
+    assert rec["extra"]["labels_ok"] is True and rec["extra"]["label_max_excess"] <= 4e-6
+    assert rec["extra"]["label_agreement"] > 0.999
     # whole-job aggregate: 2 n k f flops per step over the max-over-ranks step time
     flops = 2 * 3000 * ranks * 1024 * 64
     assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= 1e-6 * rec["value"]
@@ -113,3 +117,38 @@ def test_bench_failing_rank_fails_the_job():
     r = subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True, timeout=180)
     assert r.returncode != 0
     assert not _json_lines(r.stdout)
+
+
+def test_check_labels_catches_a_wrong_assignment():
+    """bench.check_labels: the argmin labels pass; labels with 1 % of the points moved to a far
+    centroid fail (a wrong assign kernel would pass the centroid checks, which reuse its labels)."""
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from heat_amd.core.communication import MPI_WORLD
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(20000, 16, generator=g)
+    C = torch.randn(64, 16, generator=g)
+    lab = torch.cdist(X.double(), C.double()).argmin(1)
+    ok = bench.check_labels(X, C, lab, MPI_WORLD, sample=4096)
+    assert ok["labels_ok"] and ok["label_agreement"] == 1.0 and ok["labels_checked"] == 4096
+    far = torch.cdist(X.double(), C.double()).argmax(1)
+    bad = torch.where(torch.arange(20000) % 100 == 0, far, lab)
+    res = bench.check_labels(X, C, bad, MPI_WORLD, sample=20000)
+    assert not res["labels_ok"] and res["label_max_excess"] > 1e-2
+    assert abs(res["label_agreement"] - 0.99) < 1e-3
+
+
+def test_bench_shared_gpu_rehearsal_records_itself():
+    """HEAT_BENCH_SHARED_GPU=1: the N-rank job runs on a gloo world whatever the device count and
+    the record says shared_gpu (never a scaling point)."""
+    cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "1", "--warmup", "1", "--n-per-gpu", "2000",
+           "--exact-steps", "0", "--comm-ab", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_clean_env(HEAT_BENCH_SHARED_GPU="1"), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["config"]["shared_gpu"] is True and rec["extra"]["shared_gpu"] is True
+    assert rec["extra"]["world_size_seen_by_rccl"] == 3 and rec["extra"]["labels_ok"] is True
