@@ -52,8 +52,32 @@ def timed(fn: Callable[[], object], trials: int, warmup: int = 1) -> List[float]
     return out
 
 
-def report(benchmark: str, case: Dict, times: List[float], work: Dict = None) -> Dict:
-    """Rank 0 prints {benchmark, case, n_gpus, trials, median/min seconds, derived rates}."""
+def torch_reference(fn: Callable[[], object], trials: int, warmup: int = 1) -> List[float]:
+    """Wall seconds of the reference's single-GPU torch comparator (``benchmarks/*/torch-gpu.py``
+    of the reference: the same algorithm in plain torch on this process's data), timed with device
+    synchronisation on both sides. Only meaningful in a world of one (the comparator is a 1-GPU
+    protocol); returns [] otherwise."""
+    if ht.MPI_WORLD.size != 1:
+        return []
+    for _ in range(warmup):
+        fn()
+    out = []
+    for _ in range(trials):
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        out.append(time.perf_counter() - t0)
+    return out
+
+
+def report(benchmark: str, case: Dict, times: List[float], work: Dict = None,
+           reference: List[float] = None) -> Dict:
+    """Rank 0 prints {benchmark, case, n_gpus, trials, median/min seconds, derived rates}; with
+    ``reference`` (times of :func:`torch_reference`) also ``reference_torch_s`` (median) and
+    ``speedup`` = reference median / this median."""
     times_sorted = sorted(times)
     med = times_sorted[len(times_sorted) // 2]
     rec = {"benchmark": benchmark, "case": case, "n_gpus": ht.MPI_WORLD.size,
@@ -61,6 +85,10 @@ def report(benchmark: str, case: Dict, times: List[float], work: Dict = None) ->
            "median_s": med, "min_s": times_sorted[0], "times_s": times}
     for key, amount in (work or {}).items():
         rec[key] = amount / med
+    if reference:
+        ref = sorted(reference)[len(reference) // 2]
+        rec["reference_torch_s"] = ref
+        rec["speedup"] = ref / med if med > 0 else None
     if ht.MPI_WORLD.rank == 0:
         print(json.dumps(rec), flush=True)
     return rec

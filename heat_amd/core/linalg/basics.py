@@ -173,13 +173,14 @@ def _library_better(M: int, N: int, K: int, exact: bool) -> bool:
 
 
 def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
-          accumulate: bool = False) -> torch.Tensor:
+          accumulate: bool = False, b_upper: bool = False) -> torch.Tensor:
     """``alpha * a @ b`` (``+ out`` when ``accumulate``) for 2-D operands: device fp32 on the
     hand-written MFMA kernels - the fused fp16x3 kernel when the float32 matmul precision allows it,
     else the exact f32-MFMA kernel (both 256 x 256 tiles, any operand layout, 64-bit offsets, so no
     blocking) - except products with too few output tiles to fill the GPU, which run on the library
     with exact fp32 products (:func:`_library_better`); other dtypes / host tensors on torch
-    (blocked below the library's operand limit)."""
+    (blocked below the library's operand limit). ``b_upper``: b is square upper triangular (the
+    caller's guarantee, e.g. CholeskyQR's R^-1): the 256-tile kernels skip its zero half of K."""
     if _native_fp32(a, b) and a.shape[0] == b.shape[1] >= _GRAM_MIN_N and a.shape[1] >= a.shape[0]:
         from ... import ops
 
@@ -214,10 +215,10 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
         from ... import ops
 
         if _split_gemm_ok(a, b):
-            r = ops.gemm_h3(a, b, out=out, alpha=alpha, accumulate=accumulate)
+            r = ops.gemm_h3(a, b, out=out, alpha=alpha, accumulate=accumulate, b_upper=b_upper)
             if r is not None:
                 return r
-        return ops.gemm_f32(a, b, out=out, accumulate=accumulate, alpha=alpha)
+        return ops.gemm_f32(a, b, out=out, accumulate=accumulate, alpha=alpha, b_upper=b_upper)
     r = _mm_blocked(a, b)
     if alpha != 1.0:
         r = r * alpha

@@ -20,6 +20,8 @@ fits comfortably in memory (``mode=None`` -> "complete" when m*m elements <= 2**
 """
 from __future__ import annotations
 
+import os
+
 import collections
 from typing import Optional, Tuple, Union
 
@@ -299,6 +301,10 @@ def _cholqr(local: torch.Tensor, comm, calc_q: bool, distributed: bool):
     return None
 
 
+# HEAT_QR_TRI=0: the R^-1 products as full GEMMs (A/B of the triangular-aware kernels)
+_QR_TRI = os.environ.get("HEAT_QR_TRI", "1") != "0"
+
+
 def _cholqr_native(A: torch.Tensor, comm, calc_q: bool, distributed: bool):
     """CholeskyQR2 of a device fp32 block entirely on the hand-written kernels: the Gram matrices
     (``ops.gram64``: upper-triangle tiles, split-K slices summed in fp64 - an fp64 Gram from fp32
@@ -331,14 +337,15 @@ def _cholqr_native(A: torch.Tensor, comm, calc_q: bool, distributed: bool):
     R1, Ri1 = factor(allreduce(ops.gram64(A)), True)
     if R1 is None:
         return None
-    Q1 = fgemm(A, Ri1.to(dt))
+    # R^-1 is upper triangular: output column tile n0 contracts only k < n0 + 256 (half the work)
+    Q1 = fgemm(A, Ri1.to(dt), b_upper=_QR_TRI)
     R2, Ri2 = factor(allreduce(ops.gram64(Q1)), False)
     if R2 is None:
         return None
     R = ops.gemm64(R2, R1).to(dt)
     if not calc_q:
         return None, R
-    Q = fgemm(Q1, Ri2.to(dt))
+    Q = fgemm(Q1, Ri2.to(dt), b_upper=_QR_TRI)
     return Q, R
 
 

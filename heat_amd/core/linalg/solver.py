@@ -1,9 +1,12 @@
 """
 Iterative solvers (reference ``heat/core/linalg/solver.py``: ``cg`` 13, ``lanczos`` 68).
 
-Lanczos re-orthogonalises against ALL previous Krylov vectors with two GEMVs and ONE all-reduce
-per step (``h = V^T w`` then ``w -= V h``) instead of the reference's two scalar all-reduces per
-(i, j) pair (``solver.py:151-157``, O(m^2) collectives).
+Lanczos re-orthogonalises against ALL previous Krylov vectors with one skinny GEMM and one GEMV
+per step (``h = V^T w`` then ``w -= V h``) and TWO all-reduces per step in all (``[w.w, V^T w]``
+before the matvec, ``[u.u, u^T A u]`` after it, the normalisation deferred past the matvec),
+with no host synchronisation (the breakdown test selects on the device), instead of the
+reference's two scalar all-reduces per (i, j) pair plus norms and dots (``solver.py:140-157``,
+O(m^2) collectives).
 """
 from __future__ import annotations
 
@@ -97,19 +100,29 @@ def lanczos(A: DNDarray, m: int, v0: Optional[DNDarray] = None, V_out: Optional[
     w = w - alpha * v
     T[0, 0] = alpha
     V[:, 0] = v
+    # breakdown replacements (beta ~ 0): drawn from a private generator so the global RNG state
+    # does not depend on the step count, and selected on the device - no host sync per step
+    # (one seed on every rank for replicated vectors, one per rank for their blocks)
+    gen = torch.Generator(device=dev).manual_seed(0x5EED + (comm.rank if dist else 0))
     for i in range(1, m):
-        beta = torch.sqrt(gdot((w @ w).reshape(1))[0])
-        if float(beta) < 1e-10:
-            vr = htrandom.rand(n, dtype=dtype, split=vsplit, device=A.device, comm=comm).larray
-            w = vr
-        # full re-orthogonalisation against V[:, :i]: one all-reduce of i coefficients
-        h = gdot((V[:, :i].T @ w).contiguous())
-        w = w - V[:, :i] @ h
-        nrm = torch.sqrt(gdot((w @ w).reshape(1))[0])
-        vi = w / nrm
-        w = matmul(A, as_vec(vi)).larray.to(tt)
-        alpha = gdot((w @ vi).reshape(1))[0]
-        w = w - alpha * vi - beta * V[:, i - 1]
+        # ONE all-reduce for beta^2 = w.w and the re-orthogonalisation coefficients of both the
+        # residual w and its breakdown replacement r: [w.w, V^T w, V^T r] (V read once)
+        r = torch.rand(w.shape, generator=gen, dtype=tt, device=dev)
+        Vi = V[:, :i]
+        red = torch.cat([(w @ w).reshape(1), (Vi.T @ torch.stack([w, r], 1)).T.reshape(-1)])
+        red = gdot(red)
+        beta = torch.sqrt(red[0])
+        broke = beta < 1e-10
+        h = torch.where(broke, red[1 + i:], red[1: 1 + i])
+        u = torch.where(broke, r, w) - Vi @ h
+        # normalisation deferred past the matvec: y = A u, then ONE all-reduce of [u.u, y.u] gives
+        # |u| and alpha = u^T A u / u.u (the reference's dot after normalising, solver.py:140-157)
+        y = matmul(A, as_vec(u)).larray.to(tt)
+        red2 = gdot(torch.stack([u @ u, y @ u]))
+        nrm = torch.sqrt(red2[0])
+        vi = u / nrm
+        alpha = red2[1] / red2[0]
+        w = y / nrm - alpha * vi - beta * V[:, i - 1]
         T[i - 1, i] = beta
         T[i, i - 1] = beta
         T[i, i] = alpha

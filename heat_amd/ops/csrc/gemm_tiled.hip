@@ -40,6 +40,9 @@ constexpr int TB = 256;        // block tile (rows and columns)
 constexpr int TK = 16;         // K per stage
 constexpr int TSTAGE = 32768;  // bytes per stage
 constexpr int TNBUF = 4;       // LDS stage buffers
+// bits of the kernels' ``upper`` argument
+constexpr int TG_UPPER_TILES = 1;  // square C: only the 256-tiles on or above the diagonal
+constexpr int TG_B_UPPER = 2;      // B upper triangular (B[k][n] = 0 for k > n): K clipped per column tile
 
 __device__ __forceinline__ int64_t tg_xcd_remap(int64_t orig, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8, xcd = orig % 8, loc = orig / 8;
@@ -142,9 +145,11 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
   __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * TSTAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int64_t m0, n0;
-  tg_tile(Mp / TB, Np / TB, upper, m0, n0);
+  tg_tile(Mp / TB, Np / TB, upper & TG_UPPER_TILES, m0, n0);
   // split-K: slice blockIdx.y covers stages [y kps, min((y + 1) kps, Kp / TK)) into C + y cslice
   const int64_t t0 = (int64_t)blockIdx.y * kps;
+  // B upper triangular: column tile n0 only needs k < n0 + 256 (the rest of K multiplies zeros)
+  if (upper & TG_B_UPPER) Kp = Kp < n0 + TB ? Kp : n0 + TB;
   C += (int64_t)blockIdx.y * cslice;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r = lane & 31;
@@ -194,7 +199,8 @@ __global__ __launch_bounds__(256, 1) void gemm_h3t(const _Float16* __restrict__ 
     }
   };
 
-  const int64_t nk = Kp / TK - t0 < kps ? Kp / TK - t0 : kps;
+  int64_t nk = Kp / TK - t0 < kps ? Kp / TK - t0 : kps;
+  nk = nk > 0 ? nk : 0;   // a split-K slice wholly beyond a triangular B's clipped K stores zeros
   // Steady-state stage (t + 3 < nk, no branches, so the scheduler sees one region per half): the
   // DMA of stage t+3 issued between the first accumulator row's MFMAs, the counted wait for stage
   // t+1 + barrier, then stage t+1's 16 fragment reads spread between the other 36 MFMAs. Every
@@ -337,13 +343,17 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
   __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * F32_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int64_t m0, n0;
-  tg_tile((M + TB - 1) / TB, (N + TB - 1) / TB, upper, m0, n0);
+  tg_tile((M + TB - 1) / TB, (N + TB - 1) / TB, upper & TG_UPPER_TILES, m0, n0);
+  // B upper triangular: column tile n0 only needs k < n0 + 256 (the rest of K multiplies zeros;
+  // n0 + 256 is a multiple of 16, so no new K tail appears)
+  if (upper & TG_B_UPPER) K = K < n0 + TB ? K : n0 + TB;
   // split-K: slice blockIdx.y = k in [y kps TK, min((y + 1) kps TK, K)) into C + y cslice
   {
     const int64_t k0 = (int64_t)blockIdx.y * kps * TK;
     A += AK ? k0 * lda : k0;
     B += BK_ ? k0 * ldb : k0;
     K = K - k0 < kps * TK ? K - k0 : kps * TK;
+    K = K > 0 ? K : 0;   // a slice wholly beyond the clipped K: zero partial
     C += (int64_t)blockIdx.y * cslice;
   }
   const int wm = wave >> 1, wn = wave & 1;
@@ -782,7 +792,7 @@ template <bool AK, bool BK_>
 int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, float alpha, int beta, int upper, int64_t slices, int64_t cslice, hipStream_t s) {
   const int64_t nbm = (M + TB - 1) / TB, nbn = (N + TB - 1) / TB;
-  const int64_t nwg = upper ? nbn * (nbn + 1) / 2 : nbm * nbn;
+  const int64_t nwg = (upper & TG_UPPER_TILES) ? nbn * (nbn + 1) / 2 : nbm * nbn;
   if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
   const int64_t nk = (K + TK - 1) / TK, kps = (nk + slices - 1) / slices;
   const dim3 grid((unsigned)nwg, (unsigned)((nk + kps - 1) / kps));
@@ -847,11 +857,13 @@ HA_EXPORT int ha_sum_slices32(const float* P, int64_t S, int64_t M, int64_t N, i
 // Requirements (else HA_UNSUPPORTED, the caller uses ha_gemm_f32): 16-byte aligned bases, leading
 // dimensions multiples of 4, the contiguous extent of each operand a multiple of 4, M, N >= 4.
 // slices > 1: split-K - slice s of the K range (multiples of 16) goes to C + s cslice (partials
-// for ha_sum_slices64). upper (M == N): only the 256-tiles on or above the diagonal are computed.
+// for ha_sum_slices64). upper bit 1 (M == N): only the 256-tiles on or above the diagonal are
+// computed; bit 2: B is upper triangular (B(k, n) = 0 for k > n, e.g. an R^-1 factor): column tile
+// n0 runs its K loop only to min(K, n0 + 256) - the zero half of K is never loaded or multiplied.
 HA_EXPORT int ha_gemm_f32t(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                            int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, float alpha, int beta, int upper,
                            int64_t slices, int64_t cslice, void* stream) {
-  if (M < 0 || N < 0 || K < 0 || !A || !B || !C || slices < 1 || (upper && M != N)) return HA_BAD_ARG;
+  if (M < 0 || N < 0 || K < 0 || !A || !B || !C || slices < 1 || ((upper & TG_UPPER_TILES) && M != N)) return HA_BAD_ARG;
   if (M == 0 || N == 0) return HA_OK;
   if (K < 4 || M < 4 || N < 4 || lda % 4 || ldb % 4 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return HA_UNSUPPORTED;
   if ((a_kmajor ? M : K) % 4 || (b_kmajor ? N : K) % 4) return HA_UNSUPPORTED;
@@ -874,11 +886,11 @@ HA_EXPORT int ha_gemm_h3t(const void* Ahi, const void* Alo, const void* Bhi, con
                           int64_t ldc, float alpha, int beta, int upper, int64_t slices, int64_t cslice,
                           void* stream) {
   if (M < 0 || N < 0 || Kp < 0 || Kp % TK || Mp % TB || Np % TB || Mp < M || Np < N) return HA_BAD_ARG;
-  if (slices < 1 || (upper && (M != N || Mp != Np))) return HA_BAD_ARG;
+  if (slices < 1 || ((upper & TG_UPPER_TILES) && (M != N || Mp != Np))) return HA_BAD_ARG;
   if (M == 0 || N == 0) return HA_OK;
   if ((((uintptr_t)Ahi | (uintptr_t)Alo | (uintptr_t)Bhi | (uintptr_t)Blo) & 15) != 0) return HA_BAD_ARG;
   const int64_t nbn = Np / TB;
-  const int64_t nwg = upper ? nbn * (nbn + 1) / 2 : (Mp / TB) * nbn;
+  const int64_t nwg = (upper & TG_UPPER_TILES) ? nbn * (nbn + 1) / 2 : (Mp / TB) * nbn;
   if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
   const int64_t nk = Kp / TK, kps = nk > 0 ? (nk + slices - 1) / slices : 1;
   const dim3 grid((unsigned)nwg, (unsigned)(nk > 0 ? (nk + kps - 1) / kps : 1));

@@ -1128,14 +1128,17 @@ _HA_UNSUPPORTED = 2
 
 
 def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
-             accumulate: bool = False, alpha: float = 1.0, slices: Optional[int] = None) -> torch.Tensor:
+             accumulate: bool = False, alpha: float = 1.0, slices: Optional[int] = None,
+             b_upper: bool = False) -> torch.Tensor:
     """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on the f32-input matrix cores:
     fp32 products and accumulation in k order like any fp32 GEMM, every operand layout
     (row-/column-major views such as ``x.T @ x``) without a copy, 64-bit offsets (no 4 GB operand
     limit). The 256 x 256-tile pipelined kernel (``csrc/gemm_tiled.hip: gemm_f32t``) takes
     16-byte-aligned operands whose contiguous extents are multiples of 4; anything else runs on
     the 128-tile kernel (``csrc/gemm_mfma.hip``). ``out``: a row-major fp32 [M, N] view (e.g. a
-    row block of a larger result)."""
+    row block of a larger result). ``b_upper``: b is square and upper triangular (the caller's
+    guarantee, e.g. an R^-1 factor): output column tile n0 contracts only k < n0 + 256, so the zero
+    half of K is never loaded or multiplied (~half the work at K = N = 4096)."""
     if not (a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32 \
             or a.dim() != 2 or b.dim() != 2:
         res = alpha * (a @ b) if alpha != 1.0 else a @ b
@@ -1160,20 +1163,21 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     L = lib()
     st = ctypes.c_void_p(stream_ptr(a.device))
     ldc = out.stride(0) if M > 1 else N
+    ub = _TG_B_UPPER if (b_upper and K == N) else 0
     if slices is None:
         slices = _splitk_slices(M, N, K, a.device)
     if slices > 1:
         # few 256 x 256 output tiles: split K so the grid fills the CUs, fp32 partial per slice,
         # slices summed in fixed order (fp64) with alpha / accumulate in the same pass
         P = torch.empty(slices * M * N, dtype=torch.float32, device=a.device)
-        rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(P), M, N, K, lda, ldb, N, int(a_km), int(not b_nm), 1.0, 0, 0,
+        rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(P), M, N, K, lda, ldb, N, int(a_km), int(not b_nm), 1.0, 0, ub,
                             slices, M * N, st)
         if rc == 0:
             check(L.ha_sum_slices32(_ptr(P), L.ha_gemm_tiled_slices(K, slices), M, N, M * N, _ptr(out), ldc,
                                     float(alpha), int(accumulate), st), "ha_sum_slices32")
             return out
     rc = L.ha_gemm_f32t(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(not b_nm),
-                        float(alpha), int(accumulate), 0, 1, 0, st)
+                        float(alpha), int(accumulate), ub, 1, 0, st)
     if rc == _HA_UNSUPPORTED:
         if alpha != 1.0:
             tmp = gemm_f32(a, b)
@@ -1279,8 +1283,14 @@ def h3_planes(x: torch.Tensor, contract_dim: int) -> H3Planes:
     return H3Planes(hi, lo, ex, flag, R, Rp, Kp)
 
 
-def gemm_h3_planes(pa: H3Planes, pb: H3Planes, out: torch.Tensor, alpha: float = 1.0, accumulate: bool = False):
-    """``out (+)= alpha * A @ B`` from pre-split operands (see :func:`h3_planes`)."""
+_TG_B_UPPER = 2   # gemm_tiled.hip: bit of the ``upper`` argument - B upper triangular, K clipped per column tile
+
+
+def gemm_h3_planes(pa: H3Planes, pb: H3Planes, out: torch.Tensor, alpha: float = 1.0, accumulate: bool = False,
+                   b_upper: bool = False):
+    """``out (+)= alpha * A @ B`` from pre-split operands (see :func:`h3_planes`). ``b_upper``: B is
+    upper triangular (caller's guarantee), so output column tile n0 contracts only k < n0 + 256."""
+    ub = _TG_B_UPPER if b_upper else 0
     if pa.Kp != pb.Kp:
         raise ValueError("gemm_h3_planes: contraction lengths differ")
     M, N = pa.rows, pb.rows
@@ -1290,24 +1300,24 @@ def gemm_h3_planes(pa: H3Planes, pb: H3Planes, out: torch.Tensor, alpha: float =
     if slices > 1:   # few output tiles: split K (see gemm_f32)
         P = torch.empty(slices * M * N, dtype=torch.float32, device=out.device)
         check(L.ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(P), M,
-                            N, pa.Kp, pa.Rp, pb.Rp, N, 1.0, 0, 0, slices, M * N, st), "ha_gemm_h3t")
+                            N, pa.Kp, pa.Rp, pb.Rp, N, 1.0, 0, ub, slices, M * N, st), "ha_gemm_h3t")
         check(L.ha_sum_slices32(_ptr(P), L.ha_gemm_tiled_slices(pa.Kp, slices), M, N, M * N, _ptr(out),
                                 out.stride(0) if M > 1 else N, float(alpha), int(accumulate), st), "ha_sum_slices32")
         return out
     check(L.ha_gemm_h3t(_ptr(pa.hi), _ptr(pa.lo), _ptr(pb.hi), _ptr(pb.lo), _ptr(pa.ex), _ptr(pb.ex), _ptr(out),
                         M, N, pa.Kp, pa.Rp, pb.Rp, out.stride(0) if M > 1 else N, float(alpha), int(accumulate),
-                        0, 1, 0, st), "ha_gemm_h3t")
+                        ub, 1, 0, st), "ha_gemm_h3t")
     return out
 
 
 def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
-            accumulate: bool = False) -> Optional[torch.Tensor]:
+            accumulate: bool = False, b_upper: bool = False) -> Optional[torch.Tensor]:
     """fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) by the fused fp16x3 MFMA kernel
     (``csrc/gemm_tiled.hip: gemm_h3t``): power-of-two scaled fp16 hi/lo planes of both operands,
     one 256 x 256-tile kernel forming hi.hi + hi.lo + lo.hi with fp32 accumulation and the exact
     unscale in its epilogue. Accuracy of an fp32 GEMM (errors <= ~2^-21 |a||b| per product).
     ``x.T @ x`` splits x once. Returns None for non-finite operands (the caller falls back; the
-    check is one host sync)."""
+    check is one host sync). ``b_upper``: b is upper triangular (see :func:`gemm_f32`)."""
     M, K = a.shape
     N = b.shape[1]
     if out is None:
@@ -1323,7 +1333,7 @@ def gemm_h3(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     pb = pa if _is_gram(a, b) else h3_planes(b, 0)
     if int((pa.flag + pb.flag).item()) != 0:
         return None
-    return gemm_h3_planes(pa, pb, out, alpha, accumulate)
+    return gemm_h3_planes(pa, pb, out, alpha, accumulate, b_upper=b_upper and K == N)
 
 
 _GRAM_KCHUNK = max(16, int(os.environ.get("HEAT_GRAM_KCHUNK", "4096")) // 16 * 16)

@@ -223,3 +223,32 @@ def check_ipc_halo():
         assert np.allclose(ht.diff(x, axis=split).numpy(), np.diff(a, axis=split))
     assert getattr(comm, "_ipc", None) is not None, "the IPC path was not taken"
     assert comm._ipc.error() == 0
+
+
+def check_ipc_iterative_paths():
+    """The latency-bound iterative paths ride the IPC one-shot when HEAT_IPC_ALLREDUCE=1: the
+    distributed Householder QR (one fp64 column-sum all-reduce per column) and Lanczos (two
+    all-reduces per step) take ``allreduce:ipc`` (PATH_COUNTS) and stay correct."""
+    from heat_amd.core.communication import PATH_COUNTS
+
+    assert os.environ.get("HEAT_IPC_ALLREDUCE") == "1"
+    comm = ht.MPI_WORLD
+    rng = np.random.default_rng(11)
+    a_np = rng.standard_normal((300, 40))
+    before = PATH_COUNTS["allreduce:ipc"]
+    q, r = ht.linalg.qr(ht.array(a_np, split=0, device="gpu"), mode="complete")
+    qq, rr = q.numpy(), r.numpy()
+    assert np.allclose(qq @ rr, a_np, atol=1e-8)
+    assert np.allclose(qq.T @ qq, np.eye(300), atol=1e-8)
+    hh = PATH_COUNTS["allreduce:ipc"] - before
+    assert hh >= 40, hh                     # at least one per column
+    spd = a_np.T @ a_np + np.eye(40)
+    before = PATH_COUNTS["allreduce:ipc"]
+    V, T = ht.lanczos(ht.array(spd, split=0, device="gpu"), 12,
+                      v0=ht.array(np.ones(40) / np.sqrt(40), split=0, device="gpu"))
+    vv = V.numpy()
+    assert np.allclose(vv.T @ vv, np.eye(12), atol=1e-8)
+    assert PATH_COUNTS["allreduce:ipc"] - before >= 2 * 11
+    assert comm._ipc.error() == 0
+    if comm.rank == 0:
+        print("PATH_COUNTS", dict(PATH_COUNTS), flush=True)

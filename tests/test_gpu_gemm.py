@@ -327,3 +327,40 @@ def test_fgemm_native_plan_products(m, k, n):
     out = torch.ones(m, n, device=dev)
     basics.fgemm(a, b, out=out, alpha=2.0, accumulate=True)
     assert torch.all((out.double() - (1 + 2 * ref)).abs() <= 2 * _bound(a, b) + 1e-6)
+
+
+@pytest.mark.parametrize("m,n", [(1000, 260), (4099, 1000), (2048, 1536), (300, 4), (777, 513)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+@pytest.mark.parametrize("kernel", ["f32", "f32_split", "h3"])
+def test_gemm_b_upper_triangular(m, n, layout, kernel):
+    """``b_upper``: B square upper triangular, output column tile n0 contracts only k < n0 + 256.
+    fp64-bounded like the full product, every operand layout, N not a multiple of 256, split-K
+    slices wholly beyond a tile's clipped K (their partials must be zero), and the result equal
+    to the full kernel's where every skipped product is a multiplication by zero."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + 31 * n)
+    a = torch.randn(m, n, generator=g).to(dev)
+    b = torch.triu(torch.randn(n, n, generator=g) + 2 * torch.eye(n)).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    ref = a.double() @ b.double()
+    if kernel == "h3":
+        c = ops.gemm_h3(A, B, b_upper=True)
+        full = ops.gemm_h3(A, B)
+        bound = 8 * n * 2.0 ** -24 * (a.abs().double() @ b.abs().double()) + 1e-30
+    else:
+        sl = 4 if kernel == "f32_split" else None
+        c = ops.gemm_f32(A, B, b_upper=True, slices=sl)
+        full = ops.gemm_f32(A, B, slices=sl)
+        bound = _bound(a, b)
+    err = (c.double() - ref).abs()
+    assert torch.all(err <= bound), err.max()
+    if kernel != "h3":
+        # skipping exact zeros changes no partial sum of a k-ordered chain: bit-identical
+        assert torch.equal(c, full)
+    # alpha / accumulate ride along
+    out = torch.ones(m, n, device=dev)
+    ops.gemm_f32(A, B, out=out, accumulate=True, alpha=0.5, b_upper=True)
+    assert torch.allclose(out.double(), 1 + 0.5 * ref, rtol=1e-5, atol=1e-3 * n ** 0.5)

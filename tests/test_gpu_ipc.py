@@ -30,3 +30,8 @@ def test_ipc_allgather_two_shot(gpu, nprocs):
 def test_ipc_halo(gpu, nprocs):
     run_distributed("tests.ipc_checks:check_ipc_halo", nprocs, timeout=110, keep_gpu=True,
                     env_extra={"HEAT_IPC_ALLREDUCE": "1"})
+
+
+def test_ipc_iterative_paths(gpu):
+    run_distributed("tests.ipc_checks:check_ipc_iterative_paths", 2, timeout=110, keep_gpu=True,
+                    env_extra={"HEAT_IPC_ALLREDUCE": "1"})
