@@ -136,10 +136,30 @@ __global__ __launch_bounds__(256, GKT == 16 ? 3 : 2) void gemm_f32s(const float*
   };
 
   floatx16 acc[2][2];
+  if (beta == 2) {
+    // C preloaded into the accumulators (acc = alpha C, alpha = +-1 checked by the host) before
+    // the first stage's loads: the epilogue only stores alpha acc = C + alpha A B (see gemm_f32t)
+    const bool fullc = m0 + GB <= M && n0 + GB <= N;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int bm = 0; bm < 2; ++bm) {
+      const int64_t rb0 = m0 + wm * 64 + bm * 32 + 4 * h;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (floatx16)(0.f);
+      for (int bn = 0; bn < 2; ++bn) {
+        const int64_t gc = n0 + wn * 64 + bn * 32 + r;
+        const float* cp = C + rb0 * ldc + gc;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int dr = (g & 3) + 8 * (g >> 2);
+          acc[bm][bn][g] = (fullc || (rb0 + dr < M && gc < N)) ? alpha * cp[dr * ldc] : 0.f;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = (floatx16)(0.f);
+  }
   auto compute = [&](int buf) {
     const float* As = sm + buf * ST_SZ;
     const float* Bs = As + A_SZ;
@@ -203,7 +223,7 @@ __global__ __launch_bounds__(256, GKT == 16 ? 3 : 2) void gemm_f32s(const float*
         const int dr = (g & 3) + 8 * (g >> 2);
         if (full || (rb0 + dr < M && gc < N)) {
           float v = alpha * acc[bm][bn][g];
-          if (beta) v += cp[dr * ldc];
+          if (beta == 1) v += cp[dr * ldc];
           cp[dr * ldc] = v;
         }
       }
@@ -236,6 +256,9 @@ HA_EXPORT int ha_gemm_f32s(const float* A, const float* B, float* C, int64_t M, 
   if (M <= 0 || N <= 0) return HA_OK;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || (lda & 3) || (ldb & 3)) return HA_UNSUPPORTED;
   if (slices > 1 && beta) return HA_BAD_ARG;
+  // accumulate with alpha = +-1: C preloaded into the accumulators (HEAT_GEMM_F32_PRELOAD=0: off)
+  static const int preload = getenv("HEAT_GEMM_F32_PRELOAD") ? atoi(getenv("HEAT_GEMM_F32_PRELOAD")) : 1;
+  if (beta) beta = (preload && (alpha == 1.f || alpha == -1.f)) ? 2 : 1;
   const int64_t tiles = ((M + GB - 1) / GB) * ((N + GB - 1) / GB);
   const int64_t kps = ha_gemm_f32s_kps(K, slices);
   const int64_t ns = ha_gemm_f32s_slices(K, slices);

@@ -43,6 +43,7 @@ constexpr int TNBUF = 4;       // LDS stage buffers
 // bits of the kernels' ``upper`` argument
 constexpr int TG_UPPER_TILES = 1;  // square C: only the 256-tiles on or above the diagonal
 constexpr int TG_B_UPPER = 2;      // B upper triangular (B[k][n] = 0 for k > n): K clipped per column tile
+constexpr int TG_PAIRED = 4;       // with TG_B_UPPER: one workgroup per column-tile pair (p, nbn - 1 - p)
 
 __device__ __forceinline__ int64_t tg_xcd_remap(int64_t orig, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8, xcd = orig % 8, loc = orig / 8;
@@ -103,6 +104,23 @@ __device__ __forceinline__ void tg_store_tile(floatx16 (&acc)[4][4], float* __re
     int er[16];
 #pragma unroll
     for (int g = 0; g < 16; ++g) er[g] = es ? es[rl + (g & 3) + 8 * (g >> 2)] : 0;
+    // beta: the C values of all four 32 x 32 blocks of this accumulator row are loaded before any
+    // is used (64 loads in flight; the fragment registers are dead here), one memory round trip
+    // per row instead of one per block
+    float cv[4][16];
+    if (beta) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t gn = n0 + wn * 128 + j * 32 + r;
+        const bool colok = full || gn < N;
+        const float* cb = C + (m0 + rl) * ldc + gn;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int dr = (g & 3) + 8 * (g >> 2);
+          cv[j][g] = (colok && (full || m0 + rl + dr < M)) ? cb[dr * ldc] : 0.f;
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int cl = wn * 128 + j * 32 + r;
@@ -110,24 +128,16 @@ __device__ __forceinline__ void tg_store_tile(floatx16 (&acc)[4][4], float* __re
       const bool colok = full || gn < N;
       const int ec = es ? es[256 + cl] : 0;
       float* cb = C + (m0 + rl) * ldc + gn;
-      float cv[16];
-      if (beta) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const int dr = (g & 3) + 8 * (g >> 2);
-          cv[g] = (colok && (full || m0 + rl + dr < M)) ? cb[dr * ldc] : 0.f;
-        }
-      }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int dr = (g & 3) + 8 * (g >> 2);
         float v = es ? ldexpf(acc[i][j][g], -(er[g] + ec)) : acc[i][j][g];
         v *= alpha;
-        if (beta) v += cv[g];
+        if (beta) v += cv[j][g];
         if (colok && (full || m0 + rl + dr < M)) cb[dr * ldc] = v;
       }
-      asm volatile("" ::: "memory");
     }
+    asm volatile("" ::: "memory");
   }
 }
 
@@ -335,15 +345,42 @@ struct F32Src {
 
 // SP: every wave moves 4 pieces of A and 4 of B (pieces 4 wave .. 4 wave + 3 of each, interleaved)
 // - else waves 0, 1 move A and waves 2, 3 move B.
-template <bool AK, bool BK_, bool MI16, bool SP>
-__global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A, const float* __restrict__ B,
-                                                    float* __restrict__ C, int64_t M, int64_t N, int64_t K,
+// PRE: accumulate with alpha = +-1, C preloaded into the accumulators (beta == 2). PAIR: triangular
+// B, one workgroup per column-tile pair (TG_PAIRED). Separate instantiations: the default kernels
+// keep their register allocation.
+template <bool AK, bool BK_, bool MI16, bool SP, bool PRE = false, bool PAIR = false>
+__global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A_, const float* __restrict__ B_,
+                                                    float* __restrict__ C_, int64_t M, int64_t N, int64_t K_,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
                                                     int upper, int64_t kps, int64_t cslice) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[TNBUF * F32_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // B upper triangular + TG_PAIRED: the workgroup computes column tiles p and nbn - 1 - p of one
+  // row panel one after the other - (p + 1) + (nbn - p) k-blocks, the same for every workgroup,
+  // so the tiles an XCD runs at once stay in step over the shared A panel (with one tile per
+  // workgroup the short tiles finish early and their successors re-stream A panels out of step)
+  const int64_t nbm = (M + TB - 1) / TB, nbn = (N + TB - 1) / TB;
+  constexpr bool paired = PAIR;
+#pragma nounroll
+  for (int pass = 0; pass < (paired ? 2 : 1); ++pass) {
+  const float* A = A_;
+  const float* B = B_;
+  float* C = C_;
+  int64_t K = K_;
   int64_t m0, n0;
-  tg_tile((M + TB - 1) / TB, (N + TB - 1) / TB, upper & TG_UPPER_TILES, m0, n0);
+  if constexpr (paired) {
+    const int64_t np = (nbn + 1) / 2;
+    const int64_t bid = tg_xcd_remap(blockIdx.x, nbm * np), pp = bid % np;
+    const int64_t j = pass == 0 ? pp : nbn - 1 - pp;
+    if (pass == 1) {
+      if (j == pp) break;   // odd nbn: the middle tile has no partner
+      __syncthreads();      // every wave is done with the first tile's stage buffers
+    }
+    m0 = (bid / np) * TB;
+    n0 = j * TB;
+  } else {
+    tg_tile(nbm, nbn, upper & TG_UPPER_TILES, m0, n0);
+  }
   // B upper triangular: column tile n0 only needs k < n0 + 256 (the rest of K multiplies zeros;
   // n0 + 256 is a multiple of 16, so no new K tail appears)
   if (upper & TG_B_UPPER) K = K < n0 + TB ? K : n0 + TB;
@@ -517,6 +554,29 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc16[i][j] = (floatx4)(0.f);
+  } else if (PRE) {
+    // C enters the accumulators (acc = alpha C: exact for the host-checked alpha = +-1), loaded
+    // before the first stage's DMA is issued, so the loads' latency hides under the prologue's
+    // and the counted wait for stage 0 covers them; the epilogue then only STORES alpha acc =
+    // C + alpha A B (a beta epilogue exposed one C load round trip per 32 x 32 block: 16 per tile,
+    // which the short-K updates of the Householder QR - 16 k-stages per tile - could not hide)
+    const int h = lane >> 5, r = lane & 31;
+    const bool full = m0 + TB <= M && n0 + TB <= N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t rg = m0 + wm * 128 + i * 32 + 4 * h;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t gn = n0 + wn * 128 + j * 32 + r;
+        const bool colok = full || gn < N;
+        const float* cb = C + rg * ldc + gn;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int dr = (g & 3) + 8 * (g >> 2);
+          acc[i][j][g] = (colok && (full || rg + dr < M)) ? alpha * cb[dr * ldc] : 0.f;
+        }
+      }
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -643,8 +703,9 @@ __global__ __launch_bounds__(256, 1) void gemm_f32t(const float* __restrict__ A,
       asm volatile("" ::: "memory");
     }
   } else {
-    tg_store_tile(acc, C, M, N, ldc, m0, n0, wm, wn, lane >> 5, lane & 31, alpha, beta, nullptr);
+    tg_store_tile(acc, C, M, N, ldc, m0, n0, wm, wn, lane >> 5, lane & 31, alpha, PRE ? 0 : beta, nullptr);
   }
+  }  // pass
 }
 
 // ------------------------------------------------------------------------ h3 operand splitting
@@ -791,18 +852,32 @@ __global__ __launch_bounds__(256) void tg_split_cols(const float* __restrict__ X
 template <bool AK, bool BK_>
 int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, float alpha, int beta, int upper, int64_t slices, int64_t cslice, hipStream_t s) {
-  const int64_t nbm = (M + TB - 1) / TB, nbn = (N + TB - 1) / TB;
-  const int64_t nwg = (upper & TG_UPPER_TILES) ? nbn * (nbn + 1) / 2 : nbm * nbn;
-  if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
-  const int64_t nk = (K + TK - 1) / TK, kps = (nk + slices - 1) / slices;
-  const dim3 grid((unsigned)nwg, (unsigned)((nk + kps - 1) / kps));
   // HEAT_GEMM_F32_SHAPE=16 selects the 16x16x4 MFMA shape, HEAT_GEMM_F32_SPREAD=0 the A-waves /
   // B-waves DMA split (A/B benchmarking)
   static const int shape = getenv("HEAT_GEMM_F32_SHAPE") ? atoi(getenv("HEAT_GEMM_F32_SHAPE")) : 32;
   static const int spread = getenv("HEAT_GEMM_F32_SPREAD") ? atoi(getenv("HEAT_GEMM_F32_SPREAD")) : 1;
+  // beta with alpha = +-1 and one slice: C preloaded into the accumulators (beta = 2, 32 x 32
+  // shape only); HEAT_GEMM_F32_PRELOAD=0 keeps the load-in-epilogue form (A/B)
+  static const int preload = getenv("HEAT_GEMM_F32_PRELOAD") ? atoi(getenv("HEAT_GEMM_F32_PRELOAD")) : 1;
+  // triangular B: one workgroup per column-tile pair; HEAT_GEMM_TRI_PAIRED=0 one tile each (A/B)
+  static const int pair_env = getenv("HEAT_GEMM_TRI_PAIRED") ? atoi(getenv("HEAT_GEMM_TRI_PAIRED")) : 1;
+  if (beta) beta = (preload && shape != 16 && slices == 1 && (alpha == 1.f || alpha == -1.f)) ? 2 : 1;
+  const bool pair = (upper & TG_B_UPPER) && !(upper & TG_UPPER_TILES) && pair_env && shape != 16 && beta != 2;
+  upper = pair ? (upper | TG_PAIRED) : (upper & ~TG_PAIRED);
+  const int64_t nbm = (M + TB - 1) / TB, nbn = (N + TB - 1) / TB;
+  const int64_t nwg = (upper & TG_UPPER_TILES) ? nbn * (nbn + 1) / 2 : pair ? nbm * ((nbn + 1) / 2) : nbm * nbn;
+  if (nwg > 0x7FFFFFFF || slices > 65535) return HA_UNSUPPORTED;
+  const int64_t nk = (K + TK - 1) / TK, kps = (nk + slices - 1) / slices;
+  const dim3 grid((unsigned)nwg, (unsigned)((nk + kps - 1) / kps));
   if (shape == 16)
     hipLaunchKernelGGL((gemm_f32t<AK, BK_, true, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc,
                        alpha, beta, upper, kps, cslice);
+  else if (beta == 2)
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false, true, true>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb,
+                       ldc, alpha, beta, upper, kps, cslice);
+  else if (pair)
+    hipLaunchKernelGGL((gemm_f32t<AK, BK_, false, true, false, true>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda,
+                       ldb, ldc, alpha, beta, upper, kps, cslice);
   else if (spread)
     hipLaunchKernelGGL((gemm_f32t<AK, BK_, false, true>), grid, dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc,
                        alpha, beta, upper, kps, cslice);

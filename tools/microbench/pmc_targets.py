@@ -11,7 +11,9 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   cdist_exact - exact (difference) cdist, SUSY size 40k x 18, 3 calls (cdist.hip: cdist_vx)
   gemm_small - 1024^3 and 2048^3 exact fp32 through fgemm's plan (gemm_small.hip / gemm_tiled.hip split-K)
   gemm_f32s_big - gemm_f32s alone at 6144^3 and 8192^3 (one K slice)
-  gram    - ht.matmul(A.T, A) at 400000 x 2048 (upper-triangle Gram tiles + fp64 slice sums)"""
+  gram    - ht.matmul(A.T, A) at 400000 x 2048 (upper-triangle Gram tiles + fp64 slice sums)
+  tri     - CholeskyQR2's A R^-1 at 1.25e6 x 4096 (upper-triangular B: K clipped per column tile),
+            2 calls, then the same product as a full GEMM, 1 call"""
 import sys
 
 import torch
@@ -54,6 +56,12 @@ def main():
     elif which == "knn":
         x = ht.random.rand(1_000_000, 128, split=0)
         ht.spatial.cdist_topk(x, x, 8)
+    elif which == "tri":
+        a = torch.randn(1_250_000, 4096, device="cuda")
+        r = torch.triu(torch.randn(4096, 4096, device="cuda")) + 4 * torch.eye(4096, device="cuda")
+        for _ in range(2):
+            ops.gemm_f32(a, r, b_upper=True)
+        ops.gemm_f32(a, r)
     elif which == "randn":
         for _ in range(3):
             ht.random.randn(1_000_000, 800, split=0)

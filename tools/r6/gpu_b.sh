@@ -5,6 +5,7 @@ mkdir -p gpurun_out/r6b
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_gemm.py -k "b_upper" > gpurun_out/r6b/test_tri.txt 2>&1 || exit 1
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_qr.py > gpurun_out/r6b/test_qr.txt 2>&1 || exit 2
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ipc.py > gpurun_out/r6b/test_ipc.txt 2>&1 || exit 6
 echo tests ok
 for tri in 0 1; do
   HEAT_QR_TRI=$tri timeout -k 10 300 python -m benchmarks.linalg.run --ops qr_r,qr --trials 3 > gpurun_out/r6b/linalg_tri$tri.jsonl 2>&1 || exit 3
