@@ -256,8 +256,9 @@ HA_EXPORT int ha_gemm_f32s(const float* A, const float* B, float* C, int64_t M, 
   if (M <= 0 || N <= 0) return HA_OK;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || (lda & 3) || (ldb & 3)) return HA_UNSUPPORTED;
   if (slices > 1 && beta) return HA_BAD_ARG;
-  // accumulate with alpha = +-1: C preloaded into the accumulators (HEAT_GEMM_F32_PRELOAD=0: off)
-  static const int preload = getenv("HEAT_GEMM_F32_PRELOAD") ? atoi(getenv("HEAT_GEMM_F32_PRELOAD")) : 1;
+  // accumulate with alpha = +-1: C preloaded into the accumulators only with HEAT_GEMM_F32_PRELOAD=1
+  // (A/B: slower, and every partial sum rounds at the scale of C, profiles/update_ab_r06.jsonl)
+  static const int preload = getenv("HEAT_GEMM_F32_PRELOAD") ? atoi(getenv("HEAT_GEMM_F32_PRELOAD")) : 0;
   if (beta) beta = (preload && (alpha == 1.f || alpha == -1.f)) ? 2 : 1;
   const int64_t tiles = ((M + GB - 1) / GB) * ((N + GB - 1) / GB);
   const int64_t kps = ha_gemm_f32s_kps(K, slices);

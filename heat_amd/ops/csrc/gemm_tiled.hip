@@ -857,8 +857,9 @@ int f32t_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, 
   static const int shape = getenv("HEAT_GEMM_F32_SHAPE") ? atoi(getenv("HEAT_GEMM_F32_SHAPE")) : 32;
   static const int spread = getenv("HEAT_GEMM_F32_SPREAD") ? atoi(getenv("HEAT_GEMM_F32_SPREAD")) : 1;
   // beta with alpha = +-1 and one slice: C preloaded into the accumulators (beta = 2, 32 x 32
-  // shape only); HEAT_GEMM_F32_PRELOAD=0 keeps the load-in-epilogue form (A/B)
-  static const int preload = getenv("HEAT_GEMM_F32_PRELOAD") ? atoi(getenv("HEAT_GEMM_F32_PRELOAD")) : 1;
+  // shape only) only with HEAT_GEMM_F32_PRELOAD=1 (A/B: 2x slower at K = 256 and 40x the error -
+  // every partial sum rounds at the scale of C; profiles/update_ab_r06.jsonl)
+  static const int preload = getenv("HEAT_GEMM_F32_PRELOAD") ? atoi(getenv("HEAT_GEMM_F32_PRELOAD")) : 0;
   // triangular B: one workgroup per column-tile pair; HEAT_GEMM_TRI_PAIRED=0 one tile each (A/B)
   static const int pair_env = getenv("HEAT_GEMM_TRI_PAIRED") ? atoi(getenv("HEAT_GEMM_TRI_PAIRED")) : 1;
   if (beta) beta = (preload && shape != 16 && slices == 1 && (alpha == 1.f || alpha == -1.f)) ? 2 : 1;

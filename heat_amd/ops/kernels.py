@@ -1189,15 +1189,21 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
 
 
 _GEMM_SMALL = os.environ.get("HEAT_GEMM_SMALL", "1") != "0"
+# the 128-tile kernel: "mid" (LDS-DMA pipelined, csrc/gemm_mid.hip: gemm_f32m) or "s" (the round-5
+# register-staged gemm_f32s, A/B)
+_GEMM_MID = os.environ.get("HEAT_GEMM_MID", "1") != "0"
 
 
 def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
-                   accumulate: bool = False, slices: Optional[int] = None) -> Optional[torch.Tensor]:
-    """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on the 128 x 128-tile kernel
-    with split-K (``csrc/gemm_small.hip: gemm_f32s``): the products whose 256 x 256 tiles cannot
-    fill the GPU (1024^3 .. 6144^3) and short-K tall updates (the Householder rank-256 update).
-    Any row-/column-major operand views; None where the kernel does not apply (host tensors,
-    unaligned operands: the caller picks another GEMM)."""
+                   accumulate: bool = False, slices: Optional[int] = None,
+                   kernel: Optional[str] = None) -> Optional[torch.Tensor]:
+    """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on a 128 x 128-tile kernel with
+    split-K, two workgroups per CU: the products whose 256 x 256 tiles cannot fill the GPU (1024^3
+    .. 6144^3) and short-K tall updates (the Householder rank-256 update). ``kernel``: "mid"
+    (default: LDS-DMA pipeline, ``csrc/gemm_mid.hip: gemm_f32m``) or "s" (register-staged,
+    ``csrc/gemm_small.hip: gemm_f32s``; also where gemm_f32m's operand requirements fail). Any
+    row-/column-major operand views; None where neither kernel applies (host tensors, unaligned
+    operands: the caller picks another GEMM)."""
     if not (_GEMM_SMALL and a.is_cuda and use_native(a)) or a.dtype != torch.float32 or b.dtype != torch.float32 \
             or a.dim() != 2 or b.dim() != 2:
         return None
@@ -1227,16 +1233,27 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
         slices = 1
         if tiles < 2 * ncu and K >= 512:   # two workgroups per CU: split K over the missing ones
             slices = max(1, min(-(-2 * ncu // tiles), K // 256, _SPLITK_MAX_BYTES // (4 * M * N)))
+    mid = (kernel or ("mid" if _GEMM_MID else "s")) == "mid"
+    if mid and ((M if a_km else K) % 4 or (N if not b_nm else K) % 4 or min(M, N, K) < 4):
+        mid = False          # gemm_f32m's operand requirements (contiguous extents multiples of 4)
+    if mid:
+        launch, used_fn = L.ha_gemm_f32m, L.ha_gemm_f32m_slices
+        bflag = int(not b_nm)            # gemm_f32m takes "B k-major"
+    else:
+        launch, used_fn = L.ha_gemm_f32s, L.ha_gemm_f32s_slices
+        bflag = int(b_nm)                # gemm_f32s takes "B n-major"
+    name = "ha_gemm_f32m" if mid else "ha_gemm_f32s"
     if slices > 1:
-        used = L.ha_gemm_f32s_slices(K, slices)
-        P = torch.empty(used * M * N, dtype=torch.float32, device=a.device)
-        check(L.ha_gemm_f32s(_ptr(A), _ptr(B), _ptr(P), M, N, K, lda, ldb, N, int(a_km), int(b_nm), 1.0, 0, slices,
-                             M * N, st), "ha_gemm_f32s")
-        check(L.ha_sum_slices32(_ptr(P), used, M, N, M * N, _ptr(out), ldc, float(alpha), int(accumulate), st),
-              "ha_sum_slices32")
-        return out
-    check(L.ha_gemm_f32s(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), int(b_nm), float(alpha),
-                         int(accumulate), 1, 0, st), "ha_gemm_f32s")
+        used = used_fn(K, slices)
+        if used > 1:
+            P = torch.empty(used * M * N, dtype=torch.float32, device=a.device)
+            check(launch(_ptr(A), _ptr(B), _ptr(P), M, N, K, lda, ldb, N, int(a_km), bflag, 1.0, 0, slices, M * N, st),
+                  name)
+            check(L.ha_sum_slices32(_ptr(P), used, M, N, M * N, _ptr(out), ldc, float(alpha), int(accumulate), st),
+                  "ha_sum_slices32")
+            return out
+    check(launch(_ptr(A), _ptr(B), _ptr(out), M, N, K, lda, ldb, ldc, int(a_km), bflag, float(alpha),
+                 int(accumulate), 1, 0, st), name)
     return out
 
 

@@ -279,10 +279,12 @@ def test_matmul_gram_and_cov_route_to_upper_tiles(gpu):
 
 @pytest.mark.parametrize("m,k,n", [(300, 257, 129), (1024, 1024, 1024), (4099, 132, 68), (64, 4096, 64), (1, 7, 1),
                                    (132, 4, 136), (2000, 36, 4), (5000, 256, 700), (128, 20000, 256), (300, 260, 132),
-                                   (4100, 128, 100)])
+                                   (4100, 128, 100), (1000, 52, 516), (2052, 1028, 260)])
 @pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
-def test_gemm_f32_small_layouts(m, k, n, layout):
-    """128-tile split-K kernel: every operand layout, edges, split-K, alpha / accumulate."""
+@pytest.mark.parametrize("kernel", ["mid", "s"])
+def test_gemm_f32_small_layouts(m, k, n, layout, kernel):
+    """128-tile split-K kernels (LDS-DMA gemm_f32m and register-staged gemm_f32s): every operand
+    layout, edges, K tails, split-K, alpha / accumulate."""
     from heat_amd import ops
 
     dev = _dev()
@@ -291,7 +293,7 @@ def test_gemm_f32_small_layouts(m, k, n, layout):
     b = torch.randn(k, n, generator=g).to(dev)
     A = a if layout[0] == "n" else a.t().contiguous().t()
     B = b if layout[1] == "n" else b.t().contiguous().t()
-    c = ops.gemm_f32_small(A, B)
+    c = ops.gemm_f32_small(A, B, kernel=kernel)
     lda = A.stride(0) if A.stride(1) == 1 else A.stride(1)
     ldb = B.stride(0) if B.stride(1) == 1 else B.stride(1)
     if lda % 4 or ldb % 4:
@@ -302,9 +304,36 @@ def test_gemm_f32_small_layouts(m, k, n, layout):
     assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
     base = torch.randn(m, n, generator=g).to(dev)
     out = base.clone()
-    ops.gemm_f32_small(A, B, out=out, alpha=-0.5, accumulate=True)
+    ops.gemm_f32_small(A, B, out=out, alpha=-0.5, accumulate=True, kernel=kernel)
     ref2 = base.double() - 0.5 * ref
     assert torch.all((out.double() - ref2).abs() <= _bound(a, b) + 1e-6 * base.abs().double())
+    # explicit split-K into a strided column block of a wider C (the Householder update's form)
+    wide = torch.randn(m, n + 12, generator=g).to(dev)
+    ref3 = wide.double().clone()
+    ref3[:, 8: 8 + n] += ref
+    ops.gemm_f32_small(A, B, out=wide[:, 8: 8 + n], accumulate=True, slices=3, kernel=kernel)
+    err = (wide.double() - ref3).abs()
+    assert torch.all(err[:, 8: 8 + n] <= _bound(a, b) + 1e-6 * ref3[:, 8: 8 + n].abs()), kernel
+    assert torch.all(err[:, :8] == 0) and torch.all(err[:, 8 + n:] == 0)
+
+
+@pytest.mark.parametrize("m,n,k", [(20000, 3840, 256), (4096, 768, 32), (9000, 300, 256)])
+def test_gemm_f32_mid_update_shape(m, n, k):
+    """The Householder trailing-update form C[:, j:] -= V X on the LDS-DMA 128-tile kernel (C a
+    column slice of a row-major matrix, V row-major, X k-major) against fp64."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + n + k)
+    A = torch.randn(m, n + 256, generator=g).to(dev)
+    V = torch.randn(m, k, generator=g).to(dev)
+    X = (torch.randn(k, n, generator=g) * 1e-2).to(dev)
+    C = A[:, 256:]
+    ref = C.double() - V.double() @ X.double()
+    left = A[:, :256].clone()
+    assert ops.gemm_f32_small(V, X, out=C, alpha=-1.0, accumulate=True, kernel="mid") is not None
+    assert torch.equal(A[:, :256], left)
+    assert torch.all((C.double() - ref).abs() <= _bound(V, X) + 1e-6 * ref.abs())
 
 
 @pytest.mark.parametrize("m,k,n", [(1000, 1000, 1000), (2048, 2048, 2048), (700, 100000, 300), (3000, 3000, 3000),

@@ -13,7 +13,9 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   gemm_f32s_big - gemm_f32s alone at 6144^3 and 8192^3 (one K slice)
   gram    - ht.matmul(A.T, A) at 400000 x 2048 (upper-triangle Gram tiles + fp64 slice sums)
   tri     - CholeskyQR2's A R^-1 at 1.25e6 x 4096 (upper-triangular B: K clipped per column tile),
-            2 calls, then the same product as a full GEMM, 1 call"""
+            2 calls, then the same product as a full GEMM, 1 call
+  mid     - the LDS-DMA 128-tile gemm_f32m: 3072^3 (3 K slices), 6144^3 (1 slice) and the
+            Householder update C[4e5, 3840] -= V[4e5, 256] X[256, 3840], 2 calls each"""
 import sys
 
 import torch
@@ -56,6 +58,18 @@ def main():
     elif which == "knn":
         x = ht.random.rand(1_000_000, 128, split=0)
         ht.spatial.cdist_topk(x, x, 8)
+    elif which == "mid":
+        torch.set_float32_matmul_precision("highest")
+        for n, sl in ((3072, 3), (6144, 1)):
+            a = torch.randn(n, n, device="cuda")
+            b = torch.randn(n, n, device="cuda")
+            for _ in range(2):
+                ops.gemm_f32_small(a, b, slices=sl, kernel="mid")
+        A = torch.randn(400_000, 4096, device="cuda")
+        V = torch.randn(400_000, 256, device="cuda")
+        X = torch.randn(256, 3840, device="cuda") * 1e-3
+        for _ in range(2):
+            ops.gemm_f32_small(V, X, out=A[:, 256:], alpha=-1.0, accumulate=True, kernel="mid")
     elif which == "tri":
         a = torch.randn(1_250_000, 4096, device="cuda")
         r = torch.triu(torch.randn(4096, 4096, device="cuda")) + 4 * torch.eye(4096, device="cuda")
