@@ -124,9 +124,9 @@ struct GmFrag {
 
 // AK: A k-major ([K][M], m contiguous) - else row-major ([M][K], k contiguous).
 // BK_: B k-major ([K][N], n contiguous) - else n-major ([N][K], k contiguous).
-// NBUF: ring slots (4: 64 KB, two workgroups per CU; 3: 48 KB, three per CU).
+// NBUF: ring slots (4: 64 KB, two workgroups per CU).
 template <bool AK, bool BK_, int NBUF>
-__global__ __launch_bounds__(256, NBUF == 3 ? 3 : 2) void gemm_f32m(const float* __restrict__ A,
+__global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
                                                                       const float* __restrict__ B,
                                                                       float* __restrict__ C, int64_t M, int64_t N,
                                                                       int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
@@ -263,6 +263,12 @@ __global__ __launch_bounds__(256, NBUF == 3 ? 3 : 2) void gemm_f32m(const float*
     mma_row(Fc, 1);
     __builtin_amdgcn_sched_barrier(0);
   };
+  // whole tiles with 128 ldc < 2^31: a uniform 64-bit tile base + 32-bit lane offsets in the
+  // epilogue (the row terms dr ldc are scalar products), no bounds tests - the 64-bit per-element
+  // form was ~1000 VALU per tile-wave against 512 MFMAs on the K = 256 update. (Loading C at the
+  // start of the last k-stage instead measured 18 % slower on that update: 214 VGPRs;
+  // profiles/gemm_mid_r06.jsonl.)
+  const bool fast = full && ldc < (1 << 23);
   auto step = [&](int64_t t, const GmFrag& Fc, GmFrag& Fn) {
     if (t + AHEAD < nk) stage(t + AHEAD, !(tail && t + AHEAD == nk - 1));
     mma_row(Fc, 0);
@@ -291,13 +297,11 @@ __global__ __launch_bounds__(256, NBUF == 3 ? 3 : 2) void gemm_f32m(const float*
     if (t + 1 < nk) step(t + 1, F1, F0);
   }
 
-  // epilogue: element (bm, bn, g) -> C[m0 + crow(bm, g)][n0 + ccol(bn)]. Whole tiles with
-  // 128 ldc < 2^31: a uniform 64-bit tile base + 32-bit lane offsets (row terms dr ldc are scalar
-  // products), no bounds tests - the 64-bit per-element form was ~1000 VALU per tile-wave against
-  // 512 MFMAs on the K = 256 update
-  if (full && ldc < (1 << 23)) {
+  // epilogue: element (bm, bn, g) -> C[m0 + crow(bm, g)][n0 + ccol(bn)]
+  if (fast) {
     float* Ct = C + m0 * ldc + n0;
     const int l = (int)ldc;
+    // one accumulator row's C values (32 loads in flight) before its stores
 #pragma unroll
     for (int bm = 0; bm < 2; ++bm) {
       float cv[2][16];
@@ -346,20 +350,233 @@ __global__ __launch_bounds__(256, NBUF == 3 ? 3 : 2) void gemm_f32m(const float*
   }
 }
 
+// Persistent form (one slice, K % 32 == 0, at least two workgroups' worth of tiles per CU): a
+// grid of two workgroups per CU, each walking its tiles as ONE stream of k-stages, so the DMA of
+// the next tile's first stages is in flight during the current tile's last MFMAs and its epilogue.
+// With one launch-wide grid of equal tiles the two workgroups of a CU start and finish together:
+// their prologue (stage-0 latency) and epilogue (C traffic) phases coincide and leave the SIMDs
+// idle, which 16-stage tiles (the Householder update, K = 256) cannot amortise.
+// Tile order: XCD x = blockIdx % 8 owns the contiguous logical tiles [x Tx, (x + 1) Tx) (grouped
+// GM-row-panel order inside), workgroup j of that XCD takes every Gx-th of them.
+// Wait counting across the epilogue: the epilogue drains vmcnt (after its first C loads), so every
+// stage DMA'd before it has landed - those stages' readies skip the vmcnt and only barrier; the
+// stages DMA'd after it are counted as usual (the epilogue's stores are older than them, and two
+// stages later they are long acknowledged).
+template <bool AK, bool BK_>
+__global__ __launch_bounds__(256, 2) void gemm_f32m_p(const float* __restrict__ A, const float* __restrict__ B,
+                                                       float* __restrict__ C, int64_t M, int64_t N, int64_t K,
+                                                       int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta) {
+  constexpr int NBUF = 4, AHEAD = 3, DPS = 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * MSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, r = lane & 31;
+  const unsigned tn = (unsigned)((N + MB - 1) / MB), tm = (unsigned)((M + MB - 1) / MB);
+  const unsigned tiles = tm * tn;
+  const unsigned x = blockIdx.x % 8, j = blockIdx.x / 8, Gx = gridDim.x / 8;
+  const unsigned Tx = (tiles + 7) / 8, tbeg = x * Tx;
+  const unsigned tend = tbeg + Tx < tiles ? tbeg + Tx : tiles;
+  const unsigned ntl = tbeg + j < tend ? (tend - tbeg - j + Gx - 1) / Gx : 0;
+  const int64_t nk = K / MK;
+  const int64_t TT = (int64_t)ntl * nk;
+  if (TT == 0) return;
+  constexpr unsigned GM = 8;
+  auto tile_of = [&](int64_t i, int64_t& m0, int64_t& n0) {
+    const unsigned L = tbeg + j + (unsigned)i * Gx;
+    const unsigned grp = L / (GM * tn), gfirst = grp * GM;
+    const unsigned gsz = tm - gfirst < GM ? tm - gfirst : GM;
+    m0 = (int64_t)(gfirst + (L % (GM * tn)) % gsz) * MB;
+    n0 = (int64_t)((L % (GM * tn)) / gsz) * MB;
+  };
+  const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  GmSrc<!AK> sa;
+  GmSrc<!BK_> sb;
+  int64_t dT = 0;   // next stage to DMA
+  auto issue = [&]() {
+    if (dT < TT) {
+      const int64_t ks = dT % nk;
+      if (ks == 0) {
+        int64_t dm0, dn0;
+        tile_of(dT / nk, dm0, dn0);
+        sa.init(A, lda, M, dm0, lane);
+        sb.init(B, ldb, N, dn0, lane);
+      }
+      const unsigned dst = sbase + (unsigned)((dT % NBUF) * MSTAGE);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = 2 * wave + i;
+        gm_dma16(sa.src(ks * MK, q), dst + q * 1024);
+        gm_dma16(sb.src(ks * MK, q), dst + MOP + q * 1024);
+      }
+    }
+    ++dT;
+  };
+  auto load = [&](GmFrag& F, int64_t t) {
+    const unsigned char* base = smem + (t % NBUF) * MSTAGE;
+    auto opnd = [&](const unsigned char* b, int w0, bool kc, float (&o)[2][8]) __attribute__((always_inline)) {
+      if (kc) {
+#pragma unroll
+        for (int bl = 0; bl < 2; ++bl) {
+          const int row = w0 + 32 * bl + r;
+          const floatx4 x0 = *reinterpret_cast<const floatx4*>(b + (2 * h) * 2048 + row * 16);
+          const floatx4 x1 = *reinterpret_cast<const floatx4*>(b + (2 * h + 1) * 2048 + row * 16);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            o[bl][s] = x0[s];
+            o[bl][4 + s] = x1[s];
+          }
+        }
+      } else {
+        typedef float floatx2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const floatx2 v = *reinterpret_cast<const floatx2*>(b + (8 * h + s) * 512 + (w0 + 2 * r) * 4);
+          o[0][s] = v[0];
+          o[1][s] = v[1];
+        }
+      }
+    };
+    opnd(base, wm * 64, !AK, F.a);
+    opnd(base + MOP, wn * 64, !BK_, F.b);
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = (floatx16)(0.f);
+  auto mma_row = [&](const GmFrag& F, int bm) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[bm][s], F.b[bn][s], acc[bm][bn], 0, 0, 0);
+  };
+
+  int64_t landed = -1;   // every stage <= landed is known to be in LDS (an epilogue drained vmcnt)
+  auto ready = [&](int64_t t) {
+    const int64_t later = dT - 1 - t;   // stages DMA'd after t (dT - 1: the last one issued)
+    if (t <= landed) {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else if (later >= 2) {
+      gm_wait_barrier<2 * DPS>();
+    } else if (later == 1) {
+      gm_wait_barrier<DPS>();
+    } else {
+      gm_wait_barrier<0>();
+    }
+  };
+  auto epilogue = [&](int64_t i) {
+    int64_t m0, n0;
+    tile_of(i, m0, n0);
+    // lane coordinates made opaque per tile: otherwise the compiler hoists all 64 element
+    // offsets (64-bit) out of the tile loop and spills them
+    int he = h, re = r;
+    asm volatile("" : "+v"(he), "+v"(re));
+    auto crow = [&](int bm, int g) -> int {
+      const int rho = (g & 3) + 8 * (g >> 2) + 4 * he;
+      return wm * 64 + (AK ? 2 * rho + bm : 32 * bm + rho);
+    };
+    auto ccol = [&](int bn) -> int { return wn * 64 + (BK_ ? 2 * re + bn : 32 * bn + re); };
+    const bool full = m0 + MB <= M && n0 + MB <= N;
+    if (full && ldc < (1 << 23)) {
+      float* Ct = C + m0 * ldc + n0;
+      const unsigned l = (unsigned)ldc;
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm) {
+        float cv[2][16];
+        if (beta) {
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) cv[bn][g] = Ct[(unsigned)crow(bm, g) * l + (unsigned)ccol(bn)];
+        }
+        if (bm == 0) gm_vm_wait<0>();
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            float v = alpha * acc[bm][bn][g];
+            if (beta) v += cv[bn][g];
+            Ct[(unsigned)crow(bm, g) * l + (unsigned)ccol(bn)] = v;
+          }
+      }
+    } else {
+      gm_vm_wait<0>();
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) {
+          const int64_t gc = n0 + ccol(bn);
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int64_t gr = m0 + crow(bm, g);
+            if (gr < M && gc < N) {
+              float v = alpha * acc[bm][bn][g];
+              if (beta) v += C[gr * ldc + gc];
+              C[gr * ldc + gc] = v;
+            }
+          }
+        }
+    }
+    landed = dT - 1;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = (floatx16)(0.f);
+  };
+  auto body = [&](int64_t t, const GmFrag& Fc, GmFrag& Fn) {
+    issue();            // stage t + AHEAD (of this tile or the next)
+    mma_row(Fc, 0);
+    if (t + 1 < TT) {
+      ready(t + 1);
+      load(Fn, t + 1);
+    }
+    mma_row(Fc, 1);
+  };
+
+  // nk even (host: K % 32 == 0): every tile starts with its fragments in F0
+  GmFrag F0, F1;
+  for (int q = 0; q < AHEAD; ++q) issue();
+  ready(0);
+  load(F0, 0);
+  int64_t t = 0;
+  for (unsigned i = 0; i < ntl; ++i) {
+    for (int64_t ks = 0; ks < nk; ks += 2, t += 2) {
+      body(t, F0, F1);
+      body(t + 1, F1, F0);
+    }
+    epilogue(i);
+  }
+}
+
 template <bool AK, bool BK_>
 int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, float alpha, int beta, int64_t slices, int64_t cslice, hipStream_t s) {
-  // HEAT_GM_NBUF=3: three-slot ring, three workgroups per CU (A/B)
-  static const int nbuf = getenv("HEAT_GM_NBUF") ? atoi(getenv("HEAT_GM_NBUF")) : 4;
+  // (a three-slot ring with three workgroups per CU measured 2-4 % slower with the 32-bit-offset
+  // epilogue, profiles/gemm_mid_r06.jsonl, and spills with the early C loads: not instantiated)
   const int64_t tiles = ((M + MB - 1) / MB) * ((N + MB - 1) / MB);
   const int64_t nk = (K + MK - 1) / MK, kps = (nk + slices - 1) / slices;
   const int64_t ns = (nk + kps - 1) / kps;
   if (tiles > 0x7fffffffLL || ns > 65535) return HA_UNSUPPORTED;
+  // persistent grid: HEAT_GM_PERSIST=n from n tiles per CU on
+  // (A/B: measured 5 % slower than the one-tile-per-workgroup grid on the K = 256 update,
+  // profiles/gemm_mid_r06.jsonl - off by default)
+  static const int pmin = getenv("HEAT_GM_PERSIST") ? atoi(getenv("HEAT_GM_PERSIST")) : 0;
+  static const int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  if (pmin > 0 && ns == 1 && K % (2 * MK) == 0 && tiles >= (int64_t)pmin * ncu) {
+    const unsigned G = (unsigned)(2 * ((ncu + 3) / 4) * 4);   // two per CU, a multiple of 8
+    hipLaunchKernelGGL((gemm_f32m_p<AK, BK_>), dim3(G), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta);
+    return ha_launch_status();
+  }
   const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
-  if (nbuf == 3)
-    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 3>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
-  else
-    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
   return ha_launch_status();
 }
 

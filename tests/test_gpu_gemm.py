@@ -317,6 +317,28 @@ def test_gemm_f32_small_layouts(m, k, n, layout, kernel):
     assert torch.all(err[:, :8] == 0) and torch.all(err[:, 8 + n:] == 0)
 
 
+@pytest.mark.parametrize("m,k,n", [(6000, 96, 5000), (5996, 64, 4100)])
+@pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
+def test_gemm_f32_mid_persistent(m, k, n, layout):
+    """Enough 128-tiles for the persistent gemm_f32m grid (cross-tile DMA prefetch, >= 4 tiles per
+    CU, K % 32 == 0): every layout, edge tiles in M and N, plain and accumulating."""
+    from heat_amd import ops
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(m + k + n)
+    a = torch.randn(m, k, generator=g).to(dev)
+    b = torch.randn(k, n, generator=g).to(dev)
+    A = a if layout[0] == "n" else a.t().contiguous().t()
+    B = b if layout[1] == "n" else b.t().contiguous().t()
+    ref = a.double() @ b.double()
+    c = ops.gemm_f32_small(A, B, kernel="mid")
+    assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (c.double() - ref).abs().max()
+    base = torch.randn(m, n, generator=g).to(dev)
+    out = base.clone()
+    ops.gemm_f32_small(A, B, out=out, alpha=-1.0, accumulate=True, kernel="mid")
+    assert torch.all((out.double() - (base.double() - ref)).abs() <= _bound(a, b) + 1e-6 * base.abs().double())
+
+
 @pytest.mark.parametrize("m,n,k", [(20000, 3840, 256), (4096, 768, 32), (9000, 300, 256)])
 def test_gemm_f32_mid_update_shape(m, n, k):
     """The Householder trailing-update form C[:, j:] -= V X on the LDS-DMA 128-tile kernel (C a
