@@ -131,25 +131,39 @@ _GEMM_PLAN = os.environ.get("HEAT_GEMM_PLAN", "1") != "0"   # 0: the library for
 
 
 def _native_plan(M: int, N: int, K: int):
-    """(kernel, K slices) for an exact fp32 product that fills the GPU poorly with 256 x 256 tiles,
-    from a cost model fitted to the split-K scan (profiles/gemm_splitk_scan_r05.jsonl): time ~
-    waves x (K per slice + a fixed per-tile overhead) + the slice sum. gemm_f32t: 256-tiles, one
-    workgroup per CU, overhead 256 k; gemm_f32s: 128-tiles, two per CU, overhead 130 k at 0.74x the
-    per-k cost of a 256-tile wave; slice sums (s + 1) M N 4 bytes at ~4 TB/s. Picks 1024^3 ->
-    f32s x8 (1.18x hipBLASLt), 2048^3 -> f32t x4 (1.35x), 3072^3 / 6144^3 -> f32t x3 (1.22x / 1.18x)."""
+    """(kernel, K slices) for an exact fp32 product that fills the GPU poorly with 256 x 256 tiles.
+    Cost model (units of K per output element): time ~ M N (K + s o_k) / (eff_k rate_k) + the
+    split-K slice sum, (s + 1) M N 4 bytes at ~4 TB/s, plus one extra launch (~5 us) when s > 1.
+    gemm_f32t ("f32t"): 256-tiles, one workgroup per CU, o = 256 k (prologue + C epilogue per
+    tile), rate 1; gemm_f32m ("f32s": the 128-tile LDS-DMA kernel behind ops.gemm_f32_small),
+    two workgroups per CU, o = 64, rate 0.92; a workgroup alone on its CU runs at 2 x 0.87 of the
+    shared rate, so a last wave of at most one per CU costs 0.575 of a wave. eff = W / (the
+    waves' time) for W waves of tiles x slices. Measured (profiles/
+    gemm_mid_r06.jsonl, r6i rows) and picked: 1024^3 f32s x4 (0.032 ms, 1.30x hipBLASLt), 2048^3
+    f32s x1 (0.140, 1.07x), 3072^3 f32s x4 (0.506, 1.11x), 4096^3 f32t x1 (0.977, 1.04x), 6144^3
+    f32s x1 (3.55, 1.16x)."""
     from ... import ops
 
     ncu = ops.num_cus(torch.device("cuda", torch.cuda.current_device())) if torch.cuda.is_available() else 256
     t256 = -(-M // 256) * -(-N // 256)
     t128 = -(-M // 128) * -(-N // 128)
+    unit = 2.0 * M * N / 140e12           # seconds per unit of K at ~140 TF
     best = None
     for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
         ks = -(-K // s)
         if s > 1 and (ks < 64 or s * M * N * 4 > (1 << 30)):
             continue
-        sumc = 0.0 if s == 1 else (s + 1) * M * N * 4.37e-6
-        for kern, cost in (("f32t", -(-t256 * s // ncu) * (ks + 256) * 1.0 + sumc),
-                           ("f32s", -(-t128 * s // (2 * ncu)) * (ks + 130) * 0.74 + sumc)):
+        extra = 0.0 if s == 1 else (s + 1) * M * N * 4 / 4e12 / unit + 5e-6 / unit
+        for kern, tiles, slots, o, rate in (("f32t", t256, ncu, 256, 1.0), ("f32s", t128, 2 * ncu, 64, 0.92)):
+            w = tiles * s / slots
+            full, frac = int(w), w - int(w)
+            if kern == "f32s" and 0 < frac <= 0.5:
+                # a last wave of at most one workgroup per CU runs unshared: 1 / (2 x 0.87) of a wave
+                waves = full + 0.575
+            else:
+                waves = full + (1 if frac > 0 else 0)
+            eff = w / waves
+            cost = (K + s * o) / (eff * rate) + extra
             if best is None or cost < best[0]:
                 best = (cost, kern, s)
     return best[1], best[2]

@@ -1627,7 +1627,7 @@ def householder_factor(local: torch.Tensor, g0: int = 0, m_total: Optional[int] 
     block; the outer block is then applied to the trailing matrix as ONE block reflector
     Q_b = I - V T V^T with T = (striu(V^T V) + diag(1/tau))^-1 (``tri_inv_upper``), W = V^T C
     from the fp64 matrix-core kernel (``csrc/linalg64.hip: vtc64``, exact products, split-K in
-    fixed order) and C -= V (T^T W) as one fp32 GEMM (hipBLASLt: a plain small-K update, see
+    fixed order) and C -= V (T^T W) as one fp32 GEMM (``csrc/gemm_mid.hip: gemm_f32m``, see
     ``_HH_UPDATE``). Each 32-column panel is factored in a compact m x 32 copy and its V^T V comes
     from the column sums of the steps (no separate pass)."""
     m_r, n = local.shape
@@ -1742,16 +1742,16 @@ def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, tra
     return C
 
 
-# the rank-nc update C -= V X of the Householder QR: blas (hipBLASLt fp32) | f32 (gemm_f32t) | h3
-# (fp16x3 MFMA). The update is a plain fp32 GEMM with a small K (256 outer / 32 inner) and a tall
-# C that is read and written once; measured at 1.25e6 rows (tools/microbench/hh_parts.py,
-# profiles/householder_r04.md): K = 256, N = 3840: hipBLASLt 19.8 ms vs gemm_f32t 32.2 ms;
-# K = 32, N = 224 (strided C): 0.60 vs 1.25 ms - gemm_f32t's 256 x 256 tile pays its prologue and
-# C epilogue per 16 k-stages there. The blas form runs at float32 matmul precision "highest" whatever
-# the caller set: under "high" hipBLASLt drops to a reduced-precision fp32 path (measured ||Q^T Q - I||
-# 1.5e-5 instead of 1.2e-7, tools/microbench/hh_prec.py), and the Householder path is the backward-
-# stable one.
-_HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "blas")
+# the rank-nc update C -= V X of the Householder QR: small (default: the LDS-DMA 128-tile gemm_f32m,
+# csrc/gemm_mid.hip) | blas (hipBLASLt fp32) | f32 (the 256-tile gemm_f32t) | h3 (fp16x3 MFMA). The
+# update is a plain fp32 GEMM with a small K (256 outer / 32 inner) and a tall C read and written
+# once. Measured at 1.25e6 rows (tools/microbench/gemm_mid.py, profiles/gemm_mid_r06.jsonl):
+# K = 256, N = 3840: gemm_f32m 23.05 ms, hipBLASLt 19.75, gemm_f32t 27.6; the whole 1.25e6 x 4096
+# factorisation + Q 1.354 s native vs 1.305 s with the library update (tools/microbench/
+# hh_update_ab.py) - 4 % for a QR with no library GEMM in it. The blas form runs at float32 matmul
+# precision "highest" whatever the caller set: under "high" hipBLASLt drops to a reduced-precision
+# fp32 path (measured ||Q^T Q - I|| 1.5e-5 instead of 1.2e-7, tools/microbench/hh_prec.py).
+_HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "small")
 
 
 _PRECISION_LOCK = threading.RLock()
@@ -1784,7 +1784,7 @@ def _exact_addmm_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: floa
 def _hh_block_update(C: torch.Tensor, V: torch.Tensor, Tm: torch.Tensor, transpose: bool, native: bool, st,
                      red) -> None:
     """C -= V op(T) (V^T C) in place: W = V^T C with fp64 accumulation (summed over the ranks by
-    ``red``), X = op(T) W in fp64 (``gemm64``), then the rank-nc update (fp32: hipBLASLt, see
+    ``red``), X = op(T) W in fp64 (``gemm64``), then the rank-nc update (fp32: ``gemm_f32m``, see
     ``_HH_UPDATE``; fp64: ``gemm64``)."""
     if C.shape[1] == 0 or V.shape[1] == 0:
         return

@@ -226,7 +226,7 @@ class PartialH5DataLoaderIter:
         self.batch_size = dl.batch_size
         self.drop_last = dl.drop_last
         self._collate = dl.collate_fn
-        n = ds.lcl_full_sz
+        n = self._rows = ds.lcl_full_sz
         self.length = n // self.batch_size if self.drop_last else -(-n // self.batch_size)
         self._num_yielded = 0
         self._carry = []
@@ -282,6 +282,15 @@ class PartialH5DataLoaderIter:
             # every batch of the epoch was yielded. The loader is finished only once its end marker
             # was taken off the queue: with drop_last the leftover rows can sit in windows nobody
             # fetched, and a loader blocked on them must be cancelled by the next epoch, not joined
+            if self._queue is not None and self._num_yielded * self.batch_size >= self._rows:
+                # every row was yielded (no drop_last remainder), so every window was taken: the
+                # loader's next item is its end marker - take it (the epoch is then finished and
+                # the next one joins the loader instead of racing its pre-read of window 0)
+                item = self._queue.get()
+                if isinstance(item, tuple) and item[0] == "error":
+                    raise item[1]
+                if item is _END:
+                    self._queue = None
             if self._queue is None:
                 self.dataset._epoch_done = True
             raise StopIteration
