@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 ( while sleep 50; do echo "tick $(date +%T)"; done ) &
 HB=$!
 rc=0
-for b in kmeans kmeans_reference distance_matrix knn statistical_moments lasso linalg linalg_high; do
+for b in ${SUITE_LIST:-kmeans kmeans_reference distance_matrix knn statistical_moments lasso linalg linalg_high}; do
   echo "== $b $(date +%T)"
   timeout -k 10 900 python -u -m benchmarks.run_all --gpus 1 --only $b --out "$OUT/suite.jsonl" --timeout 880 > "$OUT/$b.log" 2>&1 || { rc=$?; echo "$b failed rc=$rc"; break; }
 done
