@@ -34,6 +34,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 namespace {
 
 constexpr int MB = 128;       // tile rows / columns
@@ -74,76 +76,85 @@ __device__ __forceinline__ void gm_vm_wait() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// One operand's staging for this lane. KC (k-contiguous, [rows][K] with leading dimension ld):
-// piece q = k-chunk q >> 1 (4 k), rows 64 (q & 1) + lane; image [4 chunks][128 rows][4] - piece q
-// at q KB. Else row-contiguous ([K][rows]): piece q = k-rows 2 q + (lane >> 5), 4 rows
-// 4 (lane & 31) .. + 3; image [16 k][128 rows] at 512 B per k-row - piece q at q KB too.
+// One operand's staging for this lane, TR tile rows (128 or 256). KC (k-contiguous, [rows][K]
+// with leading dimension ld): G = TR / 64 row groups; piece q = k-chunk q / G (4 k), rows
+// 64 (q % G) + lane; image [4 chunks][TR rows][4] - piece q at q KB. Else row-contiguous ([K][rows]):
+// RP = TR / 4 lanes per k-row, piece q = k-rows KPP q + lane / RP (KPP = 64 / RP), 4 rows
+// 4 (lane % RP) .. + 3; image [16 k][TR rows] at 4 TR bytes per k-row - piece q at q KB too.
 // Out-of-range rows are clamped (their results are masked at the store).
-template <bool KC>
+template <bool KC, int TR>
 struct GmSrc {
-  const float* rp[2];  // KC: this lane's row of each 64-row group
-  const float* cp;     // row-contiguous: this lane's 4-row group at k = lane >> 5
+  static constexpr int G = TR / 64, RP = TR / 4, KPP = 64 / RP;
+  const float* rp[G];  // KC: this lane's row of each 64-row group
+  const float* cp;     // row-contiguous: this lane's 4-row group at k = lane / RP
   int64_t ld;
   __device__ __forceinline__ void init(const float* P, int64_t ld_, int64_t rows, int64_t r0, int lane) {
     ld = ld_;
     if (KC) {
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
+      for (int g = 0; g < G; ++g) {
         const int64_t row = r0 + 64 * g + lane;
         rp[g] = P + (row < rows ? row : rows - 1) * ld;
       }
     } else {
-      int64_t c = r0 + 4 * (lane & 31);
+      int64_t c = r0 + 4 * (lane % RP);
       c = c + 4 <= rows ? c : rows - 4;
-      cp = P + (int64_t)(lane >> 5) * ld + c;
+      cp = P + (int64_t)(lane / RP) * ld + c;
     }
   }
   // source of piece q of the stage at k0 (whole stage in range)
   __device__ __forceinline__ const float* src(int64_t k0, int q) const {
-    return KC ? rp[q & 1] + k0 + 4 * (q >> 1) : cp + (k0 + 2 * q) * ld;
+    return KC ? rp[q % G] + k0 + 4 * (q / G) : cp + (k0 + KPP * q) * ld;
   }
   // the same with the k index clamped into [0, K) (the tail stage; the clamped entries are zeroed
   // after they land). KC requires K % 4 == 0.
   __device__ __forceinline__ const float* src_clamped(int64_t k0, int q, int64_t K, int lane) const {
     if (KC) {
-      const int64_t k = k0 + 4 * (q >> 1) + 4 <= K ? k0 + 4 * (q >> 1) : K - 4;
-      return rp[q & 1] + k;
+      const int64_t k = k0 + 4 * (q / G) + 4 <= K ? k0 + 4 * (q / G) : K - 4;
+      return rp[q % G] + k;
     }
-    const int64_t k = k0 + 2 * q + (lane >> 5);
-    return cp + ((k < K ? k : K - 1) - (lane >> 5)) * ld;
+    const int64_t k = k0 + KPP * q + lane / RP;
+    return cp + ((k < K ? k : K - 1) - lane / RP) * ld;
   }
   __device__ __forceinline__ bool beyond(int64_t k0, int q, int64_t K, int lane) const {
-    return KC ? k0 + 4 * (q >> 1) >= K : k0 + 2 * q + (lane >> 5) >= K;
+    return KC ? k0 + 4 * (q / G) >= K : k0 + KPP * q + lane / RP >= K;
   }
 };
 
-// Fragments of one stage for a wave: a[b][s], bb[b][s] = block b's operand at k = 8 h + s.
+// Fragments of one stage for a wave: a[b][s], b[b][s] = block b's operand at k = 8 h + s.
+template <int WMB>
 struct GmFrag {
-  float a[2][8], b[2][8];
+  float a[WMB][8], b[2][8];
 };
 
 // AK: A k-major ([K][M], m contiguous) - else row-major ([M][K], k contiguous).
 // BK_: B k-major ([K][N], n contiguous) - else n-major ([N][K], k contiguous).
-// NBUF: ring slots (4: 64 KB, two workgroups per CU).
-template <bool AK, bool BK_, int NBUF>
-__global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
-                                                                      const float* __restrict__ B,
-                                                                      float* __restrict__ C, int64_t M, int64_t N,
-                                                                      int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                                      float alpha, int beta, int64_t kps,
-                                                                      int64_t cslice) {
-  constexpr int AHEAD = NBUF - 1;   // stages in flight
-  constexpr int DPS = 4;            // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * MSTAGE];
+// WMB: 32 x 32 blocks per wave along M - 2: 128 x 128 tiles (waves of 64 x 64, 64 KB of LDS for
+// NBUF = 4, the default); 4: 256 x 128 tiles (waves of 128 x 64: 0.75 LDS floats per MFMA instead
+// of 1, 43 instead of 32 flop per staged byte; NBUF = 3, 72 KB; measured slower - A/B only). Two
+// workgroups per CU either way.
+template <bool AK, bool BK_, int WMB, int NBUF>
+__global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A, const float* __restrict__ B,
+                                                    float* __restrict__ C, int64_t M, int64_t N, int64_t K,
+                                                    int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
+                                                    int64_t kps, int64_t cslice) {
+  constexpr int TM = 64 * WMB;          // tile rows
+  constexpr int AOP = TM * MK * 4;      // bytes of A per stage
+  constexpr int STG = AOP + MOP;        // bytes per stage
+  constexpr int PAW = TM / 64;          // A pieces per wave per stage (TM / 16 pieces / 4 waves)
+  constexpr int AHEAD = NBUF - 1;       // stages in flight
+  constexpr int DPS = PAW + 2;          // DMA instructions per wave per stage
+  static_assert(NBUF * STG <= 80 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r = lane & 31;
-  const unsigned tn = (unsigned)((N + MB - 1) / MB), tm = (unsigned)((M + MB - 1) / MB);
+  const unsigned tn = (unsigned)((N + MB - 1) / MB), tm = (unsigned)((M + TM - 1) / TM);
   const unsigned bid = gm_xcd_remap(blockIdx.x, tm * tn);
   constexpr unsigned GM = 8;
   const unsigned grp = bid / (GM * tn), gfirst = grp * GM;
   const unsigned gsz = tm - gfirst < GM ? tm - gfirst : GM;
-  const int64_t m0 = (int64_t)(gfirst + (bid % (GM * tn)) % gsz) * MB, n0 = (int64_t)((bid % (GM * tn)) / gsz) * MB;
+  const int64_t m0 = (int64_t)(gfirst + (bid % (GM * tn)) % gsz) * TM, n0 = (int64_t)((bid % (GM * tn)) / gsz) * MB;
   // split-K: slice blockIdx.y = k in [y kps MK, min((y + 1) kps MK, K)) into C + y cslice
   {
     const int64_t k0 = (int64_t)blockIdx.y * kps * MK;
@@ -152,85 +163,110 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     K = K - k0 < kps * MK ? K - k0 : kps * MK;
     C += (int64_t)blockIdx.y * cslice;
   }
-  GmSrc<!AK> sa;
-  GmSrc<!BK_> sb;
+  GmSrc<!AK, TM> sa;
+  GmSrc<!BK_, MB> sb;
   sa.init(A, lda, M, m0, lane);
   sb.init(B, ldb, N, n0, lane);
   const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
 
   auto stage = [&](int64_t t, bool full) {
-    const unsigned dst = sbase + (unsigned)((t % NBUF) * MSTAGE);
+    const unsigned dst = sbase + (unsigned)((t % NBUF) * STG);
     const int64_t k0 = t * MK;
+#pragma unroll
+    for (int i = 0; i < PAW; ++i) {
+      const int q = PAW * wave + i;
+      gm_dma16(full ? sa.src(k0, q) : sa.src_clamped(k0, q, K, lane), dst + q * 1024);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = 2 * wave + i;
-      gm_dma16(full ? sa.src(k0, q) : sa.src_clamped(k0, q, K, lane), dst + q * 1024);
-      gm_dma16(full ? sb.src(k0, q) : sb.src_clamped(k0, q, K, lane), dst + MOP + q * 1024);
+      gm_dma16(full ? sb.src(k0, q) : sb.src_clamped(k0, q, K, lane), dst + AOP + q * 1024);
     }
   };
   auto zero_tail = [&](int64_t t) {
-    unsigned char* dst = smem + (t % NBUF) * MSTAGE;
+    unsigned char* dst = smem + (t % NBUF) * STG;
     const int64_t k0 = t * MK;
+#pragma unroll
+    for (int i = 0; i < PAW; ++i) {
+      const int q = PAW * wave + i;
+      if (sa.beyond(k0, q, K, lane)) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = 2 * wave + i;
-      if (sa.beyond(k0, q, K, lane)) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
-      if (sb.beyond(k0, q, K, lane)) *reinterpret_cast<floatx4*>(dst + MOP + q * 1024 + lane * 16) = (floatx4)(0.f);
+      if (sb.beyond(k0, q, K, lane)) *reinterpret_cast<floatx4*>(dst + AOP + q * 1024 + lane * 16) = (floatx4)(0.f);
     }
   };
 
-  // fragment reads. k-contiguous operand, block b: row 32 b + r of the wave's 64, k-chunks 2 h and
-  // 2 h + 1 (two ds_read_b128). Row-contiguous: rows 2 r, 2 r + 1 of the wave's 64 (blocks 0, 1)
-  // at k-row 8 h + s (one ds_read_b64 per s).
-  auto load = [&](GmFrag& F, int64_t t) {
-    const unsigned char* base = smem + (t % NBUF) * MSTAGE;
-    auto opnd = [&](const unsigned char* b, int w0, bool kc, float (&o)[2][8]) __attribute__((always_inline)) {
-      if (kc) {
+  // fragment reads, NB blocks of an operand per wave over TR tile rows. k-contiguous operand,
+  // block b: row 32 b + r of the wave's rows, k-chunks 2 h and 2 h + 1 (two ds_read_b128).
+  // Row-contiguous: rows NB r .. NB r + NB - 1 of the wave's rows (blocks 0 .. NB - 1) at k-row
+  // 8 h + s (one ds_read_b64 / b128 per s; conflict-free: a lane group spans 64 banks).
+  typedef float floatx2 __attribute__((ext_vector_type(2)));
+  auto opnd = [&](const unsigned char* b, int w0, auto kc_tag, auto nb_tag, auto tr_tag, float (*o)[8])
+      __attribute__((always_inline)) {
+    constexpr bool kc = decltype(kc_tag)::value;
+    constexpr int NB = decltype(nb_tag)::value, TR = decltype(tr_tag)::value;
+    if constexpr (kc) {
 #pragma unroll
-        for (int bl = 0; bl < 2; ++bl) {
-          const int row = w0 + 32 * bl + r;
-          const floatx4 x0 = *reinterpret_cast<const floatx4*>(b + (2 * h) * 2048 + row * 16);
-          const floatx4 x1 = *reinterpret_cast<const floatx4*>(b + (2 * h + 1) * 2048 + row * 16);
+      for (int bl = 0; bl < NB; ++bl) {
+        const int row = w0 + 32 * bl + r;
+        const floatx4 x0 = *reinterpret_cast<const floatx4*>(b + (2 * h) * (TR * 16) + row * 16);
+        const floatx4 x1 = *reinterpret_cast<const floatx4*>(b + (2 * h + 1) * (TR * 16) + row * 16);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            o[bl][s] = x0[s];
-            o[bl][4 + s] = x1[s];
-          }
-        }
-      } else {
-        typedef float floatx2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const floatx2 v = *reinterpret_cast<const floatx2*>(b + (8 * h + s) * 512 + (w0 + 2 * r) * 4);
-          o[0][s] = v[0];
-          o[1][s] = v[1];
+        for (int s = 0; s < 4; ++s) {
+          o[bl][s] = x0[s];
+          o[bl][4 + s] = x1[s];
         }
       }
-    };
-    opnd(base, wm * 64, !AK, F.a);
-    opnd(base + MOP, wn * 64, !BK_, F.b);
+    } else if constexpr (NB == 2) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const floatx2 v = *reinterpret_cast<const floatx2*>(b + (8 * h + s) * (TR * 4) + (w0 + 2 * r) * 4);
+        o[0][s] = v[0];
+        o[1][s] = v[1];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(b + (8 * h + s) * (TR * 4) + (w0 + 4 * r) * 4);
+#pragma unroll
+        for (int bl = 0; bl < 4; ++bl) o[bl][s] = v[bl];
+      }
+    }
+  };
+  auto load = [&](GmFrag<WMB>& F, int64_t t) {
+    const unsigned char* base = smem + (t % NBUF) * STG;
+    opnd(base, wm * 32 * WMB, std::integral_constant<bool, !AK>(), std::integral_constant<int, WMB>(),
+         std::integral_constant<int, TM>(), F.a);
+    opnd(base + AOP, wn * 64, std::integral_constant<bool, !BK_>(), std::integral_constant<int, 2>(),
+         std::integral_constant<int, MB>(), F.b);
   };
 
   // accumulator (block bm, bn) element g <-> tile row / column (see the header)
   auto crow = [&](int bm, int g) -> int {
     const int rho = (g & 3) + 8 * (g >> 2) + 4 * h;
-    return wm * 64 + (AK ? 2 * rho + bm : 32 * bm + rho);
+    return wm * 32 * WMB + (AK ? WMB * rho + bm : 32 * bm + rho);
   };
   auto ccol = [&](int bn) -> int { return wn * 64 + (BK_ ? 2 * r + bn : 32 * bn + r); };
 
-  floatx16 acc[2][2];
-  const bool full = m0 + MB <= M && n0 + MB <= N;
+  floatx16 acc[WMB][2];
+  const bool full = m0 + TM <= M && n0 + MB <= N;
 #pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
+  for (int bm = 0; bm < WMB; ++bm)
 #pragma unroll
     for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = (floatx16)(0.f);
 
-  auto mma_row = [&](const GmFrag& F, int bm) {
+  auto mma_row = [&](const GmFrag<WMB>& F, int bm) {
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn)
         acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[bm][s], F.b[bn][s], acc[bm][bn], 0, 0, 0);
+  };
+  auto mma_half = [&](const GmFrag<WMB>& F, int part) {
+#pragma unroll
+    for (int bm = part * WMB / 2; bm < (part + 1) * WMB / 2; ++bm) mma_row(F, bm);
   };
 
   const int64_t nk = K > 0 ? (K + MK - 1) / MK : 0;
@@ -246,40 +282,40 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     else if (later == 1) gm_wait_barrier<DPS>();
     else gm_wait_barrier<0>();
   };
-  // steady state: stage t + AHEAD issued (whole, in range), MFMAs of block row 0 around it, the
-  // counted wait for stage t + 1 + barrier, then stage t + 1's fragment reads between block row
-  // 1's MFMAs
-  auto step_full = [&](int64_t t, const GmFrag& Fc, GmFrag& Fn) {
+  // steady state: stage t + AHEAD issued (whole, in range), MFMAs of the first half of the block
+  // rows around it, the counted wait for stage t + 1 + barrier, then stage t + 1's fragment reads
+  // between the second half's MFMAs
+  auto step_full = [&](int64_t t, const GmFrag<WMB>& Fc, GmFrag<WMB>& Fn) {
     stage(t + AHEAD, true);
-    mma_row(Fc, 0);
+    mma_half(Fc, 0);
 #pragma unroll
     for (int q = 0; q < DPS; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (the asm DMA)
+      __builtin_amdgcn_sched_group_barrier(0x008, 8 * WMB / DPS, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // VMEM read (the asm DMA)
     }
     __builtin_amdgcn_sched_barrier(0);
     gm_wait_barrier<(AHEAD - 1) * DPS>();
     load(Fn, t + 1);
-    mma_row(Fc, 1);
+    mma_half(Fc, 1);
     __builtin_amdgcn_sched_barrier(0);
   };
-  // whole tiles with 128 ldc < 2^31: a uniform 64-bit tile base + 32-bit lane offsets in the
+  // whole tiles with 256 ldc < 2^31: a uniform 64-bit tile base + 32-bit lane offsets in the
   // epilogue (the row terms dr ldc are scalar products), no bounds tests - the 64-bit per-element
   // form was ~1000 VALU per tile-wave against 512 MFMAs on the K = 256 update. (Loading C at the
-  // start of the last k-stage instead measured 18 % slower on that update: 214 VGPRs;
-  // profiles/gemm_mid_r06.jsonl.)
+  // start of the last k-stage instead measured 18 % slower on that update: 214 VGPRs; a persistent
+  // grid with cross-tile DMA prefetch measured 5 % slower; profiles/gemm_mid_r06.jsonl.)
   const bool fast = full && ldc < (1 << 23);
-  auto step = [&](int64_t t, const GmFrag& Fc, GmFrag& Fn) {
+  auto step = [&](int64_t t, const GmFrag<WMB>& Fc, GmFrag<WMB>& Fn) {
     if (t + AHEAD < nk) stage(t + AHEAD, !(tail && t + AHEAD == nk - 1));
-    mma_row(Fc, 0);
+    mma_half(Fc, 0);
     if (t + 1 < nk) {
       ready(t + 1);
       load(Fn, t + 1);
     }
-    mma_row(Fc, 1);
+    mma_half(Fc, 1);
   };
 
-  GmFrag F0, F1;
+  GmFrag<WMB> F0, F1;
   for (int64_t t = 0; t < AHEAD && t < nk; ++t) stage(t, !(tail && t == nk - 1));
   if (nk > 0) {
     ready(0);
@@ -303,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     const int l = (int)ldc;
     // one accumulator row's C values (32 loads in flight) before its stores
 #pragma unroll
-    for (int bm = 0; bm < 2; ++bm) {
+    for (int bm = 0; bm < WMB; ++bm) {
       float cv[2][16];
       if (beta) {
 #pragma unroll
@@ -323,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     return;
   }
 #pragma unroll
-  for (int bm = 0; bm < 2; ++bm) {
+  for (int bm = 0; bm < WMB; ++bm) {
     float cv[2][16];
     if (beta) {
 #pragma unroll
@@ -350,233 +386,19 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
   }
 }
 
-// Persistent form (one slice, K % 32 == 0, at least two workgroups' worth of tiles per CU): a
-// grid of two workgroups per CU, each walking its tiles as ONE stream of k-stages, so the DMA of
-// the next tile's first stages is in flight during the current tile's last MFMAs and its epilogue.
-// With one launch-wide grid of equal tiles the two workgroups of a CU start and finish together:
-// their prologue (stage-0 latency) and epilogue (C traffic) phases coincide and leave the SIMDs
-// idle, which 16-stage tiles (the Householder update, K = 256) cannot amortise.
-// Tile order: XCD x = blockIdx % 8 owns the contiguous logical tiles [x Tx, (x + 1) Tx) (grouped
-// GM-row-panel order inside), workgroup j of that XCD takes every Gx-th of them.
-// Wait counting across the epilogue: the epilogue drains vmcnt (after its first C loads), so every
-// stage DMA'd before it has landed - those stages' readies skip the vmcnt and only barrier; the
-// stages DMA'd after it are counted as usual (the epilogue's stores are older than them, and two
-// stages later they are long acknowledged).
-template <bool AK, bool BK_>
-__global__ __launch_bounds__(256, 2) void gemm_f32m_p(const float* __restrict__ A, const float* __restrict__ B,
-                                                       float* __restrict__ C, int64_t M, int64_t N, int64_t K,
-                                                       int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta) {
-  constexpr int NBUF = 4, AHEAD = 3, DPS = 4;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * MSTAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5, r = lane & 31;
-  const unsigned tn = (unsigned)((N + MB - 1) / MB), tm = (unsigned)((M + MB - 1) / MB);
-  const unsigned tiles = tm * tn;
-  const unsigned x = blockIdx.x % 8, j = blockIdx.x / 8, Gx = gridDim.x / 8;
-  const unsigned Tx = (tiles + 7) / 8, tbeg = x * Tx;
-  const unsigned tend = tbeg + Tx < tiles ? tbeg + Tx : tiles;
-  const unsigned ntl = tbeg + j < tend ? (tend - tbeg - j + Gx - 1) / Gx : 0;
-  const int64_t nk = K / MK;
-  const int64_t TT = (int64_t)ntl * nk;
-  if (TT == 0) return;
-  constexpr unsigned GM = 8;
-  auto tile_of = [&](int64_t i, int64_t& m0, int64_t& n0) {
-    const unsigned L = tbeg + j + (unsigned)i * Gx;
-    const unsigned grp = L / (GM * tn), gfirst = grp * GM;
-    const unsigned gsz = tm - gfirst < GM ? tm - gfirst : GM;
-    m0 = (int64_t)(gfirst + (L % (GM * tn)) % gsz) * MB;
-    n0 = (int64_t)((L % (GM * tn)) / gsz) * MB;
-  };
-  const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
-  GmSrc<!AK> sa;
-  GmSrc<!BK_> sb;
-  int64_t dT = 0;   // next stage to DMA
-  auto issue = [&]() {
-    if (dT < TT) {
-      const int64_t ks = dT % nk;
-      if (ks == 0) {
-        int64_t dm0, dn0;
-        tile_of(dT / nk, dm0, dn0);
-        sa.init(A, lda, M, dm0, lane);
-        sb.init(B, ldb, N, dn0, lane);
-      }
-      const unsigned dst = sbase + (unsigned)((dT % NBUF) * MSTAGE);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int q = 2 * wave + i;
-        gm_dma16(sa.src(ks * MK, q), dst + q * 1024);
-        gm_dma16(sb.src(ks * MK, q), dst + MOP + q * 1024);
-      }
-    }
-    ++dT;
-  };
-  auto load = [&](GmFrag& F, int64_t t) {
-    const unsigned char* base = smem + (t % NBUF) * MSTAGE;
-    auto opnd = [&](const unsigned char* b, int w0, bool kc, float (&o)[2][8]) __attribute__((always_inline)) {
-      if (kc) {
-#pragma unroll
-        for (int bl = 0; bl < 2; ++bl) {
-          const int row = w0 + 32 * bl + r;
-          const floatx4 x0 = *reinterpret_cast<const floatx4*>(b + (2 * h) * 2048 + row * 16);
-          const floatx4 x1 = *reinterpret_cast<const floatx4*>(b + (2 * h + 1) * 2048 + row * 16);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            o[bl][s] = x0[s];
-            o[bl][4 + s] = x1[s];
-          }
-        }
-      } else {
-        typedef float floatx2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const floatx2 v = *reinterpret_cast<const floatx2*>(b + (8 * h + s) * 512 + (w0 + 2 * r) * 4);
-          o[0][s] = v[0];
-          o[1][s] = v[1];
-        }
-      }
-    };
-    opnd(base, wm * 64, !AK, F.a);
-    opnd(base + MOP, wn * 64, !BK_, F.b);
-  };
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-    for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = (floatx16)(0.f);
-  auto mma_row = [&](const GmFrag& F, int bm) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int bn = 0; bn < 2; ++bn)
-        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[bm][s], F.b[bn][s], acc[bm][bn], 0, 0, 0);
-  };
-
-  int64_t landed = -1;   // every stage <= landed is known to be in LDS (an epilogue drained vmcnt)
-  auto ready = [&](int64_t t) {
-    const int64_t later = dT - 1 - t;   // stages DMA'd after t (dT - 1: the last one issued)
-    if (t <= landed) {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    } else if (later >= 2) {
-      gm_wait_barrier<2 * DPS>();
-    } else if (later == 1) {
-      gm_wait_barrier<DPS>();
-    } else {
-      gm_wait_barrier<0>();
-    }
-  };
-  auto epilogue = [&](int64_t i) {
-    int64_t m0, n0;
-    tile_of(i, m0, n0);
-    // lane coordinates made opaque per tile: otherwise the compiler hoists all 64 element
-    // offsets (64-bit) out of the tile loop and spills them
-    int he = h, re = r;
-    asm volatile("" : "+v"(he), "+v"(re));
-    auto crow = [&](int bm, int g) -> int {
-      const int rho = (g & 3) + 8 * (g >> 2) + 4 * he;
-      return wm * 64 + (AK ? 2 * rho + bm : 32 * bm + rho);
-    };
-    auto ccol = [&](int bn) -> int { return wn * 64 + (BK_ ? 2 * re + bn : 32 * bn + re); };
-    const bool full = m0 + MB <= M && n0 + MB <= N;
-    if (full && ldc < (1 << 23)) {
-      float* Ct = C + m0 * ldc + n0;
-      const unsigned l = (unsigned)ldc;
-#pragma unroll
-      for (int bm = 0; bm < 2; ++bm) {
-        float cv[2][16];
-        if (beta) {
-#pragma unroll
-          for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-            for (int g = 0; g < 16; ++g) cv[bn][g] = Ct[(unsigned)crow(bm, g) * l + (unsigned)ccol(bn)];
-        }
-        if (bm == 0) gm_vm_wait<0>();
-#pragma unroll
-        for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            float v = alpha * acc[bm][bn][g];
-            if (beta) v += cv[bn][g];
-            Ct[(unsigned)crow(bm, g) * l + (unsigned)ccol(bn)] = v;
-          }
-      }
-    } else {
-      gm_vm_wait<0>();
-#pragma unroll
-      for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-        for (int bn = 0; bn < 2; ++bn) {
-          const int64_t gc = n0 + ccol(bn);
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int64_t gr = m0 + crow(bm, g);
-            if (gr < M && gc < N) {
-              float v = alpha * acc[bm][bn][g];
-              if (beta) v += C[gr * ldc + gc];
-              C[gr * ldc + gc] = v;
-            }
-          }
-        }
-    }
-    landed = dT - 1;
-#pragma unroll
-    for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-      for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = (floatx16)(0.f);
-  };
-  auto body = [&](int64_t t, const GmFrag& Fc, GmFrag& Fn) {
-    issue();            // stage t + AHEAD (of this tile or the next)
-    mma_row(Fc, 0);
-    if (t + 1 < TT) {
-      ready(t + 1);
-      load(Fn, t + 1);
-    }
-    mma_row(Fc, 1);
-  };
-
-  // nk even (host: K % 32 == 0): every tile starts with its fragments in F0
-  GmFrag F0, F1;
-  for (int q = 0; q < AHEAD; ++q) issue();
-  ready(0);
-  load(F0, 0);
-  int64_t t = 0;
-  for (unsigned i = 0; i < ntl; ++i) {
-    for (int64_t ks = 0; ks < nk; ks += 2, t += 2) {
-      body(t, F0, F1);
-      body(t + 1, F1, F0);
-    }
-    epilogue(i);
-  }
-}
-
 template <bool AK, bool BK_>
 int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, float alpha, int beta, int64_t slices, int64_t cslice, hipStream_t s) {
-  // (a three-slot ring with three workgroups per CU measured 2-4 % slower with the 32-bit-offset
-  // epilogue, profiles/gemm_mid_r06.jsonl, and spills with the early C loads: not instantiated)
-  const int64_t tiles = ((M + MB - 1) / MB) * ((N + MB - 1) / MB);
+                int64_t ldc, float alpha, int beta, int64_t slices, int64_t cslice, int wide, hipStream_t s) {
+  const int64_t tm = wide ? 256 : MB;
+  const int64_t tiles = ((M + tm - 1) / tm) * ((N + MB - 1) / MB);
   const int64_t nk = (K + MK - 1) / MK, kps = (nk + slices - 1) / slices;
   const int64_t ns = (nk + kps - 1) / kps;
   if (tiles > 0x7fffffffLL || ns > 65535) return HA_UNSUPPORTED;
-  // persistent grid: HEAT_GM_PERSIST=n from n tiles per CU on
-  // (A/B: measured 5 % slower than the one-tile-per-workgroup grid on the K = 256 update,
-  // profiles/gemm_mid_r06.jsonl - off by default)
-  static const int pmin = getenv("HEAT_GM_PERSIST") ? atoi(getenv("HEAT_GM_PERSIST")) : 0;
-  static const int ncu = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return v > 0 ? v : 256;
-  }();
-  if (pmin > 0 && ns == 1 && K % (2 * MK) == 0 && tiles >= (int64_t)pmin * ncu) {
-    const unsigned G = (unsigned)(2 * ((ncu + 3) / 4) * 4);   // two per CU, a multiple of 8
-    hipLaunchKernelGGL((gemm_f32m_p<AK, BK_>), dim3(G), dim3(256), 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta);
-    return ha_launch_status();
-  }
   const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
-  hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  if (wide)
+    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4, 3>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
+  else
+    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 2, 4>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
   return ha_launch_status();
 }
 
@@ -594,19 +416,24 @@ HA_EXPORT int64_t ha_gemm_f32m_slices(int64_t K, int64_t slices) {
 // C[M, N] (row-major, ldc) = alpha A B (+ C if beta), exact fp32 products and accumulation.
 // a_kmajor: A element (m, k) at A[k lda + m] (else A[m lda + k]); b_kmajor: B element (k, n) at
 // B[k ldb + n] (else B[n ldb + k]). slices > 1: split-K over 16-k stages, slice y -> C + y cslice
-// (beta must be 0; the caller sums the partials). Requirements (else HA_UNSUPPORTED): 16-byte
+// (beta must be 0; the caller sums the partials). tile: 0 auto, 1 128 x 128, 2 256 x 128. Requirements (else HA_UNSUPPORTED): 16-byte
 // aligned A and B, lda and ldb multiples of 4, the contiguous extent of each operand (K for a
 // k-contiguous one, M / N for the other) a multiple of 4, M, N, K >= 4.
 HA_EXPORT int ha_gemm_f32m(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                            int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, float alpha, int beta, int64_t slices,
-                           int64_t cslice, void* stream) {
+                           int64_t cslice, int tile, void* stream) {
   if (M < 0 || N < 0 || K < 0 || !A || !B || !C || slices < 1) return HA_BAD_ARG;
   if (slices > 1 && beta) return HA_BAD_ARG;
   if (M == 0 || N == 0) return HA_OK;
   if (K < 4 || M < 4 || N < 4 || lda % 4 || ldb % 4 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return HA_UNSUPPORTED;
   if ((a_kmajor ? M : K) % 4 || (b_kmajor ? N : K) % 4) return HA_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-#define HA_F32M(AK, BK) return f32m_launch<AK, BK>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, slices, cslice, s)
+  // tile 1: 128 x 128, 2: 256 x 128 (wide), 0: 128 x 128 unless HEAT_GM_WIDE=1. The wide tile
+  // measured slower on every shape (71 vs 84 % MFMA-busy at 6144^3, update 25.2 vs 23.3 ms;
+  // profiles/gemm_mid_r06.jsonl, r6j rows): an A/B form only
+  static const int wide_env = getenv("HEAT_GM_WIDE") ? atoi(getenv("HEAT_GM_WIDE")) : 0;
+  const int wide = tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
+#define HA_F32M(AK, BK) return f32m_launch<AK, BK>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, slices, cslice, wide, s)
   if (a_kmajor) {
     if (b_kmajor) HA_F32M(true, true);
     HA_F32M(true, false);

@@ -1200,7 +1200,8 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
     """Exact fp32 ``alpha * a @ b`` (``+ out`` when ``accumulate``) on a 128 x 128-tile kernel with
     split-K, two workgroups per CU: the products whose 256 x 256 tiles cannot fill the GPU (1024^3
     .. 6144^3) and short-K tall updates (the Householder rank-256 update). ``kernel``: "mid"
-    (default: LDS-DMA pipeline, ``csrc/gemm_mid.hip: gemm_f32m``) or "s" (register-staged,
+    (default: LDS-DMA pipeline, ``csrc/gemm_mid.hip: gemm_f32m``, 256 x 128 tiles where they fill
+    the GPU, else 128 x 128; "mid128" / "mid256" force one) or "s" (register-staged,
     ``csrc/gemm_small.hip: gemm_f32s``; also where gemm_f32m's operand requirements fail). Any
     row-/column-major operand views; None where neither kernel applies (host tensors, unaligned
     operands: the caller picks another GEMM)."""
@@ -1233,11 +1234,14 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
         slices = 1
         if tiles < 2 * ncu and K >= 512:   # two workgroups per CU: split K over the missing ones
             slices = max(1, min(-(-2 * ncu // tiles), K // 256, _SPLITK_MAX_BYTES // (4 * M * N)))
-    mid = (kernel or ("mid" if _GEMM_MID else "s")) == "mid"
+    kernel = kernel or ("mid" if _GEMM_MID else "s")
+    mid = kernel.startswith("mid")
+    tile = {"mid128": 1, "mid256": 2}.get(kernel, 0)
     if mid and ((M if a_km else K) % 4 or (N if not b_nm else K) % 4 or min(M, N, K) < 4):
         mid = False          # gemm_f32m's operand requirements (contiguous extents multiples of 4)
     if mid:
-        launch, used_fn = L.ha_gemm_f32m, L.ha_gemm_f32m_slices
+        used_fn = L.ha_gemm_f32m_slices
+        launch = lambda *args: L.ha_gemm_f32m(*args[:-1], tile, args[-1])   # noqa: E731
         bflag = int(not b_nm)            # gemm_f32m takes "B k-major"
     else:
         launch, used_fn = L.ha_gemm_f32s, L.ha_gemm_f32s_slices

@@ -281,7 +281,7 @@ def test_matmul_gram_and_cov_route_to_upper_tiles(gpu):
                                    (132, 4, 136), (2000, 36, 4), (5000, 256, 700), (128, 20000, 256), (300, 260, 132),
                                    (4100, 128, 100), (1000, 52, 516), (2052, 1028, 260)])
 @pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
-@pytest.mark.parametrize("kernel", ["mid", "s"])
+@pytest.mark.parametrize("kernel", ["mid128", "mid256", "s"])
 def test_gemm_f32_small_layouts(m, k, n, layout, kernel):
     """128-tile split-K kernels (LDS-DMA gemm_f32m and register-staged gemm_f32s): every operand
     layout, edges, K tails, split-K, alpha / accumulate."""
@@ -317,11 +317,11 @@ def test_gemm_f32_small_layouts(m, k, n, layout, kernel):
     assert torch.all(err[:, :8] == 0) and torch.all(err[:, 8 + n:] == 0)
 
 
-@pytest.mark.parametrize("m,k,n", [(6000, 96, 5000), (5996, 64, 4100)])
+@pytest.mark.parametrize("m,k,n", [(6000, 96, 5000), (5996, 64, 4100), (2000, 1000, 1000)])
 @pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
-def test_gemm_f32_mid_persistent(m, k, n, layout):
-    """Enough 128-tiles for the persistent gemm_f32m grid (cross-tile DMA prefetch, >= 4 tiles per
-    CU, K % 32 == 0): every layout, edge tiles in M and N, plain and accumulating."""
+def test_gemm_f32_mid_auto_tile(m, k, n, layout):
+    """gemm_f32m with its default tile choice (256 x 128 where the wide tiles fill the GPU): every
+    layout, edge tiles in M and N, plain and accumulating."""
     from heat_amd import ops
 
     dev = _dev()
@@ -340,7 +340,8 @@ def test_gemm_f32_mid_persistent(m, k, n, layout):
 
 
 @pytest.mark.parametrize("m,n,k", [(20000, 3840, 256), (4096, 768, 32), (9000, 300, 256)])
-def test_gemm_f32_mid_update_shape(m, n, k):
+@pytest.mark.parametrize("kernel", ["mid128", "mid256"])
+def test_gemm_f32_mid_update_shape(m, n, k, kernel):
     """The Householder trailing-update form C[:, j:] -= V X on the LDS-DMA 128-tile kernel (C a
     column slice of a row-major matrix, V row-major, X k-major) against fp64."""
     from heat_amd import ops
@@ -353,7 +354,7 @@ def test_gemm_f32_mid_update_shape(m, n, k):
     C = A[:, 256:]
     ref = C.double() - V.double() @ X.double()
     left = A[:, :256].clone()
-    assert ops.gemm_f32_small(V, X, out=C, alpha=-1.0, accumulate=True, kernel="mid") is not None
+    assert ops.gemm_f32_small(V, X, out=C, alpha=-1.0, accumulate=True, kernel=kernel) is not None
     assert torch.equal(A[:, :256], left)
     assert torch.all((C.double() - ref).abs() <= _bound(V, X) + 1e-6 * ref.abs())
 

@@ -45,16 +45,18 @@ def main():
             b = torch.randn(n, n, device="cuda")
             reps = 50 if n <= 2048 else 10
             ref = a.double() @ b.double()
-            c = K.gemm_f32_small(a, b, kernel="mid")
+            c = K.gemm_f32_small(a, b, kernel="mid256")
             err = float((c.double() - ref).abs().max())
             t_lib = timed(lambda: torch.mm(a, b), reps)
             sl = (1, 2, 3, 4, 6, 8, 12) if n <= 3072 else (1, 2, 3)
-            t_m, s_m = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid"), sl, reps)
+            t_m, s_m = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid128"), sl, reps)
+            t_w, s_w = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid256"), sl, reps)
             t_s, s_s = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="s"), sl, reps)
             t_t, s_t = best(lambda s: K.gemm_f32(a, b, slices=s), sl, reps)
             fl = 2.0 * n ** 3
             print(json.dumps({"M": n, "N": n, "K": n, "hipblaslt_ms": round(t_lib, 4), "f32m_ms": round(t_m, 4),
-                              "f32m_slices": s_m, "f32s_ms": round(t_s, 4), "f32s_slices": s_s,
+                              "f32m_slices": s_m, "f32m256_ms": round(t_w, 4), "f32m256_slices": s_w,
+                              "f32m256_vs_lib": round(t_w / t_lib, 3), "f32s_ms": round(t_s, 4), "f32s_slices": s_s,
                               "f32t_ms": round(t_t, 4), "f32t_slices": s_t, "f32m_vs_lib": round(t_m / t_lib, 3),
                               "f32s_vs_lib": round(t_s / t_lib, 3), "hipblaslt_tf": round(fl / t_lib / 1e9, 1),
                               "f32m_tf": round(fl / t_m / 1e9, 1), "f32m_max_abs_err": err}), flush=True)
@@ -69,15 +71,17 @@ def main():
             X = torch.randn(Kd, N, device="cuda") * 1e-3
             rows = slice(0, 4096)
             ref = C[rows].double() - V[rows].double() @ X.double()
-            K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid")
+            K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid256")
             err = float((C[rows].double() - ref).abs().max())
             t_lib = timed(lambda: K._exact_addmm_(C, V, X, -1.0), 5)
-            t_m = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid"), 5)
+            t_m = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid128"), 5)
+            t_w = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid256"), 5)
             t_s = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="s"), 5)
             t_t = timed(lambda: K.gemm_f32(V, X, out=C, accumulate=True, alpha=-1.0), 5)
             fl = 2.0 * m * N * Kd
             print(json.dumps({"M": m, "N": N, "K": Kd, "update": True, "hipblaslt_ms": round(t_lib, 3),
-                              "f32m_ms": round(t_m, 3), "f32s_ms": round(t_s, 3), "f32t_ms": round(t_t, 3),
+                              "f32m_ms": round(t_m, 3), "f32m256_ms": round(t_w, 3),
+                              "f32m256_vs_lib": round(t_w / t_lib, 3), "f32s_ms": round(t_s, 3), "f32t_ms": round(t_t, 3),
                               "f32m_vs_lib": round(t_m / t_lib, 3), "hipblaslt_tf": round(fl / t_lib / 1e9, 1),
                               "f32m_tf": round(fl / t_m / 1e9, 1), "f32m_max_abs_err_4096rows": err}), flush=True)
             del V, X, ref

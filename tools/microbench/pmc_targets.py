@@ -64,12 +64,12 @@ def main():
             a = torch.randn(n, n, device="cuda")
             b = torch.randn(n, n, device="cuda")
             for _ in range(2):
-                ops.gemm_f32_small(a, b, slices=sl, kernel="mid")
+                ops.gemm_f32_small(a, b, slices=sl, kernel="mid256")
         A = torch.randn(400_000, 4096, device="cuda")
         V = torch.randn(400_000, 256, device="cuda")
         X = torch.randn(256, 3840, device="cuda") * 1e-3
         for _ in range(2):
-            ops.gemm_f32_small(V, X, out=A[:, 256:], alpha=-1.0, accumulate=True, kernel="mid")
+            ops.gemm_f32_small(V, X, out=A[:, 256:], alpha=-1.0, accumulate=True, kernel="mid256")
     elif which == "tri":
         a = torch.randn(1_250_000, 4096, device="cuda")
         r = torch.triu(torch.randn(4096, 4096, device="cuda")) + 4 * torch.eye(4096, device="cuda")
