@@ -16,7 +16,8 @@ on every path (``extra.comm_ab``) and ``extra.comm.collective_paths`` counts the
 collective of the run took.
 Secondary workloads: ``--workload cdist`` (distance_matrix, streamed), ``--workload knn`` (the
 distance_matrix config reduced to each row's ``--topk`` nearest rows by the fused kernel, no
-matrix) and ``--workload moments`` (statistical_moments mean/var of 1e9 float32).
+matrix), ``--workload moments`` (statistical_moments mean/var of 1e9 float32) and ``--workload qr``
+(the tall-skinny QR config: ht.linalg.qr of 1.25e6 x 4096 float32 per GPU, split=0, Q and R).
 """
 from __future__ import annotations
 
@@ -34,7 +35,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="kmeans", choices=["kmeans", "cdist", "knn", "moments"])
+    p.add_argument("--workload", default="kmeans", choices=["kmeans", "cdist", "knn", "moments", "qr"])
     p.add_argument("--n-per-gpu", type=int, default=None,
                    help="kmeans: points per GPU (1.25e7); moments: elements per GPU (1e9)")
     p.add_argument("--rows", type=int, default=1_000_000, help="cdist: total rows (strong scaling)")
@@ -307,6 +308,33 @@ def main():
         extra["certified_rechecked_fraction"] = st["rechecked"] / st["queries"] if st["queries"] else None
         extra.update(validate_knn(x, d, idx, comm))
         scaling = "strong"
+    elif args.workload == "qr":
+        # BASELINE tall-skinny QR config: 1e7 x 4096 float32 split=0 on 8 GPUs = 1.25e6 rows per GPU
+        # (weak scaling), ht.linalg.qr (CholeskyQR2: Gram + fp64 Cholesky + triangular-B products,
+        # R replicated, Q split like A) at float32 matmul precision "highest" (exact fp32 products)
+        args.n_per_gpu = args.n_per_gpu or (1_250_000 if torch.cuda.is_available() else 4096)
+        f = args.f or (4096 if torch.cuda.is_available() else 64)
+        n = args.n_per_gpu * n_gpus
+        torch.set_float32_matmul_precision("highest")
+        ht.random.seed(11)
+        a = ht.random.randn(n, f, split=0, device=dev)
+        for _ in range(args.warmup):
+            q, r = ht.linalg.qr(a, mode="reduced")
+        del q, r
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            q, r = ht.linalg.qr(a, mode="reduced")
+        sync()
+        dt = time.perf_counter() - t0
+        ms = rank_times(comm, dt, args.steps, extra)
+        flops = 4.0 * n * f * f - 4.0 * f ** 3 / 3
+        value = flops / (ms * 1e-3) / 1e9
+        metric, unit = "tsqr_gflops", "GFLOP/s"
+        cfg = {"model": "tsqr Q,R m={} n={} float32 split=0 (CholeskyQR2)".format(n, f), "global_batch": n,
+               "seq_len": f, "parallelism": "dp{}".format(n_gpus), "n_per_gpu": args.n_per_gpu}
+        extra["flop_convention"] = "4 m n^2 - 4 n^3 / 3 (Householder QR with Q formed)"
+        extra.update(validate_qr(a, q, r, comm))
     else:
         args.n_per_gpu = args.n_per_gpu or 1_000_000_000
         n = args.n_per_gpu * n_gpus
@@ -543,6 +571,26 @@ def check_labels(X, C, lab, comm, sample: int = 65536) -> dict:
         excess = comm.allreduce(excess, ht.MPI.MAX)
     return {"label_agreement": agree / max(total, 1.0), "label_max_excess": excess,
             "labels_checked": int(total), "labels_ok": excess <= 4e-6}
+
+
+def validate_qr(a, q, r, comm) -> dict:
+    """The timed QR's factors against fp64, outside the timed region: orthogonality of the first
+    64 columns of Q (Q[:, :64]^T Q[:, :64] summed over the ranks), the reconstruction Q R = A on the
+    first 4096 local rows of every rank (relative to max |A|), R upper triangular."""
+    import heat_amd as ht
+
+    Q, A = q.larray, a.larray
+    R = ht.resplit(r, None).larray if r.is_distributed() else r.larray
+    G = Q[:, :64].double().T @ Q[:, :64].double()
+    if comm.size > 1:
+        comm.Allreduce(ht.MPI.IN_PLACE, G, ht.MPI.SUM)
+    orth = float((G - torch.eye(G.shape[0], dtype=torch.float64, device=G.device)).abs().max())
+    rows = min(4096, A.shape[0])
+    rec = float((Q[:rows].double() @ R.double() - A[:rows].double()).abs().max() / A[:rows].abs().max()) if rows else 0.0
+    rec = comm.allreduce(rec, ht.MPI.MAX) if comm.size > 1 else rec
+    upper = bool(torch.equal(R, torch.triu(R)))
+    return {"q_orth_err_64cols": orth, "qr_rec_rel_err": rec, "r_upper": upper,
+            "qr_ok": bool(orth < 1e-4 and rec < 1e-4 and upper)}
 
 
 def validate_moments(x, m, v, comm) -> dict:

@@ -54,10 +54,11 @@ def test_bench_multi_rank_one_json_line(ranks):
     assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= 1e-6 * rec["value"]
 
 
-@pytest.mark.parametrize("workload", ["moments", "cdist", "knn"])
+@pytest.mark.parametrize("workload", ["moments", "cdist", "knn", "qr"])
 def test_bench_secondary_workloads_validate(workload):
     env = dict(os.environ, HEAT_COMM_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    extra_args = ["--n-per-gpu", "100000"] if workload == "moments" else ["--rows", "6000", "--f", "8"]
+    extra_args = {"moments": ["--n-per-gpu", "100000"], "qr": ["--n-per-gpu", "3000", "--f", "48"]}.get(
+        workload, ["--rows", "6000", "--f", "8"])
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
            "--workload", workload] + extra_args
@@ -70,6 +71,9 @@ def test_bench_secondary_workloads_validate(workload):
         assert ex["mean_abs_err_vs_fp64"] < 1e-5 and ex["var_rel_err_vs_fp64"] < 1e-5
     elif workload == "cdist":
         assert ex["sample_max_sq_err_rel_vs_fp64"] < 1e-5
+    elif workload == "qr":
+        assert lines[0]["scaling"] == "weak" and lines[0]["config"]["global_batch"] == 6000
+        assert ex["qr_ok"] is True and ex["q_orth_err_64cols"] < 1e-5 and ex["r_upper"] is True
     else:
         assert lines[0]["scaling"] == "strong" and lines[0]["config"]["global_batch"] == 6000
         assert ex["self_first"] is True and ex["index_agreement"] == 1.0 and ex["max_rel_dist_err"] < 1e-5
