@@ -323,7 +323,9 @@ def main():
         del q, r
         sync()
         t0 = time.perf_counter()
+        q = r = None
         for _ in range(args.steps):
+            q = r = None     # the previous step's 20 GB Q is released before the next is allocated
             q, r = ht.linalg.qr(a, mode="reduced")
         sync()
         dt = time.perf_counter() - t0
