@@ -136,17 +136,19 @@ def _native_plan(M: int, N: int, K: int):
     split-K slice sum, (s + 1) M N 4 bytes at ~4 TB/s, plus one extra launch (~5 us) when s > 1.
     gemm_f32t ("f32t"): 256-tiles, one workgroup per CU, o = 256 k (prologue + C epilogue per
     tile), rate 1; gemm_f32m ("f32s": the 128-tile LDS-DMA kernel behind ops.gemm_f32_small),
-    two workgroups per CU, o = 64, rate 0.92; a workgroup alone on its CU runs at 2 x 0.87 of the
-    shared rate, so a last wave of at most one per CU costs 0.575 of a wave. eff = W / (the
-    waves' time) for W waves of tiles x slices. Measured (profiles/
-    gemm_mid_r06.jsonl, r6i rows) and picked: 1024^3 f32s x4 (0.032 ms, 1.30x hipBLASLt), 2048^3
-    f32s x1 (0.140, 1.07x), 3072^3 f32s x4 (0.506, 1.11x), 4096^3 f32t x1 (0.977, 1.04x), 6144^3
-    f32s x1 (3.55, 1.16x)."""
+    two workgroups per CU, o = 64, rate 0.92; its 64 x 64-tile form ("f32m64"), rate 0.90 - no
+    split-K needed where 128-tiles are too few; a workgroup alone on its CU runs at 2 x 0.87 of
+    the shared rate, so a last wave of at most one per CU costs 0.575 of a wave. eff = W / (the
+    waves' time) for W waves of tiles x slices. Measured (profiles/gemm_mid_r06.jsonl, r6m rows)
+    and picked: 1024^3 f32m64 x1 (0.023 ms, 0.88x hipBLASLt), 2048^3 f32m64 x1 (0.141, 1.10x; the
+    128-tile form ties), 3072^3 f32m64 x1 (0.470, 1.04x), 4096^3 f32t x1 (0.977, 1.04x), 6144^3
+    f32s x1 (3.58, 1.17x)."""
     from ... import ops
 
     ncu = ops.num_cus(torch.device("cuda", torch.cuda.current_device())) if torch.cuda.is_available() else 256
     t256 = -(-M // 256) * -(-N // 256)
     t128 = -(-M // 128) * -(-N // 128)
+    t64 = -(-M // 64) * -(-N // 64)
     unit = 2.0 * M * N / 140e12           # seconds per unit of K at ~140 TF
     best = None
     for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
@@ -154,10 +156,11 @@ def _native_plan(M: int, N: int, K: int):
         if s > 1 and (ks < 64 or s * M * N * 4 > (1 << 30)):
             continue
         extra = 0.0 if s == 1 else (s + 1) * M * N * 4 / 4e12 / unit + 5e-6 / unit
-        for kern, tiles, slots, o, rate in (("f32t", t256, ncu, 256, 1.0), ("f32s", t128, 2 * ncu, 64, 0.92)):
+        for kern, tiles, slots, o, rate in (("f32t", t256, ncu, 256, 1.0), ("f32s", t128, 2 * ncu, 64, 0.92),
+                                            ("f32m64", t64, 2 * ncu, 64, 0.90)):
             w = tiles * s / slots
             full, frac = int(w), w - int(w)
-            if kern == "f32s" and 0 < frac <= 0.5:
+            if kern != "f32t" and 0 < frac <= 0.5:
                 # a last wave of at most one workgroup per CU runs unshared: 1 / (2 x 0.87) of a wave
                 waves = full + 0.575
             else:
@@ -211,8 +214,9 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
         # products whose 256 x 256 tiles do not fill the GPU: the hand-written kernel and K-slice
         # count of the measured cost model (_native_plan); the library only if neither applies
         kern, sl = _native_plan(a.shape[0], b.shape[1], a.shape[1])
-        if _GEMM_PLAN and kern == "f32s":
-            r = _kern.gemm_f32_small(a, b, out=out, alpha=alpha, accumulate=accumulate, slices=sl)
+        if _GEMM_PLAN and kern in ("f32s", "f32m64"):
+            r = _kern.gemm_f32_small(a, b, out=out, alpha=alpha, accumulate=accumulate, slices=sl,
+                                     kernel="mid64" if kern == "f32m64" else None)
             if r is not None:
                 return r
         elif _GEMM_PLAN:

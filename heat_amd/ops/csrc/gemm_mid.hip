@@ -60,20 +60,20 @@ __device__ __forceinline__ void gm_dma16(const void* g, unsigned lds) {
                : "memory");
 }
 
-// at most N of this wave's vector-memory ops outstanding, LDS ops retired, then the barrier
+// at most N of this wave's vector-memory ops outstanding, LDS ops retired, then the barrier (any
+// N < 64: the count is an assembler immediate; an earlier three-case form fell back to vmcnt(0)
+// for the counts of the 256 x 128 variant, 12 and 6)
 template <int N>
 __device__ __forceinline__ void gm_wait_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int N>
 __device__ __forceinline__ void gm_vm_wait() {
-  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
 // One operand's staging for this lane, TR tile rows (128 or 256). KC (k-contiguous, [rows][K]
@@ -122,9 +122,9 @@ struct GmSrc {
 };
 
 // Fragments of one stage for a wave: a[b][s], b[b][s] = block b's operand at k = 8 h + s.
-template <int WMB>
+template <int WMB, int WNB>
 struct GmFrag {
-  float a[WMB][8], b[2][8];
+  float a[WMB][8], b[WNB][8];
 };
 
 // AK: A k-major ([K][M], m contiguous) - else row-major ([M][K], k contiguous).
@@ -133,28 +133,31 @@ struct GmFrag {
 // NBUF = 4, the default); 4: 256 x 128 tiles (waves of 128 x 64: 0.75 LDS floats per MFMA instead
 // of 1, 43 instead of 32 flop per staged byte; NBUF = 3, 72 KB; measured slower - A/B only). Two
 // workgroups per CU either way.
-template <bool AK, bool BK_, int WMB, int NBUF>
+template <bool AK, bool BK_, int WMB, int NBUF, int WNB = 2>
 __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
                                                     int64_t kps, int64_t cslice) {
   constexpr int TM = 64 * WMB;          // tile rows
+  constexpr int TN = 64 * WNB;          // tile columns
   constexpr int AOP = TM * MK * 4;      // bytes of A per stage
-  constexpr int STG = AOP + MOP;        // bytes per stage
+  constexpr int BOP = TN * MK * 4;      // bytes of B per stage
+  constexpr int STG = AOP + BOP;        // bytes per stage
   constexpr int PAW = TM / 64;          // A pieces per wave per stage (TM / 16 pieces / 4 waves)
+  constexpr int PBW = TN / 64;          // B pieces per wave per stage
   constexpr int AHEAD = NBUF - 1;       // stages in flight
-  constexpr int DPS = PAW + 2;          // DMA instructions per wave per stage
+  constexpr int DPS = PAW + PBW;        // DMA instructions per wave per stage
   static_assert(NBUF * STG <= 80 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r = lane & 31;
-  const unsigned tn = (unsigned)((N + MB - 1) / MB), tm = (unsigned)((M + TM - 1) / TM);
+  const unsigned tn = (unsigned)((N + TN - 1) / TN), tm = (unsigned)((M + TM - 1) / TM);
   const unsigned bid = gm_xcd_remap(blockIdx.x, tm * tn);
   constexpr unsigned GM = 8;
   const unsigned grp = bid / (GM * tn), gfirst = grp * GM;
   const unsigned gsz = tm - gfirst < GM ? tm - gfirst : GM;
-  const int64_t m0 = (int64_t)(gfirst + (bid % (GM * tn)) % gsz) * TM, n0 = (int64_t)((bid % (GM * tn)) / gsz) * MB;
+  const int64_t m0 = (int64_t)(gfirst + (bid % (GM * tn)) % gsz) * TM, n0 = (int64_t)((bid % (GM * tn)) / gsz) * TN;
   // split-K: slice blockIdx.y = k in [y kps MK, min((y + 1) kps MK, K)) into C + y cslice
   {
     const int64_t k0 = (int64_t)blockIdx.y * kps * MK;
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     C += (int64_t)blockIdx.y * cslice;
   }
   GmSrc<!AK, TM> sa;
-  GmSrc<!BK_, MB> sb;
+  GmSrc<!BK_, TN> sb;
   sa.init(A, lda, M, m0, lane);
   sb.init(B, ldb, N, n0, lane);
   const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
@@ -178,8 +181,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
       gm_dma16(full ? sa.src(k0, q) : sa.src_clamped(k0, q, K, lane), dst + q * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = 2 * wave + i;
+    for (int i = 0; i < PBW; ++i) {
+      const int q = PBW * wave + i;
       gm_dma16(full ? sb.src(k0, q) : sb.src_clamped(k0, q, K, lane), dst + AOP + q * 1024);
     }
   };
@@ -192,8 +195,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
       if (sa.beyond(k0, q, K, lane)) *reinterpret_cast<floatx4*>(dst + q * 1024 + lane * 16) = (floatx4)(0.f);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = 2 * wave + i;
+    for (int i = 0; i < PBW; ++i) {
+      const int q = PBW * wave + i;
       if (sb.beyond(k0, q, K, lane)) *reinterpret_cast<floatx4*>(dst + AOP + q * 1024 + lane * 16) = (floatx4)(0.f);
     }
   };
@@ -219,6 +222,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
           o[bl][4 + s] = x1[s];
         }
       }
+    } else if constexpr (NB == 1) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) o[0][s] = *reinterpret_cast<const float*>(b + (8 * h + s) * (TR * 4) + (w0 + r) * 4);
     } else if constexpr (NB == 2) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
@@ -235,12 +241,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
       }
     }
   };
-  auto load = [&](GmFrag<WMB>& F, int64_t t) {
+  auto load = [&](GmFrag<WMB, WNB>& F, int64_t t) {
     const unsigned char* base = smem + (t % NBUF) * STG;
     opnd(base, wm * 32 * WMB, std::integral_constant<bool, !AK>(), std::integral_constant<int, WMB>(),
          std::integral_constant<int, TM>(), F.a);
-    opnd(base + AOP, wn * 64, std::integral_constant<bool, !BK_>(), std::integral_constant<int, 2>(),
-         std::integral_constant<int, MB>(), F.b);
+    opnd(base + AOP, wn * 32 * WNB, std::integral_constant<bool, !BK_>(), std::integral_constant<int, WNB>(),
+         std::integral_constant<int, TN>(), F.b);
   };
 
   // accumulator (block bm, bn) element g <-> tile row / column (see the header)
@@ -248,25 +254,34 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     const int rho = (g & 3) + 8 * (g >> 2) + 4 * h;
     return wm * 32 * WMB + (AK ? WMB * rho + bm : 32 * bm + rho);
   };
-  auto ccol = [&](int bn) -> int { return wn * 64 + (BK_ ? 2 * r + bn : 32 * bn + r); };
+  auto ccol = [&](int bn) -> int { return wn * 32 * WNB + (BK_ ? WNB * r + bn : 32 * bn + r); };
 
-  floatx16 acc[WMB][2];
-  const bool full = m0 + TM <= M && n0 + MB <= N;
+  floatx16 acc[WMB][WNB];
+  const bool full = m0 + TM <= M && n0 + TN <= N;
 #pragma unroll
   for (int bm = 0; bm < WMB; ++bm)
 #pragma unroll
-    for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = (floatx16)(0.f);
+    for (int bn = 0; bn < WNB; ++bn) acc[bm][bn] = (floatx16)(0.f);
 
-  auto mma_row = [&](const GmFrag<WMB>& F, int bm) {
+  auto mma_row = [&](const GmFrag<WMB, WNB>& F, int bm) {
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-      for (int bn = 0; bn < 2; ++bn)
+      for (int bn = 0; bn < WNB; ++bn)
         acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[bm][s], F.b[bn][s], acc[bm][bn], 0, 0, 0);
   };
-  auto mma_half = [&](const GmFrag<WMB>& F, int part) {
+  // the stage's MFMAs in two halves around the barrier: by block rows, or (one block row) by k-steps
+  auto mma_half = [&](const GmFrag<WMB, WNB>& F, int part) {
+    if constexpr (WMB >= 2) {
 #pragma unroll
-    for (int bm = part * WMB / 2; bm < (part + 1) * WMB / 2; ++bm) mma_row(F, bm);
+      for (int bm = part * WMB / 2; bm < (part + 1) * WMB / 2; ++bm) mma_row(F, bm);
+    } else {
+#pragma unroll
+      for (int s = 4 * part; s < 4 * part + 4; ++s)
+#pragma unroll
+        for (int bn = 0; bn < WNB; ++bn)
+          acc[0][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(F.a[0][s], F.b[bn][s], acc[0][bn], 0, 0, 0);
+    }
   };
 
   const int64_t nk = K > 0 ? (K + MK - 1) / MK : 0;
@@ -285,12 +300,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
   // steady state: stage t + AHEAD issued (whole, in range), MFMAs of the first half of the block
   // rows around it, the counted wait for stage t + 1 + barrier, then stage t + 1's fragment reads
   // between the second half's MFMAs
-  auto step_full = [&](int64_t t, const GmFrag<WMB>& Fc, GmFrag<WMB>& Fn) {
+  auto step_full = [&](int64_t t, const GmFrag<WMB, WNB>& Fc, GmFrag<WMB, WNB>& Fn) {
     stage(t + AHEAD, true);
     mma_half(Fc, 0);
 #pragma unroll
     for (int q = 0; q < DPS; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 8 * WMB / DPS, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * WMB * WNB / DPS, 0);  // MFMA
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // VMEM read (the asm DMA)
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -305,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
   // start of the last k-stage instead measured 18 % slower on that update: 214 VGPRs; a persistent
   // grid with cross-tile DMA prefetch measured 5 % slower; profiles/gemm_mid_r06.jsonl.)
   const bool fast = full && ldc < (1 << 23);
-  auto step = [&](int64_t t, const GmFrag<WMB>& Fc, GmFrag<WMB>& Fn) {
+  auto step = [&](int64_t t, const GmFrag<WMB, WNB>& Fc, GmFrag<WMB, WNB>& Fn) {
     if (t + AHEAD < nk) stage(t + AHEAD, !(tail && t + AHEAD == nk - 1));
     mma_half(Fc, 0);
     if (t + 1 < nk) {
@@ -315,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     mma_half(Fc, 1);
   };
 
-  GmFrag<WMB> F0, F1;
+  GmFrag<WMB, WNB> F0, F1;
   for (int64_t t = 0; t < AHEAD && t < nk; ++t) stage(t, !(tail && t == nk - 1));
   if (nk > 0) {
     ready(0);
@@ -340,15 +355,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
     // one accumulator row's C values (32 loads in flight) before its stores
 #pragma unroll
     for (int bm = 0; bm < WMB; ++bm) {
-      float cv[2][16];
+      float cv[WNB][16];
       if (beta) {
 #pragma unroll
-        for (int bn = 0; bn < 2; ++bn)
+        for (int bn = 0; bn < WNB; ++bn)
 #pragma unroll
           for (int g = 0; g < 16; ++g) cv[bn][g] = Ct[crow(bm, g) * l + ccol(bn)];
       }
 #pragma unroll
-      for (int bn = 0; bn < 2; ++bn)
+      for (int bn = 0; bn < WNB; ++bn)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           float v = alpha * acc[bm][bn][g];
@@ -360,10 +375,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
   }
 #pragma unroll
   for (int bm = 0; bm < WMB; ++bm) {
-    float cv[2][16];
+    float cv[WNB][16];
     if (beta) {
 #pragma unroll
-      for (int bn = 0; bn < 2; ++bn) {
+      for (int bn = 0; bn < WNB; ++bn) {
         const int64_t gc = n0 + ccol(bn);
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
@@ -373,7 +388,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
       }
     }
 #pragma unroll
-    for (int bn = 0; bn < 2; ++bn) {
+    for (int bn = 0; bn < WNB; ++bn) {
       const int64_t gc = n0 + ccol(bn);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
@@ -389,13 +404,16 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
 template <bool AK, bool BK_>
 int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, float alpha, int beta, int64_t slices, int64_t cslice, int wide, hipStream_t s) {
-  const int64_t tm = wide ? 256 : MB;
-  const int64_t tiles = ((M + tm - 1) / tm) * ((N + MB - 1) / MB);
+  const int64_t tm = wide == 1 ? 256 : wide == 2 ? 64 : MB, tnn = wide == 2 ? 64 : MB;
+  const int64_t tiles = ((M + tm - 1) / tm) * ((N + tnn - 1) / tnn);
   const int64_t nk = (K + MK - 1) / MK, kps = (nk + slices - 1) / slices;
   const int64_t ns = (nk + kps - 1) / kps;
   if (tiles > 0x7fffffffLL || ns > 65535) return HA_UNSUPPORTED;
   const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
-  if (wide)
+  if (wide == 2)
+    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 1, 4, 1>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
+                       cslice);
+  else if (wide)
     hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4, 3>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
   else
     hipLaunchKernelGGL((gemm_f32m<AK, BK_, 2, 4>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
@@ -416,7 +434,8 @@ HA_EXPORT int64_t ha_gemm_f32m_slices(int64_t K, int64_t slices) {
 // C[M, N] (row-major, ldc) = alpha A B (+ C if beta), exact fp32 products and accumulation.
 // a_kmajor: A element (m, k) at A[k lda + m] (else A[m lda + k]); b_kmajor: B element (k, n) at
 // B[k ldb + n] (else B[n ldb + k]). slices > 1: split-K over 16-k stages, slice y -> C + y cslice
-// (beta must be 0; the caller sums the partials). tile: 0 auto, 1 128 x 128, 2 256 x 128. Requirements (else HA_UNSUPPORTED): 16-byte
+// (beta must be 0; the caller sums the partials). tile: 0 auto, 1 128 x 128, 2 256 x 128, 3 64 x 64.
+// Requirements (else HA_UNSUPPORTED): 16-byte
 // aligned A and B, lda and ldb multiples of 4, the contiguous extent of each operand (K for a
 // k-contiguous one, M / N for the other) a multiple of 4, M, N, K >= 4.
 HA_EXPORT int ha_gemm_f32m(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
@@ -432,7 +451,7 @@ HA_EXPORT int ha_gemm_f32m(const float* A, const float* B, float* C, int64_t M, 
   // measured slower on every shape (71 vs 84 % MFMA-busy at 6144^3, update 25.2 vs 23.3 ms;
   // profiles/gemm_mid_r06.jsonl, r6j rows): an A/B form only
   static const int wide_env = getenv("HEAT_GM_WIDE") ? atoi(getenv("HEAT_GM_WIDE")) : 0;
-  const int wide = tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
+  const int wide = tile == 3 ? 2 : tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
 #define HA_F32M(AK, BK) return f32m_launch<AK, BK>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, slices, cslice, wide, s)
   if (a_kmajor) {
     if (b_kmajor) HA_F32M(true, true);

@@ -51,14 +51,20 @@ def main():
             sl = (1, 2, 3, 4, 6, 8, 12) if n <= 3072 else (1, 2, 3)
             t_m, s_m = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid128"), sl, reps)
             t_w, s_w = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid256"), sl, reps)
+            t_6, s_6 = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid64"), sl[:4], reps)
             t_s, s_s = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="s"), sl, reps)
             t_t, s_t = best(lambda s: K.gemm_f32(a, b, slices=s), sl, reps)
+            from heat_amd.core.linalg import basics
+            t_p = timed(lambda: basics.fgemm(a, b), reps)   # what ht.matmul runs (the plan's pick)
+            plan = basics._native_plan(n, n, n)
             fl = 2.0 * n ** 3
             print(json.dumps({"M": n, "N": n, "K": n, "hipblaslt_ms": round(t_lib, 4), "f32m_ms": round(t_m, 4),
                               "f32m_slices": s_m, "f32m256_ms": round(t_w, 4), "f32m256_slices": s_w,
-                              "f32m256_vs_lib": round(t_w / t_lib, 3), "f32s_ms": round(t_s, 4), "f32s_slices": s_s,
+                              "f32m256_vs_lib": round(t_w / t_lib, 3), "f32m64_ms": round(t_6, 4), "f32m64_slices": s_6,
+                              "f32m64_vs_lib": round(t_6 / t_lib, 3), "f32s_ms": round(t_s, 4), "f32s_slices": s_s,
                               "f32t_ms": round(t_t, 4), "f32t_slices": s_t, "f32m_vs_lib": round(t_m / t_lib, 3),
-                              "f32s_vs_lib": round(t_s / t_lib, 3), "hipblaslt_tf": round(fl / t_lib / 1e9, 1),
+                              "f32s_vs_lib": round(t_s / t_lib, 3), "plan": list(plan), "plan_ms": round(t_p, 4),
+                              "plan_vs_lib": round(t_p / t_lib, 3), "hipblaslt_tf": round(fl / t_lib / 1e9, 1),
                               "f32m_tf": round(fl / t_m / 1e9, 1), "f32m_max_abs_err": err}), flush=True)
             del a, b, ref, c
             torch.cuda.empty_cache()
