@@ -21,6 +21,7 @@ import math
 from typing import List, Optional, Tuple, Union
 
 import numpy as np
+import functools
 import os
 
 import torch
@@ -130,6 +131,7 @@ def _native_fp32(a: torch.Tensor, b: torch.Tensor) -> bool:
 _GEMM_PLAN = os.environ.get("HEAT_GEMM_PLAN", "1") != "0"   # 0: the library for the small products
 
 
+@functools.lru_cache(maxsize=1024)
 def _native_plan(M: int, N: int, K: int):
     """(kernel, K slices) for an exact fp32 product that fills the GPU poorly with 256 x 256 tiles.
     Cost model (units of K per output element): time ~ M N (K + s o_k) / (eff_k rate_k) + the
@@ -172,6 +174,7 @@ def _native_plan(M: int, N: int, K: int):
     return best[1], best[2]
 
 
+@functools.lru_cache(maxsize=1024)
 def _library_better(M: int, N: int, K: int, exact: bool) -> bool:
     """Plain fp32 GEMMs whose 256 x 256 output tiles fill the 256 CUs poorly go to the library
     (hipBLASLt, exact fp32 products). Measured (``tools/microbench/gemm_small.py``, profiles/README):

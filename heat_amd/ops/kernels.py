@@ -1192,6 +1192,9 @@ _GEMM_SMALL = os.environ.get("HEAT_GEMM_SMALL", "1") != "0"
 # the 128-tile kernel: "mid" (LDS-DMA pipelined, csrc/gemm_mid.hip: gemm_f32m) or "s" (the round-5
 # register-staged gemm_f32s, A/B)
 _GEMM_MID = os.environ.get("HEAT_GEMM_MID", "1") != "0"
+# products with K <= this on the 64 x 64-tile gemm_f32m by default (the Householder in-block
+# updates, K = 32: 1.25e6 x 4096 factor + Q 1.346 -> 1.322 s, profiles/gemm_mid_r06.jsonl); 0 = off
+_GM64_MAXK = int(os.environ.get("HEAT_GM64_MAXK", "64"))
 
 
 def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
@@ -1234,6 +1237,8 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
         slices = 1
         if tiles < 2 * ncu and K >= 512:   # two workgroups per CU: split K over the missing ones
             slices = max(1, min(-(-2 * ncu // tiles), K // 256, _SPLITK_MAX_BYTES // (4 * M * N)))
+    if kernel is None and _GEMM_MID and K <= _GM64_MAXK:
+        kernel = "mid64"   # short K: per-tile latency dominates, more (smaller) tiles per CU hide it
     kernel = kernel or ("mid" if _GEMM_MID else "s")
     mid = kernel.startswith("mid")
     tile = {"mid128": 1, "mid256": 2, "mid64": 3}.get(kernel, 0)
