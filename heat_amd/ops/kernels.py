@@ -1756,8 +1756,8 @@ def householder_apply(A: torch.Tensor, panels, C: torch.Tensor, g0: int = 0, tra
 # update is a plain fp32 GEMM with a small K (256 outer / 32 inner) and a tall C read and written
 # once. Measured at 1.25e6 rows (tools/microbench/gemm_mid.py, profiles/gemm_mid_r06.jsonl):
 # K = 256, N = 3840: gemm_f32m 23.05 ms, hipBLASLt 19.75, gemm_f32t 27.6; the whole 1.25e6 x 4096
-# factorisation + Q 1.354 s native vs 1.305 s with the library update (tools/microbench/
-# hh_update_ab.py) - 4 % for a QR with no library GEMM in it. The blas form runs at float32 matmul
+# factorisation + Q 1.32 s native (K <= 64 products on the 64 x 64 tile) vs 1.28-1.31 s with the
+# library update (tools/microbench/hh_update_ab.py) - 1-3 % for a QR with no library GEMM in it. The blas form runs at float32 matmul
 # precision "highest" whatever the caller set: under "high" hipBLASLt drops to a reduced-precision
 # fp32 path (measured ||Q^T Q - I|| 1.5e-5 instead of 1.2e-7, tools/microbench/hh_prec.py).
 _HH_UPDATE = os.environ.get("HEAT_HH_UPDATE", "small")

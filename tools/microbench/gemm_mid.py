@@ -82,12 +82,14 @@ def main():
             t_lib = timed(lambda: K._exact_addmm_(C, V, X, -1.0), 5)
             t_m = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid128"), 5)
             t_w = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid256"), 5)
+            t_6 = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid64"), 5)
             t_s = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="s"), 5)
             t_t = timed(lambda: K.gemm_f32(V, X, out=C, accumulate=True, alpha=-1.0), 5)
             fl = 2.0 * m * N * Kd
             print(json.dumps({"M": m, "N": N, "K": Kd, "update": True, "hipblaslt_ms": round(t_lib, 3),
                               "f32m_ms": round(t_m, 3), "f32m256_ms": round(t_w, 3),
-                              "f32m256_vs_lib": round(t_w / t_lib, 3), "f32s_ms": round(t_s, 3), "f32t_ms": round(t_t, 3),
+                              "f32m256_vs_lib": round(t_w / t_lib, 3), "f32m64_ms": round(t_6, 3),
+                              "f32m64_vs_lib": round(t_6 / t_lib, 3), "f32s_ms": round(t_s, 3), "f32t_ms": round(t_t, 3),
                               "f32m_vs_lib": round(t_m / t_lib, 3), "hipblaslt_tf": round(fl / t_lib / 1e9, 1),
                               "f32m_tf": round(fl / t_m / 1e9, 1), "f32m_max_abs_err_4096rows": err}), flush=True)
             del V, X, ref
