@@ -94,7 +94,9 @@ __global__ __launch_bounds__(256) void gemm64(const double* __restrict__ A, cons
 }
 
 // upper Cholesky of the nb x nb block at G[k0, k0] (row-major, ld), in place (the strictly lower
-// part of the block is zeroed); one workgroup of 256 threads.
+// part of the block is zeroed); one workgroup of 256 threads. (One-wave forms measured slower: the
+// block in LDS 113 vs 89 us - LDS round trips on the dependency chain; a register-resident,
+// fully unrolled form did not compile in 40 minutes.)
 __global__ __launch_bounds__(256) void chol_diag(double* __restrict__ G, int64_t ld, int64_t k0, int nb,
                                                  int* __restrict__ info) {
   __shared__ double S[64][65];
@@ -137,7 +139,10 @@ __global__ __launch_bounds__(256) void chol_diag(double* __restrict__ G, int64_t
 }
 
 // R12 = R11^-T G12 for the rows [k0, k0 + nb) and columns [k0 + nb, n) of G (row-major): thread
-// c owns column c of the panel; forward substitution over the nb rows with R11 from LDS.
+// c owns column c of the panel; forward substitution over the nb rows with R11 from LDS. FULL
+// (nb == 64, every panel but a last partial one): no per-row guards, so x stays in 128 VGPRs -
+// the guarded form put x in scratch (528 B per thread: 205 us per panel, 13 ms per factor).
+template <bool FULL>
 __global__ __launch_bounds__(256) void chol_panel(double* __restrict__ G, int64_t ld, int64_t n, int64_t k0, int nb) {
   __shared__ double R[64][65];
   const int tid = threadIdx.x;
@@ -149,22 +154,36 @@ __global__ __launch_bounds__(256) void chol_panel(double* __restrict__ G, int64_
   const int64_t c = k0 + nb + (int64_t)blockIdx.x * 256 + tid;
   if (c >= n) return;
   double x[64];
+  if constexpr (FULL) {
 #pragma unroll
-  for (int i = 0; i < 64; ++i)
-    if (i < nb) x[i] = G[(k0 + i) * ld + c];
+    for (int i = 0; i < 64; ++i) x[i] = G[(k0 + i) * ld + c];
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    if (i < nb) {
+    for (int i = 0; i < 64; ++i) {
       double s = x[i];
 #pragma unroll
-      for (int p = 0; p < 64; ++p)
-        if (p < i) s -= R[p][i] * x[p];
+      for (int p = 0; p < i; ++p) s -= R[p][i] * x[p];
       x[i] = s / R[i][i];
     }
-  }
 #pragma unroll
-  for (int i = 0; i < 64; ++i)
-    if (i < nb) G[(k0 + i) * ld + c] = x[i];
+    for (int i = 0; i < 64; ++i) G[(k0 + i) * ld + c] = x[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; ++i)
+      if (i < nb) x[i] = G[(k0 + i) * ld + c];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      if (i < nb) {
+        double s = x[i];
+#pragma unroll
+        for (int p = 0; p < 64; ++p)
+          if (p < i) s -= R[p][i] * x[p];
+        x[i] = s / R[i][i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i)
+      if (i < nb) G[(k0 + i) * ld + c] = x[i];
+  }
 }
 
 // inverse of every b x b upper-triangular diagonal block (b <= 64) of R (row-major, ld) into the
@@ -661,7 +680,10 @@ HA_EXPORT int ha_chol_upper64(double* G, int64_t n, int64_t ld, int* info, void*
     hipLaunchKernelGGL(chol_diag, dim3(1), dim3(256), 0, s, G, ld, k0, nb, info);
     const int64_t k1 = k0 + nb, m = n - k1;
     if (m <= 0) break;
-    hipLaunchKernelGGL(chol_panel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, G, ld, n, k0, nb);
+    if (nb == 64)
+      hipLaunchKernelGGL(chol_panel<true>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, G, ld, n, k0, nb);
+    else
+      hipLaunchKernelGGL(chol_panel<false>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, G, ld, n, k0, nb);
     // G22 -= R12^T R12: A = R12^T (k-major: element (i, p) at R12[p][i]), B = R12 (k-major)
     const double* R12 = G + k0 * ld + k1;
     const int rc = gemm64_launch<true, true, true>(R12, R12, G + k1 * ld + k1, m, m, nb, ld, ld, ld, 1, 0, 0, 0,
