@@ -351,8 +351,9 @@ def _cholqr_native(A: torch.Tensor, comm, calc_q: bool, distributed: bool):
 
 def _cond_estimate_inv(R: torch.Tensor, Rinv: torch.Tensor, iters: int = 12) -> float:
     """2-norm condition number estimate ||R|| ||R^-1|| by power iteration on R^T R and
-    R^-T R^-1 (fp64 matrix-vector products on ``ops.gemm64``; deterministic start vector)."""
-    from ... import ops
+    R^-T R^-1 (fp64 matrix-vector products on ``ops.gemv64``, the transposes copied once;
+    deterministic start vector)."""
+    from ...ops import kernels as _k
 
     n = R.shape[0]
     if n == 0:
@@ -361,10 +362,11 @@ def _cond_estimate_inv(R: torch.Tensor, Rinv: torch.Tensor, iters: int = 12) -> 
     x0 = (torch.rand(n, 1, generator=g, dtype=torch.float64) + 0.5).to(R.device)
     res = []
     for M in (R, Rinv):
+        Mt = M.T.contiguous()
         x = x0 / x0.norm()
         s = 0.0
         for _ in range(iters):
-            y = ops.gemm64(M.T, ops.gemm64(M, x))
+            y = _k.gemv64(Mt, _k.gemv64(M, x))
             s = float(y.norm())
             if not 0.0 < s < float("inf"):
                 return float("inf")

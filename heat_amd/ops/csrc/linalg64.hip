@@ -726,3 +726,32 @@ HA_EXPORT int ha_trtri_upper64(const double* R, int64_t n, int64_t ld, double* X
   }
   return ha_launch_status();
 }
+
+namespace {
+// y[r] = sum_k M[r][k] x[k] (fp64, row-major M with leading dimension ld): one 256-thread block per
+// row, a fixed-order tree reduction (deterministic). The condition estimate of CholeskyQR2 runs
+// 48 of these on 4096 x 4096 factors; on gemm64 (64 x 64 tiles, one output column) each took
+// 0.44 ms - 21 ms per QR - against ~30 us at HBM speed here.
+__global__ __launch_bounds__(256) void gemv64_rows(const double* __restrict__ M, int64_t ld, int64_t cols,
+                                                   const double* __restrict__ x, double* __restrict__ y) {
+  __shared__ double red[4];
+  const int64_t r = blockIdx.x;
+  const double* row = M + r * ld;
+  double s = 0.0;
+  for (int64_t k = threadIdx.x; k < cols; k += 256) s = fma(row[k], x[k], s);
+  s = ha_wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) y[r] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+}  // namespace
+
+// y = M x for a row-major fp64 M [rows, cols] (leading dimension ld), x [cols], y [rows].
+HA_EXPORT int ha_gemv64(const double* M, int64_t rows, int64_t cols, int64_t ld, const double* x, double* y,
+                        void* stream) {
+  if (rows < 0 || cols < 0 || ld < cols || !M || !x || !y) return HA_BAD_ARG;
+  if (rows == 0) return HA_OK;
+  if (rows > 0x7fffffffLL) return HA_UNSUPPORTED;
+  hipLaunchKernelGGL(gemv64_rows, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, M, ld, cols, x, y);
+  return ha_launch_status();
+}

@@ -1543,6 +1543,22 @@ def gemm64(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
+def gemv64(m: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """fp64 ``m @ x`` for a matrix [rows, cols] and a vector [cols] (or [cols, 1]): one block per
+    row with a fixed-order reduction (``csrc/linalg64.hip: gemv64_rows``) for device fp64 input
+    (a row-major view; a transposed view is copied once), torch otherwise."""
+    shape1 = x.dim() == 2
+    xv = x.reshape(-1)
+    if not (_native64(m) and xv.dtype == torch.float64 and m.dim() == 2 and m.shape[1] == xv.numel()):
+        return m @ x
+    M = m if (m.stride(1) == 1 and (m.shape[0] <= 1 or m.stride(0) >= m.shape[1])) else m.contiguous()
+    xc = xv.contiguous()
+    y = torch.empty(M.shape[0], dtype=torch.float64, device=m.device)
+    check(lib().ha_gemv64(_ptr(M), M.shape[0], M.shape[1], M.stride(0) if M.shape[0] > 1 else M.shape[1], _ptr(xc),
+                          _ptr(y), ctypes.c_void_p(stream_ptr(m.device))), "ha_gemv64")
+    return y.reshape(-1, 1) if shape1 else y
+
+
 def cholesky_upper(g: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """Upper Cholesky factor R (G = R^T R) of a symmetric positive definite fp64 matrix and a
     device int32 ``info`` (0, or 1 + the first failing column). Device tensors: the blocked

@@ -252,3 +252,20 @@ def _householder_two_level_check(dev, ops):
     assert orth < 1e-6, orth
     rec = (Q @ r.double() - a.to(dev).double()).abs().max().item() / a.abs().max().item()
     assert rec < 1e-5, rec
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (4096, 4096), (300, 1000), (1000, 3)])
+def test_gemv64_device(rows, cols):
+    """fp64 matrix-vector product kernel (CholeskyQR2's condition estimate) against torch fp64,
+    row-major and transposed-view inputs."""
+    from heat_amd.ops import kernels as K
+
+    dev = _dev()
+    g = torch.Generator().manual_seed(rows + cols)
+    m = torch.randn(rows, cols, generator=g, dtype=torch.float64).to(dev)
+    x = torch.randn(cols, 1, generator=g, dtype=torch.float64).to(dev)
+    y = K.gemv64(m, x)
+    assert y.shape == (rows, 1)
+    assert torch.allclose(y, m @ x, rtol=1e-12, atol=1e-12 * cols)
+    yt = K.gemv64(m.T, torch.ones(rows, dtype=torch.float64, device=dev))
+    assert torch.allclose(yt, m.sum(0), rtol=1e-12, atol=1e-12 * rows)
