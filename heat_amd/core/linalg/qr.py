@@ -81,9 +81,14 @@ def qr(a: DNDarray, tiles_per_proc: Union[int, torch.Tensor] = 1, calc_q: bool =
         k = min(r.shape)
         d = torch.sign(torch.diagonal(r[:k, :k]))
         d = torch.where(d == 0, torch.ones_like(d), d)
-        r = torch.cat([d.unsqueeze(1) * r[:k], r[k:]], 0)
-        if q is not None:
-            q = torch.cat([q[:, :k] * d.unsqueeze(0), q[:, k:]], 1)
+        # in place, and only when a sign flips (CholeskyQR's R has a positive diagonal already):
+        # the former cat-of-products form copied the m x n Q twice (~16 ms at 1.25e6 x 4096)
+        if not bool((d == 1).all()):
+            r = r.clone() if r._base is not None else r
+            r[:k] *= d.unsqueeze(1)
+            if q is not None:
+                q = q.clone() if q._base is not None else q
+                q[:, :k] *= d.unsqueeze(0)
         R = DNDarray(r, tuple(r.shape), dtype, a.split, a.device, a.comm, True)
         Q = DNDarray(q, tuple(q.shape), dtype, a.split, a.device, a.comm, True) if calc_q else None
         return QR(Q, R)

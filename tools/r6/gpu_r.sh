@@ -2,7 +2,7 @@
 # round 6, call r: vectorised fp64 slice sums (Gram) - QR
 # tests, TSQR benchmark, kernel trace of the factor
 set -o pipefail
-OUT=gpurun_out/r6r; mkdir -p $OUT
+OUT=gpurun_out/r6s; mkdir -p $OUT
 ROOT=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp PYTHONPATH=$ROOT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_qr.py tests/test_gpu_gemm.py -k "gram or qr or cholesky or householder or tri or split" > $OUT/test_qr.txt 2>&1 || exit 1
