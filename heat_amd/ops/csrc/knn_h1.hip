@@ -472,17 +472,23 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
   // HEAT_H1_CFG=q (A/B): one barrier per 4 chunks (8-slot ring, 73.7 KB of LDS per workgroup):
   // 368-370 vs 297 ms for the pair form on one box (knn_h1_ab_r05.jsonl)
   static const bool cfg_q = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'q';
-#define HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, PB)                                                        \
+  // HEAT_H1_CFG=p (A/B): the f = 128 default with one barrier per pair of chunks (8-wave workgroup)
+  static const bool cfg_p = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'p';
+  // HEAT_H1_CFG=o (A/B): the round-5 f = 128 form, two workgroups per CU of 4 waves x 32 points, one
+  // barrier per pair of chunks
+  static const bool cfg_o = getenv("HEAT_H1_CFG") && getenv("HEAT_H1_CFG")[0] == 'o';
+#define HA_H1TK_LAUNCH_K(FP, KH, KO, NPB, TPI, MINB, WV, PB)                                                    \
   do {                                                                                                         \
     using KC = H3Cfg<FP, NPB>;                                                                                 \
     const size_t lds = (PB > 1 ? 2 * PB : TPI >= 3 ? 3 : 4) * ((size_t)TPI * KC::KS * 1024 + TPI * 512); /* slots */ \
     const int ppw = WV * NPB * 32;                                                                             \
     const unsigned blocks = (unsigned)((n + ppw - 1) / ppw);                                                   \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, 16, KO, NPB, TPI, MINB, WV, PB>),             \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(h1_topk<FP, KH, KO, NPB, TPI, MINB, WV, PB>),             \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                  \
-    hipLaunchKernelGGL((h1_topk<FP, 16, KO, NPB, TPI, MINB, WV, PB>), dim3(blocks), dim3(64 * WV), lds, s, p,   \
+    hipLaunchKernelGGL((h1_topk<FP, KH, KO, NPB, TPI, MINB, WV, PB>), dim3(blocks), dim3(64 * WV), lds, s, p,   \
                        sx, n, image, u, meta, kpad / (TPI * 32), kn, dist, idx, cert, dbg);                     \
   } while (0)
+#define HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, PB) HA_H1TK_LAUNCH_K(FP, 16, KO, NPB, TPI, MINB, WV, PB)
 #define HA_H1TK_LAUNCH(FP, KO, NPB, TPI, MINB, WV) HA_H1TK_LAUNCH_X(FP, KO, NPB, TPI, MINB, WV, 1)
 #define HA_H1TK(FP)                                                                                              \
   case FP: {                                                                                                     \
@@ -495,15 +501,24 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
     /* 2-tile chunks, one barrier per pair of chunks, chunk ch + 2 issued during ch (4-tile chunks, one */   \
     /* barrier each, 3 in flight for f = 16: whole 1 KB image pieces per wave). Measured at f = 128 */            \
     /* (tools/microbench/h1_ab.py, one box): pair 309-310 ms, per-chunk barrier (HEAT_H1_CFG=b) 313-315; */     \
-    /* 3-tile chunks / 2 in flight +2%; one workgroup of 4 x 64 points per CU (HEAT_H1_CFG=a) +30% */           \
+    /* 3-tile chunks / 2 in flight +2%; one workgroup of 4 x 64 points per CU (HEAT_H1_CFG=a) +30%. */          \
+    /* f = 128 (round 6, bench.py --workload knn, one box, knn_h1_ab_r06.jsonl): ONE workgroup per CU of */       \
+    /* 8 waves x 32 points, one barrier per 4 chunks (8-slot ring, 136 KB): every staged chunk feeds 256 */        \
+    /* points (half the DMA instructions and L2 reads per point) and a quarter of the barriers: 277-279 */        \
+    /* vs 295-298 ms (round-5 form, HEAT_H1_CFG=o); a barrier per pair (p) 282-283 */                          \
     constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
     constexpr int PAIR = TPB == 2 ? 2 : 1;                                                                       \
     if (FP == 128 && cfg_a && kp == 32) {                                                                        \
       HA_H1TK_LAUNCH(128, 32, 2, 4, 1, 4);                                                                       \
     } else if (FP == 128 && cfg_w8 && kp == 32) {                                                                \
       HA_H1TK_LAUNCH(128, 32, 1, 2, 1, 8);                                                                       \
+    } else if (FP == 128 && cfg_p && kp == 32) {                                                                 \
+      HA_H1TK_LAUNCH_X(128, 32, 1, 2, 1, 8, 2);                                                                  \
     } else if (FP == 128 && cfg_q && kp == 32) {                                                                 \
       HA_H1TK_LAUNCH_X(128, 32, 1, 2, 2, 4, 4);                                                                  \
+    } else if (FP == 128 && !cfg_o && !cfg_b) {                                                                  \
+      if (kp == 32) HA_H1TK_LAUNCH_X(128, 32, 1, 2, 1, 8, 4);                                                    \
+      else HA_H1TK_LAUNCH_X(128, 16, 1, 2, 1, 8, 4);                                                             \
     } else if (cfg_b && kp == 32) {                                                                              \
       HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2, 4);                                                                      \
     } else if (kp == 32) {                                                                                       \
