@@ -85,16 +85,20 @@ power = pow
 
 
 def bitwise_and(t1, t2, out=None, where=True) -> DNDarray:
+    """Element-wise bitwise AND of integer or boolean operands (floats raise TypeError); ``where``
+    masks the positions written."""
     _check_exact(t1, t2, "bitwise_and")
     return _operations.binary_op(torch.bitwise_and, t1, t2, out, where)
 
 
 def bitwise_or(t1, t2, out=None, where=True) -> DNDarray:
+    """Element-wise bitwise OR of integer or boolean operands (floats raise TypeError)."""
     _check_exact(t1, t2, "bitwise_or")
     return _operations.binary_op(torch.bitwise_or, t1, t2, out, where)
 
 
 def bitwise_xor(t1, t2, out=None, where=True) -> DNDarray:
+    """Element-wise bitwise XOR of integer or boolean operands (floats raise TypeError)."""
     _check_exact(t1, t2, "bitwise_xor")
     return _operations.binary_op(torch.bitwise_xor, t1, t2, out, where)
 
@@ -110,11 +114,13 @@ bitwise_not = invert
 
 
 def left_shift(t1, t2, out=None, where=True) -> DNDarray:
+    """Element-wise ``t1 << t2`` for integer operands (floats raise TypeError)."""
     _check_exact(t1, t2, "left_shift")
     return _operations.binary_op(torch.bitwise_left_shift, t1, t2, out, where)
 
 
 def right_shift(t1, t2, out=None, where=True) -> DNDarray:
+    """Element-wise ``t1 >> t2`` (arithmetic shift) for integer operands (floats raise TypeError)."""
     _check_exact(t1, t2, "right_shift")
     return _operations.binary_op(torch.bitwise_right_shift, t1, t2, out, where)
 

@@ -90,16 +90,20 @@ class RegressionMixin:
 
 
 def is_classifier(estimator: object) -> bool:
+    """True when ``estimator`` is a ClassificationMixin."""
     return isinstance(estimator, ClassificationMixin)
 
 
 def is_estimator(estimator: object) -> bool:
+    """True when ``estimator`` is a BaseEstimator."""
     return isinstance(estimator, BaseEstimator)
 
 
 def is_clusterer(estimator: object) -> bool:
+    """True when ``estimator`` is a ClusteringMixin."""
     return isinstance(estimator, ClusteringMixin)
 
 
 def is_regressor(estimator: object) -> bool:
+    """True when ``estimator`` is a RegressionMixin."""
     return isinstance(estimator, RegressionMixin)

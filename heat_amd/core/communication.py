@@ -1087,10 +1087,12 @@ __default_comm = MPI_WORLD
 
 
 def get_comm() -> Communication:
+    """The process-wide default communicator (COMM_WORLD unless ``use_comm`` changed it)."""
     return __default_comm
 
 
 def sanitize_comm(comm: Optional[Communication]) -> Communication:
+    """``comm`` if it is a Communication, the default communicator for None; TypeError otherwise."""
     if comm is None:
         return get_comm()
     if isinstance(comm, Communication):
@@ -1099,5 +1101,6 @@ def sanitize_comm(comm: Optional[Communication]) -> Communication:
 
 
 def use_comm(comm: Communication = None):
+    """Make ``comm`` (or COMM_WORLD for None) the default communicator of new arrays."""
     global __default_comm
     __default_comm = sanitize_comm(comm)

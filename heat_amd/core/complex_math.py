@@ -18,6 +18,7 @@ def angle(x, deg: bool = False, out=None) -> DNDarray:
 
 
 def conjugate(x, out=None) -> DNDarray:
+    """Element-wise complex conjugate (a copy for real input). Local op, split preserved."""
     return _operations.local_op(lambda t: torch.conj(t).resolve_conj(), x, out, no_cast=True)
 
 
@@ -25,6 +26,7 @@ conj = conjugate
 
 
 def imag(x) -> DNDarray:
+    """Imaginary part (zeros of the same shape for real input). Local op, split preserved."""
     if types.heat_type_is_complexfloating(x.dtype):
         return _operations.local_op(lambda t: torch.imag(t).clone(), x, no_cast=True)
     from . import factories
@@ -33,6 +35,7 @@ def imag(x) -> DNDarray:
 
 
 def real(x) -> DNDarray:
+    """Real part (the array itself for real input). Local op, split preserved."""
     if types.heat_type_is_complexfloating(x.dtype):
         return _operations.local_op(lambda t: torch.real(t).clone(), x, no_cast=True)
     return x

@@ -211,30 +211,39 @@ def __factory_like(a, dtype, split, factory: Callable, device, comm, order: str 
 
 
 def empty(shape, dtype=types.float32, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Uninitialised array of global ``shape``. With ``split`` each rank allocates only its block of
+    that axis (``comm.chunk``), on ``device``. Reference ``heat/core/factories.py: empty``."""
     return __factory(shape, dtype, split, torch.empty, device, comm, order)
 
 
 def empty_like(a, dtype=None, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Uninitialised array with the shape of ``a``; dtype, split, device and comm default to ``a``'s."""
     return __factory_like(a, dtype, split, empty, device, comm, order=order)
 
 
 def zeros(shape, dtype=types.float32, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Array of zeros of global ``shape`` (each rank fills only its block along ``split``)."""
     return __factory(shape, dtype, split, torch.zeros, device, comm, order)
 
 
 def zeros_like(a, dtype=None, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Zeros with the shape of ``a``; dtype, split, device and comm default to ``a``'s."""
     return __factory_like(a, dtype, split, zeros, device, comm, order=order)
 
 
 def ones(shape, dtype=types.float32, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Array of ones of global ``shape`` (each rank fills only its block along ``split``)."""
     return __factory(shape, dtype, split, torch.ones, device, comm, order)
 
 
 def ones_like(a, dtype=None, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Ones with the shape of ``a``; dtype, split, device and comm default to ``a``'s."""
     return __factory_like(a, dtype, split, ones, device, comm, order=order)
 
 
 def full(shape, fill_value, dtype=types.float32, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """Array of global ``shape`` filled with ``fill_value`` (a complex value makes a real default dtype
+    complex, as in the reference)."""
     if isinstance(fill_value, complex) and not types.heat_type_is_complexfloating(types.canonical_heat_type(dtype)):
         # a complex fill value makes the default (real) dtype complex, like the reference
         dtype = types.complex64 if types.canonical_heat_type(dtype) is not types.float64 else types.complex128
@@ -246,6 +255,7 @@ def full(shape, fill_value, dtype=types.float32, split=None, device=None, comm=N
 
 
 def full_like(a, fill_value, dtype=types.float32, split=None, device=None, comm=None, order="C") -> DNDarray:
+    """``fill_value`` with the shape of ``a``; split, device and comm default to ``a``'s."""
     return __factory_like(a, dtype, split, full, device, comm, fill_value=fill_value, order=order)
 
 
@@ -304,6 +314,8 @@ def linspace(start, stop, num: int = 50, endpoint: bool = True, retstep: bool = 
 
 def logspace(start, stop, num: int = 50, endpoint: bool = True, base: float = 10.0, dtype=None, split=None,
              device=None, comm=None) -> DNDarray:
+    """``num`` samples ``base ** t`` for t evenly spaced over [start, stop] (computed in float64, then cast
+    to ``dtype``, float32 by default); split like ``linspace``."""
     y = linspace(start, stop, num=num, endpoint=endpoint, split=split, device=device, comm=comm, dtype=types.float64)
     data = torch.pow(torch.tensor(base, dtype=torch.float64, device=y.larray.device), y.larray)
     htype = types.canonical_heat_type(dtype) if dtype is not None else types.float32

@@ -75,38 +75,47 @@ def allclose(x, y, rtol: float = 1e-05, atol: float = 1e-08, equal_nan: bool = F
 
 
 def isfinite(x) -> DNDarray:
+    """Element-wise test for finite values (not inf, not nan); boolean result, split preserved."""
     return _operations.local_op(torch.isfinite, x, no_cast=True)
 
 
 def isinf(x) -> DNDarray:
+    """Element-wise test for +inf or -inf; boolean result, split preserved."""
     return _operations.local_op(torch.isinf, x, no_cast=True)
 
 
 def isnan(x) -> DNDarray:
+    """Element-wise test for nan; boolean result, split preserved."""
     return _operations.local_op(torch.isnan, x, no_cast=True)
 
 
 def isneginf(x, out=None) -> DNDarray:
+    """Element-wise test for -inf; boolean result, split preserved."""
     return _operations.local_op(torch.isneginf, x, out, no_cast=True)
 
 
 def isposinf(x, out=None) -> DNDarray:
+    """Element-wise test for +inf; boolean result, split preserved."""
     return _operations.local_op(torch.isposinf, x, out, no_cast=True)
 
 
 def logical_and(t1, t2) -> DNDarray:
+    """Element-wise truth-value AND of two operands (non-zero is True); broadcasting binary op."""
     return _operations.binary_op(lambda a, b: torch.logical_and(a.bool(), b.bool()), t1, t2)
 
 
 def logical_or(t1, t2) -> DNDarray:
+    """Element-wise truth-value OR of two operands (non-zero is True); broadcasting binary op."""
     return _operations.binary_op(lambda a, b: torch.logical_or(a.bool(), b.bool()), t1, t2)
 
 
 def logical_xor(t1, t2) -> DNDarray:
+    """Element-wise truth-value XOR of two operands (non-zero is True); broadcasting binary op."""
     return _operations.binary_op(lambda a, b: torch.logical_xor(a.bool(), b.bool()), t1, t2)
 
 
 def logical_not(t, out=None) -> DNDarray:
+    """Element-wise truth-value NOT; boolean result, split preserved."""
     return _operations.local_op(torch.logical_not, t, out, no_cast=True)
 
 

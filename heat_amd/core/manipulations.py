@@ -242,6 +242,8 @@ def column_stack(arrays: Sequence[DNDarray]) -> DNDarray:
 
 
 def hstack(arrays: Sequence[DNDarray]) -> DNDarray:
+    """Stack arrays column-wise: concatenation along axis 1, or along axis 0 when every input is 1-D
+    (numpy semantics). Reference ``heat/core/manipulations.py: hstack``."""
     arrays = list(arrays)
     if all(a.ndim == 1 for a in arrays):
         return concatenate(arrays, axis=0)
@@ -466,10 +468,12 @@ def flip(a: DNDarray, axis=None) -> DNDarray:
 
 
 def fliplr(a: DNDarray) -> DNDarray:
+    """Reverse the order of the columns (axis 1); a split along axis 1 moves blocks between mirrored ranks."""
     return flip(a, 1)
 
 
 def flipud(a: DNDarray) -> DNDarray:
+    """Reverse the order of the rows (axis 0); a split along axis 0 moves blocks between mirrored ranks."""
     return flip(a, 0)
 
 
@@ -852,18 +856,21 @@ def split(x: DNDarray, indices_or_sections, axis: int = 0) -> List[DNDarray]:
 
 
 def hsplit(x: DNDarray, indices_or_sections) -> List[DNDarray]:
+    """Split into sub-arrays along axis 1 (axis 0 for 1-D input), as ``split(x, indices_or_sections, 1)``."""
     if len(x.gshape) < 1:
         raise ValueError("hsplit only works on arrays of 1 or more dimensions")
     return split(x, indices_or_sections, axis=1 if x.ndim > 1 else 0)
 
 
 def vsplit(x: DNDarray, indices_or_sections) -> List[DNDarray]:
+    """Split into sub-arrays along axis 0 (input of 2 or more dimensions)."""
     if len(x.gshape) < 2:
         raise ValueError("vsplit only works on arrays of 2 or more dimensions")
     return split(x, indices_or_sections, axis=0)
 
 
 def dsplit(x: DNDarray, indices_or_sections) -> List[DNDarray]:
+    """Split into sub-arrays along axis 2 (input of 3 or more dimensions)."""
     if len(x.gshape) < 3:
         raise ValueError("dsplit only works on arrays of 3 or more dimensions")
     return split(x, indices_or_sections, axis=2)

@@ -12,26 +12,32 @@ __all__ = ["eq", "equal", "ge", "greater", "greater_equal", "gt", "le", "less", 
 
 
 def eq(x, y) -> DNDarray:
+    """Element-wise ``x == y`` (boolean); operands broadcast, a scalar operand is allowed."""
     return _operations.binary_op(torch.eq, x, y)
 
 
 def ne(x, y) -> DNDarray:
+    """Element-wise ``x != y`` (boolean); operands broadcast, a scalar operand is allowed."""
     return _operations.binary_op(torch.ne, x, y)
 
 
 def ge(x, y) -> DNDarray:
+    """Element-wise ``x >= y`` (boolean); operands broadcast, a scalar operand is allowed."""
     return _operations.binary_op(torch.ge, x, y)
 
 
 def gt(x, y) -> DNDarray:
+    """Element-wise ``x > y`` (boolean); operands broadcast, a scalar operand is allowed."""
     return _operations.binary_op(torch.gt, x, y)
 
 
 def le(x, y) -> DNDarray:
+    """Element-wise ``x <= y`` (boolean); operands broadcast, a scalar operand is allowed."""
     return _operations.binary_op(torch.le, x, y)
 
 
 def lt(x, y) -> DNDarray:
+    """Element-wise ``x < y`` (boolean); operands broadcast, a scalar operand is allowed."""
     return _operations.binary_op(torch.lt, x, y)
 
 

@@ -30,14 +30,17 @@ def fabs(x, out=None) -> DNDarray:
 
 
 def ceil(x, out=None) -> DNDarray:
+    """Element-wise ceiling (smallest integer-valued float >= x). Local op, split preserved."""
     return _operations.local_op(torch.ceil, x, out)
 
 
 def floor(x, out=None) -> DNDarray:
+    """Element-wise floor (largest integer-valued float <= x). Local op, split preserved."""
     return _operations.local_op(torch.floor, x, out)
 
 
 def trunc(x, out=None) -> DNDarray:
+    """Element-wise truncation toward zero. Local op, split preserved."""
     return _operations.local_op(torch.trunc, x, out)
 
 

@@ -228,14 +228,17 @@ def heat_type_of(obj) -> Type[datatype]:
 
 
 def heat_type_is_exact(ht_dtype) -> builtins.bool:
+    """True for the exact (boolean and integer) heat types."""
     return canonical_heat_type(ht_dtype) in _exact
 
 
 def heat_type_is_inexact(ht_dtype) -> builtins.bool:
+    """True for the floating-point and complex heat types."""
     return canonical_heat_type(ht_dtype) in _inexact
 
 
 def heat_type_is_complexfloating(ht_dtype) -> builtins.bool:
+    """True for complex64 / complex128."""
     return canonical_heat_type(ht_dtype) in _complexfloating
 
 
@@ -353,6 +356,8 @@ def promote_types(type1, type2) -> Type[datatype]:
 
 
 def issubdtype(arg1, arg2) -> builtins.bool:
+    """numpy-style ``issubdtype``: whether ``arg1`` is ``arg2`` or below it in the heat type hierarchy
+    (arguments may be heat types, torch / numpy dtypes or their names)."""
     if not (isinstance(arg1, type) and issubclass(arg1, datatype)):
         arg1 = canonical_heat_type(arg1)
     if not (isinstance(arg2, type) and issubclass(arg2, datatype)):
@@ -402,6 +407,7 @@ def result_type(*arrays_and_types) -> Type[datatype]:
 
 
 def iscomplex(x):
+    """Element-wise: True where the imaginary part is non-zero (all False for a real dtype)."""
     from . import factories, _operations
 
     if issubclass(x.dtype, _complexfloating):
@@ -410,6 +416,7 @@ def iscomplex(x):
 
 
 def isreal(x):
+    """Element-wise: True where the imaginary part is zero (all True for a real dtype)."""
     from . import _operations
 
     return _operations.local_op(torch.isreal, x, no_cast=True)

@@ -92,6 +92,7 @@ def lib():
 
 
 def available() -> bool:
+    """Whether the native kernel library can be loaded (the load error is kept for the messages)."""
     try:
         lib()
         return True
@@ -100,6 +101,8 @@ def available() -> bool:
 
 
 def allow_fallback() -> bool:
+    """Whether ``HEAT_AMD_ALLOW_FALLBACK=1`` lets device tensors fall back to torch when the native
+    library is missing (off by default: a missing library on a GPU box is an error)."""
     return os.environ.get("HEAT_AMD_ALLOW_FALLBACK", "0") == "1"
 
 
@@ -123,6 +126,7 @@ LAST_LAUNCH_STREAM = {}
 
 
 def stream_ptr(device=None) -> int:
+    """The raw HIP stream handle of the current torch stream of ``device`` (for the ctypes launches)."""
     s = torch.cuda.current_stream(device)
     if DEBUG_STREAMS:
         LAST_LAUNCH_STREAM[s.device.index] = s
@@ -130,6 +134,7 @@ def stream_ptr(device=None) -> int:
 
 
 def check(rc: int, name: str):
+    """Raise RuntimeError naming ``name`` when a native entry point returned a non-zero status."""
     if rc != 0:
         raise RuntimeError("native kernel {} failed with status {}".format(name, rc))
 

@@ -27,10 +27,12 @@ ARCH = os.environ.get("HEAT_AMD_ARCH", "gfx950")
 
 
 def sources():
+    """The ``.hip`` kernel sources compiled into the library."""
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
 def headers():
+    """The shared ``.h`` headers of the kernel sources."""
     return sorted(glob.glob(os.path.join(CSRC, "*.h")))
 
 
@@ -46,6 +48,7 @@ def file_flags(src: str) -> list:
 
 
 def hipcc() -> str:
+    """Path of the hipcc compiler (``$HIPCC``, PATH, then /opt/rocm/bin)."""
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
             return cand
@@ -61,6 +64,7 @@ def stale_sources() -> list:
 
 
 def needs_build() -> bool:
+    """True when the library is missing or older than a source, a header or this build script."""
     return bool(stale_sources())
 
 

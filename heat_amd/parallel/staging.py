@@ -74,6 +74,7 @@ def _ret(work, fin, async_op):
 
 
 def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
+    """``dist.all_reduce``; for a gloo group and device tensor the data goes through a host copy."""
     if not needs_staging(group, t):
         return dist.all_reduce(t, op=op, group=group, async_op=async_op)
     h = _host(t)
@@ -82,6 +83,7 @@ def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
 
 
 def broadcast(t, src, group=None, async_op=False):
+    """``dist.broadcast`` with host staging for gloo groups and device tensors."""
     if not needs_staging(group, t):
         return dist.broadcast(t, src=src, group=group, async_op=async_op)
     h = _host(t)
@@ -90,6 +92,7 @@ def broadcast(t, src, group=None, async_op=False):
 
 
 def all_gather_into_tensor(out, inp, group=None, async_op=False):
+    """``dist.all_gather_into_tensor`` with host staging for gloo groups and device tensors."""
     if not needs_staging(group, out, inp):
         return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
     ho = torch.empty(out.shape, dtype=out.dtype)
@@ -98,6 +101,7 @@ def all_gather_into_tensor(out, inp, group=None, async_op=False):
 
 
 def reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=None, async_op=False):
+    """``dist.reduce_scatter_tensor``; gloo has none, so a staged all-reduce keeps this rank's slice."""
     if not needs_staging(group, out, inp):
         return dist.reduce_scatter_tensor(out, inp, op=op, group=group, async_op=async_op)
     # gloo has no reduce_scatter of flat tensors: all-reduce the whole input, keep this rank's part
@@ -109,6 +113,7 @@ def reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=None, async_op=F
 
 
 def all_to_all_single(out, inp, out_split_sizes=None, in_split_sizes=None, group=None, async_op=False):
+    """``dist.all_to_all_single`` with host staging for gloo groups and device tensors."""
     if not needs_staging(group, out, inp):
         return dist.all_to_all_single(out, inp, out_split_sizes, in_split_sizes, group=group, async_op=async_op)
     ho = torch.empty(out.shape, dtype=out.dtype)
@@ -117,6 +122,7 @@ def all_to_all_single(out, inp, out_split_sizes=None, in_split_sizes=None, group
 
 
 def isend(t, dst, group=None, tag=0):
+    """``dist.isend``; a staged send keeps its host copy alive in the returned work object."""
     if not needs_staging(group, t):
         return dist.isend(t, dst=dst, group=group, tag=tag)
     h = _host(t)
@@ -124,6 +130,7 @@ def isend(t, dst, group=None, tag=0):
 
 
 def irecv(t, src, group=None, tag=0):
+    """``dist.irecv``; a staged receive copies into ``t`` when its work object is waited on."""
     if not needs_staging(group, t):
         return dist.irecv(t, src=src, group=group, tag=tag)
     h = torch.empty(t.shape, dtype=t.dtype)
@@ -131,10 +138,13 @@ def irecv(t, src, group=None, tag=0):
 
 
 def recv(t, src, group=None, tag=0):
+    """Blocking receive into ``t`` (staged as ``irecv``)."""
     irecv(t, src, group, tag).wait()
 
 
 def batch_isend_irecv(ops: List["dist.P2POp"]):
+    """``dist.batch_isend_irecv`` with host staging for gloo groups and device tensors; the
+    received host buffers are copied back when the returned works are waited on."""
     if not ops or not needs_staging(ops[0].group, *[o.tensor for o in ops]):
         return dist.batch_isend_irecv(ops)
     staged, fins = [], []

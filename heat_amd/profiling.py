@@ -125,6 +125,7 @@ def enable(timing: bool = False) -> None:
 
 
 def disable() -> None:
+    """Undo ``enable``: restore the unwrapped communicator methods and native ops."""
     from .core.communication import MPICommunication
     from . import ops
 
@@ -135,18 +136,22 @@ def disable() -> None:
 
 
 def enabled() -> bool:
+    """Whether the collective / native-op counters are being collected."""
     return _state["enabled"]
 
 
 def counters() -> Dict[str, Dict[str, float]]:
+    """A copy of the per-name counters collected since the last ``reset``."""
     return {k: dict(v) for k, v in _counters.items()}
 
 
 def reset() -> None:
+    """Clear all counters."""
     _counters.clear()
 
 
 def dump(path: str) -> None:
+    """Write ``counters()`` to ``path`` as JSON."""
     with open(path, "w") as f:
         json.dump(counters(), f, indent=1)
 
