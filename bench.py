@@ -318,9 +318,10 @@ def main():
         torch.set_float32_matmul_precision("highest")
         ht.random.seed(11)
         a = ht.random.randn(n, f, split=0, device=dev)
+        q = r = None
         for _ in range(args.warmup):
+            q = r = None
             q, r = ht.linalg.qr(a, mode="reduced")
-        del q, r
         sync()
         t0 = time.perf_counter()
         q = r = None
