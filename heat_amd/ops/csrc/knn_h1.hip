@@ -505,7 +505,8 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
     /* f = 128 (round 6, bench.py --workload knn, one box, knn_h1_ab_r06.jsonl): ONE workgroup per CU of */       \
     /* 8 waves x 32 points, one barrier per 4 chunks (8-slot ring, 136 KB): every staged chunk feeds 256 */        \
     /* points (half the DMA instructions and L2 reads per point) and a quarter of the barriers: 277-279 */        \
-    /* vs 295-298 ms (round-5 form, HEAT_H1_CFG=o); a barrier per pair (p) 282-283 */                          \
+    /* vs 295-298 ms (round-5 form, HEAT_H1_CFG=o); a barrier per pair (p) 282-283. f = 64: 189-191 vs */      \
+    /* 191-192 ms (f = 32 / 16 have fewer image pieces per chunk than 8 waves) */                              \
     constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
     constexpr int PAIR = TPB == 2 ? 2 : 1;                                                                       \
     if (FP == 128 && cfg_a && kp == 32) {                                                                        \
@@ -516,9 +517,11 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
       HA_H1TK_LAUNCH_X(128, 32, 1, 2, 1, 8, 2);                                                                  \
     } else if (FP == 128 && cfg_q && kp == 32) {                                                                 \
       HA_H1TK_LAUNCH_X(128, 32, 1, 2, 2, 4, 4);                                                                  \
-    } else if (FP == 128 && !cfg_o && !cfg_b) {                                                                  \
-      if (kp == 32) HA_H1TK_LAUNCH_X(128, 32, 1, 2, 1, 8, 4);                                                    \
-      else HA_H1TK_LAUNCH_X(128, 16, 1, 2, 1, 8, 4);                                                             \
+    } else if (FP >= 64 && !cfg_o && !cfg_b) {                                                                   \
+      if constexpr (FP >= 64) { /* 8 waves need >= 8 image pieces per chunk */                                   \
+        if (kp == 32) HA_H1TK_LAUNCH_X(FP, 32, 1, 2, 1, 8, 4);                                                   \
+        else HA_H1TK_LAUNCH_X(FP, 16, 1, 2, 1, 8, 4);                                                            \
+      }                                                                                                          \
     } else if (cfg_b && kp == 32) {                                                                              \
       HA_H1TK_LAUNCH(FP, 32, 1, TPB, 2, 4);                                                                      \
     } else if (kp == 32) {                                                                                       \
