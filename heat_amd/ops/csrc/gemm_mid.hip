@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
 template <bool AK, bool BK_>
 int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, float alpha, int beta, int64_t slices, int64_t cslice, int wide, hipStream_t s) {
-  const int64_t tm = wide == 1 ? 256 : wide == 2 ? 64 : MB, tnn = wide == 2 ? 64 : MB;
+  const int64_t tm = wide == 1 ? 256 : wide == 2 ? 64 : MB, tnn = wide >= 2 ? 64 : MB;
   const int64_t tiles = ((M + tm - 1) / tm) * ((N + tnn - 1) / tnn);
   const int64_t nk = (K + MK - 1) / MK, kps = (nk + slices - 1) / slices;
   const int64_t ns = (nk + kps - 1) / kps;
@@ -412,6 +412,9 @@ int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, 
   const dim3 g((unsigned)tiles, (unsigned)ns), b(256);
   if (wide == 2)
     hipLaunchKernelGGL((gemm_f32m<AK, BK_, 1, 4, 1>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
+                       cslice);
+  else if (wide == 3)
+    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 2, 4, 1>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
                        cslice);
   else if (wide)
     hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4, 3>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
@@ -434,7 +437,9 @@ HA_EXPORT int64_t ha_gemm_f32m_slices(int64_t K, int64_t slices) {
 // C[M, N] (row-major, ldc) = alpha A B (+ C if beta), exact fp32 products and accumulation.
 // a_kmajor: A element (m, k) at A[k lda + m] (else A[m lda + k]); b_kmajor: B element (k, n) at
 // B[k ldb + n] (else B[n ldb + k]). slices > 1: split-K over 16-k stages, slice y -> C + y cslice
-// (beta must be 0; the caller sums the partials). tile: 0 auto, 1 128 x 128, 2 256 x 128, 3 64 x 64.
+// (beta must be 0; the caller sums the partials). tile: 0 auto, 1 128 x 128, 2 256 x 128, 3 64 x 64,
+// 4 128 x 64 (A/B only: slower than the 128 x 128 or 64 x 64 form at every square and update shape,
+// profiles/gemm_mid_r06.jsonl r6v rows).
 // Requirements (else HA_UNSUPPORTED): 16-byte
 // aligned A and B, lda and ldb multiples of 4, the contiguous extent of each operand (K for a
 // k-contiguous one, M / N for the other) a multiple of 4, M, N, K >= 4.
@@ -451,7 +456,7 @@ HA_EXPORT int ha_gemm_f32m(const float* A, const float* B, float* C, int64_t M, 
   // measured slower on every shape (71 vs 84 % MFMA-busy at 6144^3, update 25.2 vs 23.3 ms;
   // profiles/gemm_mid_r06.jsonl, r6j rows): an A/B form only
   static const int wide_env = getenv("HEAT_GM_WIDE") ? atoi(getenv("HEAT_GM_WIDE")) : 0;
-  const int wide = tile == 3 ? 2 : tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
+  const int wide = tile == 4 ? 3 : tile == 3 ? 2 : tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
 #define HA_F32M(AK, BK) return f32m_launch<AK, BK>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, slices, cslice, wide, s)
   if (a_kmajor) {
     if (b_kmajor) HA_F32M(true, true);

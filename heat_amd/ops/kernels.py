@@ -1204,7 +1204,7 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
     split-K, two workgroups per CU: the products whose 256 x 256 tiles cannot fill the GPU (1024^3
     .. 6144^3) and short-K tall updates (the Householder rank-256 update). ``kernel``: "mid"
     (default: LDS-DMA pipeline, ``csrc/gemm_mid.hip: gemm_f32m``, 256 x 128 tiles where they fill
-    the GPU, else 128 x 128; "mid128" / "mid256" / "mid64" force a tile) or "s" (register-staged,
+    the GPU, else 128 x 128; "mid128" / "mid256" / "mid64" / "mid128x64" force a tile) or "s" (register-staged,
     ``csrc/gemm_small.hip: gemm_f32s``; also where gemm_f32m's operand requirements fail). Any
     row-/column-major operand views; None where neither kernel applies (host tensors, unaligned
     operands: the caller picks another GEMM)."""
@@ -1241,7 +1241,7 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
         kernel = "mid64"   # short K: per-tile latency dominates, more (smaller) tiles per CU hide it
     kernel = kernel or ("mid" if _GEMM_MID else "s")
     mid = kernel.startswith("mid")
-    tile = {"mid128": 1, "mid256": 2, "mid64": 3}.get(kernel, 0)
+    tile = {"mid128": 1, "mid256": 2, "mid64": 3, "mid128x64": 4}.get(kernel, 0)
     if mid and ((M if a_km else K) % 4 or (N if not b_nm else K) % 4 or min(M, N, K) < 4):
         mid = False          # gemm_f32m's operand requirements (contiguous extents multiples of 4)
     if mid:
