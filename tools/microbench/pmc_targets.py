@@ -14,6 +14,7 @@ tools/gpu_pmc_r03.sh): the hot kernels of the benchmark configs, each warmed up 
   gram    - ht.matmul(A.T, A) at 400000 x 2048 (upper-triangle Gram tiles + fp64 slice sums)
   tri     - CholeskyQR2's A R^-1 at 1.25e6 x 4096 (upper-triangular B: K clipped per column tile),
             2 calls, then the same product as a full GEMM, 1 call
+  libvsmid - 6144^3 exact fp32: hipBLASLt (torch.mm at precision highest) and gemm_f32m 128-tile, 2 calls each
   mid     - the LDS-DMA 128-tile gemm_f32m: 3072^3 (3 K slices), 6144^3 (1 slice) and the
             Householder update C[4e5, 3840] -= V[4e5, 256] X[256, 3840], 2 calls each"""
 import sys
@@ -58,6 +59,14 @@ def main():
     elif which == "knn":
         x = ht.random.rand(1_000_000, 128, split=0)
         ht.spatial.cdist_topk(x, x, 8)
+    elif which == "libvsmid":
+        torch.set_float32_matmul_precision("highest")
+        a = torch.randn(6144, 6144, device="cuda")
+        b = torch.randn(6144, 6144, device="cuda")
+        for _ in range(2):
+            torch.mm(a, b)
+        for _ in range(2):
+            ops.gemm_f32_small(a, b, slices=1, kernel="mid128")
     elif which == "mid":
         torch.set_float32_matmul_precision("highest")
         for n, sl in ((3072, 3), (6144, 1)):
