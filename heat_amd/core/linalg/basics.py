@@ -143,8 +143,11 @@ def _native_plan(M: int, N: int, K: int):
     the shared rate, so a last wave of at most one per CU costs 0.575 of a wave. eff = W / (the
     waves' time) for W waves of tiles x slices. Measured (profiles/gemm_mid_r06.jsonl, r6m rows)
     and picked: 1024^3 f32m64 x1 (0.023 ms, 0.88x hipBLASLt), 2048^3 f32m64 x1 (0.141, 1.10x; the
-    128-tile form ties), 3072^3 f32m64 x1 (0.470, 1.04x), 4096^3 f32t x1 (0.977, 1.04x), 6144^3
-    f32s x1 (3.58, 1.17x)."""
+    128-tile form ties; now f32g2, below), 3072^3 f32m64 x1 (0.470, 1.04x), 4096^3 f32t x1 (0.977, 1.04x), 6144^3
+    f32s x1 (3.58, 1.17x). Where every 128-tile workgroup has its CU alone (tiles <= CUs, one K slice,
+    K a multiple of 32, up to 4096) the form with one barrier per PAIR of 16-k stages ("f32g2", rate fitted to
+    2048^3: 0.135 ms = 1.03x hipBLASLt vs 0.144 for f32m64, gemm_mid_r06.jsonl r6v2 rows; 2-3 % slower
+    than the per-stage form once two workgroups share a CU, so only there)."""
     from ... import ops
 
     ncu = ops.num_cus(torch.device("cuda", torch.cuda.current_device())) if torch.cuda.is_available() else 256
@@ -159,7 +162,9 @@ def _native_plan(M: int, N: int, K: int):
             continue
         extra = 0.0 if s == 1 else (s + 1) * M * N * 4 / 4e12 / unit + 5e-6 / unit
         for kern, tiles, slots, o, rate in (("f32t", t256, ncu, 256, 1.0), ("f32s", t128, 2 * ncu, 64, 0.92),
-                                            ("f32m64", t64, 2 * ncu, 64, 0.90)):
+                                            ("f32m64", t64, 2 * ncu, 64, 0.90), ("f32g2", t128, 2 * ncu, 64, 1.09)):
+            if kern == "f32g2" and (s > 1 or t128 > ncu or K % 32 or K > 4096):
+                continue      # the paired-barrier form: measured where a workgroup has its CU alone
             w = tiles * s / slots
             full, frac = int(w), w - int(w)
             if kern != "f32t" and 0 < frac <= 0.5:
@@ -217,9 +222,9 @@ def fgemm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
         # products whose 256 x 256 tiles do not fill the GPU: the hand-written kernel and K-slice
         # count of the measured cost model (_native_plan); the library only if neither applies
         kern, sl = _native_plan(a.shape[0], b.shape[1], a.shape[1])
-        if _GEMM_PLAN and kern in ("f32s", "f32m64"):
+        if _GEMM_PLAN and kern in ("f32s", "f32m64", "f32g2"):
             r = _kern.gemm_f32_small(a, b, out=out, alpha=alpha, accumulate=accumulate, slices=sl,
-                                     kernel="mid64" if kern == "f32m64" else None)
+                                     kernel={"f32m64": "mid64", "f32g2": "mid128g2"}.get(kern))
             if r is not None:
                 return r
         elif _GEMM_PLAN:

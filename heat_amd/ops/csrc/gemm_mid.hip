@@ -133,7 +133,9 @@ struct GmFrag {
 // NBUF = 4, the default); 4: 256 x 128 tiles (waves of 128 x 64: 0.75 LDS floats per MFMA instead
 // of 1, 43 instead of 32 flop per staged byte; NBUF = 3, 72 KB; measured slower - A/B only). Two
 // workgroups per CU either way.
-template <bool AK, bool BK_, int WMB, int NBUF, int WNB = 2>
+// GSZ = 2 (A/B): stages in pairs under ONE barrier (a 32-deep K slice per barrier): the pair's
+// DMA lands during the previous pair, whose ring slots it then refills; K a whole number of pairs.
+template <bool AK, bool BK_, int WMB, int NBUF, int WNB = 2, int GSZ = 1>
 __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, int64_t M, int64_t N, int64_t K,
                                                     int64_t lda, int64_t ldb, int64_t ldc, float alpha, int beta,
@@ -331,6 +333,25 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
   };
 
   GmFrag<WMB, WNB> F0, F1;
+  if (GSZ == 2 && NBUF == 4 && !tail && nk % 2 == 0) {
+    stage(0, true);
+    stage(1, true);
+    for (int64_t t = 0; t < nk; t += 2) {
+      // stages t, t + 1 are this wave's only DMAs in flight: landed, and past the barrier every
+      // wave has landed its pieces and finished reading stages t - 2, t - 1 (the slots refilled now)
+      gm_wait_barrier<0>();
+      load(F0, t);
+      const bool more = t + 2 < nk;
+      if (more) stage(t + 2, true);
+      mma_half(F0, 0);
+      if (more) stage(t + 3, true);
+      load(F1, t + 1);
+      mma_half(F0, 1);
+      mma_half(F1, 0);
+      mma_half(F1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   for (int64_t t = 0; t < AHEAD && t < nk; ++t) stage(t, !(tail && t == nk - 1));
   if (nk > 0) {
     ready(0);
@@ -346,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
   for (; t < nk; t += 2) {
     step(t, F0, F1);
     if (t + 1 < nk) step(t + 1, F1, F0);
+  }
   }
 
   // epilogue: element (bm, bn, g) -> C[m0 + crow(bm, g)][n0 + ccol(bn)]
@@ -404,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32m(const float* __restrict__ A,
 template <bool AK, bool BK_>
 int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, float alpha, int beta, int64_t slices, int64_t cslice, int wide, hipStream_t s) {
-  const int64_t tm = wide == 1 ? 256 : wide == 2 ? 64 : MB, tnn = wide >= 2 ? 64 : MB;
+  const int64_t tm = wide == 1 ? 256 : wide == 2 ? 64 : MB, tnn = wide == 2 || wide == 3 ? 64 : MB;
   const int64_t tiles = ((M + tm - 1) / tm) * ((N + tnn - 1) / tnn);
   const int64_t nk = (K + MK - 1) / MK, kps = (nk + slices - 1) / slices;
   const int64_t ns = (nk + kps - 1) / kps;
@@ -416,6 +438,9 @@ int f32m_launch(const float* A, const float* B, float* C, int64_t M, int64_t N, 
   else if (wide == 3)
     hipLaunchKernelGGL((gemm_f32m<AK, BK_, 2, 4, 1>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps,
                        cslice);
+  else if (wide == 4)
+    hipLaunchKernelGGL((gemm_f32m<AK, BK_, 2, 4, 2, 2>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta,
+                       kps, cslice);
   else if (wide)
     hipLaunchKernelGGL((gemm_f32m<AK, BK_, 4, 3>), g, b, 0, s, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, kps, cslice);
   else
@@ -438,7 +463,7 @@ HA_EXPORT int64_t ha_gemm_f32m_slices(int64_t K, int64_t slices) {
 // a_kmajor: A element (m, k) at A[k lda + m] (else A[m lda + k]); b_kmajor: B element (k, n) at
 // B[k ldb + n] (else B[n ldb + k]). slices > 1: split-K over 16-k stages, slice y -> C + y cslice
 // (beta must be 0; the caller sums the partials). tile: 0 auto, 1 128 x 128, 2 256 x 128, 3 64 x 64,
-// 4 128 x 64 (A/B only: slower than the 128 x 128 or 64 x 64 form at every square and update shape,
+// 5 128 x 128 with a barrier per PAIR of 16-k stages (A/B), 4 128 x 64 (A/B only: slower than the 128 x 128 or 64 x 64 form at every square and update shape,
 // profiles/gemm_mid_r06.jsonl r6v rows).
 // Requirements (else HA_UNSUPPORTED): 16-byte
 // aligned A and B, lda and ldb multiples of 4, the contiguous extent of each operand (K for a
@@ -456,7 +481,7 @@ HA_EXPORT int ha_gemm_f32m(const float* A, const float* B, float* C, int64_t M, 
   // measured slower on every shape (71 vs 84 % MFMA-busy at 6144^3, update 25.2 vs 23.3 ms;
   // profiles/gemm_mid_r06.jsonl, r6j rows): an A/B form only
   static const int wide_env = getenv("HEAT_GM_WIDE") ? atoi(getenv("HEAT_GM_WIDE")) : 0;
-  const int wide = tile == 4 ? 3 : tile == 3 ? 2 : tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
+  const int wide = tile == 5 ? 4 : tile == 4 ? 3 : tile == 3 ? 2 : tile == 2 ? 1 : tile == 1 ? 0 : wide_env;
 #define HA_F32M(AK, BK) return f32m_launch<AK, BK>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, slices, cslice, wide, s)
   if (a_kmajor) {
     if (b_kmajor) HA_F32M(true, true);

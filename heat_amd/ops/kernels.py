@@ -1241,7 +1241,7 @@ def gemm_f32_small(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]
         kernel = "mid64"   # short K: per-tile latency dominates, more (smaller) tiles per CU hide it
     kernel = kernel or ("mid" if _GEMM_MID else "s")
     mid = kernel.startswith("mid")
-    tile = {"mid128": 1, "mid256": 2, "mid64": 3, "mid128x64": 4}.get(kernel, 0)
+    tile = {"mid128": 1, "mid256": 2, "mid64": 3, "mid128x64": 4, "mid128g2": 5}.get(kernel, 0)
     if mid and ((M if a_km else K) % 4 or (N if not b_nm else K) % 4 or min(M, N, K) < 4):
         mid = False          # gemm_f32m's operand requirements (contiguous extents multiples of 4)
     if mid:

@@ -281,7 +281,7 @@ def test_matmul_gram_and_cov_route_to_upper_tiles(gpu):
                                    (132, 4, 136), (2000, 36, 4), (5000, 256, 700), (128, 20000, 256), (300, 260, 132),
                                    (4100, 128, 100), (1000, 52, 516), (2052, 1028, 260)])
 @pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
-@pytest.mark.parametrize("kernel", ["mid128", "mid256", "mid64", "mid128x64", "s"])
+@pytest.mark.parametrize("kernel", ["mid128", "mid256", "mid64", "mid128x64", "mid128g2", "s"])
 def test_gemm_f32_small_layouts(m, k, n, layout, kernel):
     """128-tile split-K kernels (LDS-DMA gemm_f32m and register-staged gemm_f32s): every operand
     layout, edges, K tails, split-K, alpha / accumulate."""
@@ -340,7 +340,7 @@ def test_gemm_f32_mid_auto_tile(m, k, n, layout):
 
 
 @pytest.mark.parametrize("m,n,k", [(20000, 3840, 256), (4096, 768, 32), (9000, 300, 256)])
-@pytest.mark.parametrize("kernel", ["mid128", "mid256", "mid64", "mid128x64"])
+@pytest.mark.parametrize("kernel", ["mid128", "mid256", "mid64", "mid128x64", "mid128g2"])
 def test_gemm_f32_mid_update_shape(m, n, k, kernel):
     """The Householder trailing-update form C[:, j:] -= V X on the LDS-DMA 128-tile kernel (C a
     column slice of a row-major matrix, V row-major, X k-major) against fp64."""
@@ -372,7 +372,7 @@ def test_fgemm_native_plan_products(m, k, n):
     b = torch.randn(k, n, generator=g).to(dev)
     assert basics._library_better(m, n, k, True)
     kern, sl = basics._native_plan(m, n, k)
-    assert kern in ("f32t", "f32s", "f32m64") and sl >= 1
+    assert kern in ("f32t", "f32s", "f32m64", "f32g2") and sl >= 1
     c = basics.fgemm(a, b)
     ref = a.double() @ b.double()
     assert torch.all((c.double() - ref).abs() <= _bound(a, b)), (kern, sl, (c.double() - ref).abs().max())

@@ -53,6 +53,7 @@ def main():
             t_w, s_w = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid256"), sl, reps)
             t_6, s_6 = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid64"), sl[:4], reps)
             t_x, s_x = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid128x64"), sl[:4], reps)
+            t_g, s_g = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="mid128g2"), sl, reps)
             t_s, s_s = best(lambda s: K.gemm_f32_small(a, b, slices=s, kernel="s"), sl, reps)
             t_t, s_t = best(lambda s: K.gemm_f32(a, b, slices=s), sl, reps)
             from heat_amd.core.linalg import basics
@@ -64,6 +65,8 @@ def main():
                               "f32m256_vs_lib": round(t_w / t_lib, 3), "f32m64_ms": round(t_6, 4), "f32m64_slices": s_6,
                               "f32m64_vs_lib": round(t_6 / t_lib, 3), "f32m128x64_ms": round(t_x, 4),
                               "f32m128x64_slices": s_x, "f32m128x64_vs_lib": round(t_x / t_lib, 3),
+                              "f32m128g2_ms": round(t_g, 4), "f32m128g2_slices": s_g,
+                              "f32m128g2_vs_lib": round(t_g / t_lib, 3), "f32m128g2_vs_f32m": round(t_g / t_m, 3),
                               "f32s_ms": round(t_s, 4), "f32s_slices": s_s,
                               "f32t_ms": round(t_t, 4), "f32t_slices": s_t, "f32m_vs_lib": round(t_m / t_lib, 3),
                               "f32s_vs_lib": round(t_s / t_lib, 3), "plan": list(plan), "plan_ms": round(t_p, 4),
@@ -87,6 +90,7 @@ def main():
             t_w = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid256"), 5)
             t_6 = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid64"), 5)
             t_x = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid128x64"), 5)
+            t_g = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="mid128g2"), 5)
             t_s = timed(lambda: K.gemm_f32_small(V, X, out=C, accumulate=True, alpha=-1.0, kernel="s"), 5)
             t_t = timed(lambda: K.gemm_f32(V, X, out=C, accumulate=True, alpha=-1.0), 5)
             fl = 2.0 * m * N * Kd
@@ -94,7 +98,9 @@ def main():
                               "f32m_ms": round(t_m, 3), "f32m256_ms": round(t_w, 3),
                               "f32m256_vs_lib": round(t_w / t_lib, 3), "f32m64_ms": round(t_6, 3),
                               "f32m64_vs_lib": round(t_6 / t_lib, 3), "f32m128x64_ms": round(t_x, 3),
-                              "f32m128x64_vs_lib": round(t_x / t_lib, 3), "f32s_ms": round(t_s, 3), "f32t_ms": round(t_t, 3),
+                              "f32m128x64_vs_lib": round(t_x / t_lib, 3), "f32m128g2_ms": round(t_g, 3),
+                              "f32m128g2_vs_lib": round(t_g / t_lib, 3), "f32m128g2_vs_f32m": round(t_g / t_m, 3),
+                              "f32s_ms": round(t_s, 3), "f32t_ms": round(t_t, 3),
                               "f32m_vs_lib": round(t_m / t_lib, 3), "hipblaslt_tf": round(fl / t_lib / 1e9, 1),
                               "f32m_tf": round(fl / t_m / 1e9, 1), "f32m_max_abs_err_4096rows": err}), flush=True)
             del V, X, ref
