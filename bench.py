@@ -406,7 +406,7 @@ def comm_ab_isolated(comm, sizes) -> dict:
     res = {}
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True,
-                           timeout=float(os.environ.get("HEAT_BENCH_AB_TIMEOUT", "180")))
+                           timeout=float(os.environ.get("HEAT_BENCH_AB_TIMEOUT", "120")))
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         if lines:
             res = json.loads(lines[-1])
