@@ -506,7 +506,8 @@ HA_EXPORT int ha_h1_topk(const void* planes, const float* sx, int64_t n, int f, 
     /* 8 waves x 32 points, one barrier per 4 chunks (8-slot ring, 136 KB): every staged chunk feeds 256 */        \
     /* points (half the DMA instructions and L2 reads per point) and a quarter of the barriers: 277-279 */        \
     /* vs 295-298 ms (round-5 form, HEAT_H1_CFG=o); a barrier per pair (p) 282-283. f = 64: 189-191 vs */      \
-    /* 191-192 ms (f = 32 / 16 have fewer image pieces per chunk than 8 waves) */                              \
+    /* 191-192 ms (f = 32 / 16 have fewer image pieces per chunk than 8 waves). 12-entry half lists */         \
+    /* (fewer queued candidates) re-check 2 % of the queries instead of 0.05 %: 284 vs 279 ms */               \
     constexpr int TPB = FP >= 32 ? 2 : 4;                                                                        \
     constexpr int PAIR = TPB == 2 ? 2 : 1;                                                                       \
     if (FP == 128 && cfg_a && kp == 32) {                                                                        \
